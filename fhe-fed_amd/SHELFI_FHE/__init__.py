@@ -1,0 +1,235 @@
+"""SHELFI_FHE — MI355X-native drop-in for the reference's pybind11 module.
+
+Mirrors palisade_pybind/SHELFI_FHE/src/binding.cpp:14-49 (module ``SHELFI_FHE``,
+``class Scheme``, ``class CKKS(Scheme)``, ``__version__``) so that
+``import SHELFI_FHE as m; m.CKKS("ckks", 4096, 52, dir)`` in code/benchmark*.py
+keeps working.  Compute runs in libshelfi.so (HIP kernels for gfx950) through
+the C ABI in include/shelfi.h; nothing here computes on the CPU.
+
+Extensions over the reference (keyword-only, defaults reproduce it):
+``multDepth`` (L = multDepth + 1 towers; reference fixes 1, ckks.cpp:26),
+``firstModBits`` (60), ``ringDim`` (0 = PALISADE's choice), ``device``
+(HIP ordinal; default LOCAL_RANK or 0), and ``seed`` (deterministic encryption
+randomness for parity tests; 0 = OS entropy).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, List, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import ShelfiError, check
+
+__version__ = "0.1.0"
+__all__ = ["Scheme", "CKKS", "ShelfiError", "__version__"]
+
+
+class Scheme:
+    """binding.cpp:16 ``py::class_<Scheme>`` — opaque base of the scheme plugins
+    (include/scheme.h:15-32)."""
+
+    def __init__(self, scheme: str = "ckks"):
+        self._scheme = scheme
+
+
+def _default_device() -> int:
+    for var in ("SHELFI_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None and v.strip().lstrip("-").isdigit():
+            return int(v)
+    return 0
+
+
+def _as_bytes_list(learner_data) -> List[bytes]:
+    out = []
+    for item in learner_data:
+        if isinstance(item, (bytes, bytearray, memoryview)):
+            out.append(bytes(item) if not isinstance(item, bytes) else item)
+        elif isinstance(item, str):
+            # ckks.cpp:276 reads each learner through py::str; a str holding the
+            # raw bytes (latin-1) round-trips the same way
+            out.append(item.encode("latin-1"))
+        else:
+            raise TypeError("learner_data items must be bytes")
+    return out
+
+
+class CKKS(Scheme):
+    """binding.cpp:18-31 — ``CKKS(scheme="ckks", batchSize=4096, scaleFactorBits=52,
+    cryptodir="../resources/cryptoparams/")`` (ckks.cpp:5-9)."""
+
+    def __init__(self, scheme: str = "ckks", batchSize: int = 4096, scaleFactorBits: int = 52,
+                 cryptodir: str = "../resources/cryptoparams/", *, multDepth: int = 1,
+                 firstModBits: int = 60, ringDim: int = 0, device: int | None = None,
+                 seed: int = 0):
+        super().__init__(scheme)
+        if scheme.lower() != "ckks":
+            raise ValueError("only the 'ckks' scheme is implemented")
+        self.batchSize = int(batchSize)
+        self.scaleFactorBits = int(scaleFactorBits)
+        self.cryptodir = str(cryptodir)
+        self._lib = _lib.load()
+        self._ctx = C.c_void_p()
+        dev = _default_device() if device is None else int(device)
+        check(self._lib.shelfi_ctx_create(int(ringDim), int(multDepth) + 1, self.scaleFactorBits,
+                                          int(firstModBits), self.batchSize, dev,
+                                          C.byref(self._ctx)), "CKKS()")
+        if seed:
+            check(self._lib.shelfi_set_seed(self._ctx, int(seed)))
+
+    # ------------------------------------------------------------ lifecycle --
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self._lib.shelfi_ctx_destroy(ctx)
+            except Exception:
+                pass
+            self._ctx = C.c_void_p()
+
+    def info(self) -> dict:
+        inf = _lib.Info()
+        check(self._lib.shelfi_ctx_info(self._ctx, C.byref(inf)))
+        L = inf.num_towers
+        return {"ring_dim": inf.ring_dim, "num_towers": L, "batch": inf.batch,
+                "scale_bits": inf.scale_bits, "first_mod_bits": inf.first_mod_bits,
+                "device": inf.device, "moduli": [int(inf.moduli[i]) for i in range(L)],
+                "roots": [int(inf.roots[i]) for i in range(L)], "delta": inf.delta,
+                "key_id": int(inf.key_id), "keys_loaded": bool(inf.keys_loaded),
+                "palisade_keys": bool(inf.palisade_keys)}
+
+    @property
+    def ctx_handle(self) -> int:
+        return self._ctx.value
+
+    def set_seed(self, seed: int) -> None:
+        check(self._lib.shelfi_set_seed(self._ctx, int(seed)))
+
+    # ---------------------------------------------------------- keys (a2/a3) --
+    def loadCryptoParams(self) -> None:
+        """ckks.cpp:11-23: failures are printed, never raised."""
+        rc = self._lib.shelfi_load(self._ctx, self.cryptodir.encode())
+        if rc != 0:
+            print("Could not read serialization from %scryptocontext.txt: %s"
+                  % (self.cryptodir, self._lib.shelfi_last_error().decode(errors="replace")))
+
+    def genCryptoContextAndKeyGen(self) -> int:
+        """ckks.cpp:25-59: returns 1 on success, 0 on a file-write error."""
+        rc = self._lib.shelfi_keygen(self._ctx, self.cryptodir.encode())
+        if rc == _lib.SHELFI_ERR_IO:
+            print("Error writing serialization: %s"
+                  % self._lib.shelfi_last_error().decode(errors="replace"))
+            return 0
+        check(rc, "genCryptoContextAndKeyGen")
+        return 1
+
+    def set_keys(self, pk: np.ndarray, sk: np.ndarray) -> None:
+        pk = np.ascontiguousarray(pk, dtype=np.uint64)
+        sk = np.ascontiguousarray(sk, dtype=np.uint64)
+        inf = self.info()
+        L, N = inf["num_towers"], inf["ring_dim"]
+        if pk.size != 2 * L * N or sk.size != L * N:
+            raise ValueError("key shapes must be [2][L][N] and [L][N]")
+        check(self._lib.shelfi_set_keys(self._ctx, pk.ctypes.data_as(_lib.u64p),
+                                        sk.ctypes.data_as(_lib.u64p)))
+
+    def get_keys(self):
+        inf = self.info()
+        L, N = inf["num_towers"], inf["ring_dim"]
+        pk = np.zeros((2, L, N), np.uint64)
+        sk = np.zeros((L, N), np.uint64)
+        check(self._lib.shelfi_get_keys(self._ctx, pk.ctypes.data_as(_lib.u64p),
+                                        sk.ctypes.data_as(_lib.u64p)))
+        return pk, sk
+
+    # ------------------------------------------------------------ hot path --
+    def _take(self, ptr: "_lib.u8p", n: int) -> bytes:
+        try:
+            return C.string_at(ptr, n)
+        finally:
+            self._lib.shelfi_free(ptr)
+
+    def encrypt(self, data_array) -> bytes:
+        """ckks.cpp:61-104 (py::array_t<double> forcecast: float32 is widened)."""
+        x = np.ascontiguousarray(np.asarray(data_array, dtype=np.float64).reshape(-1))
+        out = _lib.u8p()
+        n_out = C.c_size_t()
+        check(self._lib.shelfi_encrypt(self._ctx, x.ctypes.data_as(_lib.f64p), x.size,
+                                       C.byref(out), C.byref(n_out)), "encrypt")
+        return self._take(out, n_out.value)
+
+    def computeWeightedAverage(self, learner_data, scaling_factors) -> bytes:
+        """ckks.cpp:264-320.  Length mismatch prints and returns b"" (:265-268);
+        weights are narrowed to float32 (:287)."""
+        learner_data = list(learner_data)
+        scaling_factors = list(scaling_factors)
+        if len(learner_data) != len(scaling_factors):
+            print("Error: learner_data and scaling_factors size mismatch")
+            return b""
+        blobs = _as_bytes_list(learner_data)
+        C_ = len(blobs)
+        if C_ == 0:
+            raise ValueError("computeWeightedAverage: no learners")
+        w = np.asarray([float(s) for s in scaling_factors], dtype=np.float32)
+        arr = (_lib.u8p * C_)()
+        lens = (C.c_size_t * C_)()
+        for i, b in enumerate(blobs):
+            arr[i] = C.cast(C.c_char_p(b), _lib.u8p)
+            lens[i] = len(b)
+        out = _lib.u8p()
+        n_out = C.c_size_t()
+        check(self._lib.shelfi_weighted_average(self._ctx, arr, lens, w.ctypes.data_as(_lib.f32p),
+                                                C_, C.byref(out), C.byref(n_out)),
+              "computeWeightedAverage")
+        return self._take(out, n_out.value)
+
+    def decrypt(self, learner_data, data_dimensions: int) -> np.ndarray:
+        """ckks.cpp:170-213 -> float64[data_dimensions]."""
+        if isinstance(learner_data, str):
+            learner_data = learner_data.encode("latin-1")
+        b = bytes(learner_data)
+        n = int(data_dimensions)
+        out = np.zeros(n, np.float64)
+        check(self._lib.shelfi_decrypt(self._ctx, C.cast(C.c_char_p(b), _lib.u8p), len(b), n,
+                                       out.ctypes.data_as(_lib.f64p)), "decrypt")
+        return out
+
+    # binding.cpp:27,29,31 register the *_cpp names on the same methods
+    encrypt_cpp = encrypt
+    decrypt_cpp = decrypt
+    computeWeightedAverage_cpp = computeWeightedAverage
+
+
+def params_generate(batchSize: int = 4096, scaleFactorBits: int = 52, multDepth: int = 1,
+                    firstModBits: int = 60, ringDim: int = 0):
+    """Host-only: the (N, q[], psi[]) chain CKKS(...) would use (no device needed)."""
+    lib = _lib.load()
+    L = multDepth + 1
+    q = (C.c_uint64 * L)()
+    psi = (C.c_uint64 * L)()
+    N = C.c_uint32()
+    check(lib.shelfi_params_generate(ringDim, L, scaleFactorBits, firstModBits, batchSize,
+                                     C.byref(N), q, psi), "params_generate")
+    return int(N.value), [int(x) for x in q], [int(x) for x in psi]
+
+
+def blob_info(blob: bytes) -> dict:
+    lib = _lib.load()
+    k = C.c_uint64()
+    d = C.c_uint32()
+    s = C.c_double()
+    kid = C.c_uint64()
+    check(lib.shelfi_blob_info(C.cast(C.c_char_p(blob), _lib.u8p), len(blob), C.byref(k),
+                               C.byref(d), C.byref(s), C.byref(kid)), "blob_info")
+    return {"num_cts": int(k.value), "depth": int(d.value), "scale": float(s.value),
+            "key_id": int(kid.value)}
+
+
+def blob_residues(blob: bytes, ring_dim: int, num_towers: int) -> np.ndarray:
+    """View of a blob's payload as [K][2][L][N] uint64 (host)."""
+    hdr = _lib.load().shelfi_blob_header_bytes()
+    arr = np.frombuffer(blob, dtype="<u8", offset=hdr)
+    return arr.reshape(-1, 2, num_towers, ring_dim)

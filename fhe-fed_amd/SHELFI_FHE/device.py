@@ -1,0 +1,130 @@
+"""Device-resident batch API over torch tensors (HBM in, HBM out).
+
+PyTorch is used only as plumbing — HBM allocation, the current HIP stream and
+torch.distributed (RCCL over xGMI) — while every arithmetic step is a libshelfi
+kernel launched on torch's current stream.  Ciphertext batches are uint64 data
+in the [K][2][L][N] layout (stored in int64 tensors: torch has no full uint64
+arithmetic, and none is done on them here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+from . import _lib
+from ._lib import check
+
+
+def _torch():
+    import torch  # deferred: the bytes API does not need torch
+
+    return torch
+
+
+def _stream_ptr(tensor) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(tensor.device).cuda_stream
+
+
+def ct_shape(ckks, K: int):
+    inf = ckks.info()
+    return (K, 2, inf["num_towers"], inf["ring_dim"])
+
+
+def empty_ct(ckks, K: int, device=None):
+    torch = _torch()
+    if device is None:
+        device = "cuda:%d" % ckks.info()["device"]
+    return torch.empty(ct_shape(ckks, K), dtype=torch.int64, device=device)
+
+
+def _check_ct(t, ckks, K=None):
+    inf = ckks.info()
+    if not t.is_cuda or not t.is_contiguous() or t.element_size() != 8:
+        raise ValueError("ciphertext tensors must be contiguous 64-bit CUDA tensors")
+    if t.dim() != 4 or t.shape[1] != 2 or t.shape[2] != inf["num_towers"] or t.shape[3] != inf["ring_dim"]:
+        raise ValueError("ciphertext tensor must have shape [K][2][L][N] = [K][2][%d][%d]"
+                         % (inf["num_towers"], inf["ring_dim"]))
+    if K is not None and t.shape[0] != K:
+        raise ValueError("ciphertext tensors hold different numbers of ciphertexts")
+
+
+def wavg(ckks, cts: Sequence, weights: Sequence[float], out=None):
+    """sum_c W_c * cts[c] (EvalMult by (float)w_c + EvalAdd), fully on device."""
+    torch = _torch()
+    cts = list(cts)
+    if len(cts) != len(weights) or not cts:
+        raise ValueError("need one weight per learner and at least one learner")
+    K = cts[0].shape[0]
+    for t in cts:
+        _check_ct(t, ckks, K)
+    if out is None:
+        out = torch.empty_like(cts[0])
+    _check_ct(out, ckks, K)
+    ptrs = (C.c_void_p * len(cts))(*[t.data_ptr() for t in cts])
+    w = (C.c_float * len(cts))(*[float(x) for x in weights])
+    check(_lib.load().shelfi_dev_wavg(ckks._ctx, ptrs, w, len(cts), K, C.c_void_p(out.data_ptr()),
+                                      C.c_void_p(_stream_ptr(out))), "dev_wavg")
+    return out
+
+
+def modq(ckks, buf):
+    """Fold a collective's uint64 sum of <= 15 partial sums back into [0, q_t)."""
+    _check_ct(buf, ckks)
+    check(_lib.load().shelfi_dev_modq(ckks._ctx, C.c_void_p(buf.data_ptr()), buf.shape[0],
+                                      C.c_void_p(_stream_ptr(buf))), "dev_modq")
+    return buf
+
+
+def encrypt(ckks, x, out=None):
+    """encode + encrypt a float64 CUDA vector into ceil(n / batch) ciphertexts."""
+    torch = _torch()
+    if not x.is_cuda or x.dtype != torch.float64:
+        raise ValueError("x must be a float64 CUDA tensor")
+    x = x.contiguous().view(-1)
+    B = ckks.info()["batch"]
+    K = (x.numel() + B - 1) // B
+    if out is None:
+        out = empty_ct(ckks, K, x.device)
+    _check_ct(out, ckks, K)
+    check(_lib.load().shelfi_dev_encrypt(ckks._ctx, C.c_void_p(x.data_ptr()), x.numel(),
+                                         C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(x))),
+          "dev_encrypt")
+    return out
+
+
+def decrypt(ckks, ct, n: int, scale: float, out=None):
+    """decrypt + decode K ciphertexts of scaling factor `scale` into n float64 values."""
+    torch = _torch()
+    _check_ct(ct, ckks)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=ct.device)
+    check(_lib.load().shelfi_dev_decrypt(ckks._ctx, C.c_void_p(ct.data_ptr()), ct.shape[0],
+                                         float(scale), int(n), C.c_void_p(out.data_ptr()),
+                                         C.c_void_p(_stream_ptr(ct))), "dev_decrypt")
+    return out
+
+
+def ntt(ckks, polys, inverse: bool = False):
+    """In-place negacyclic NTT (PALISADE order) of [P][N] polys; tower = p % L."""
+    inf = ckks.info()
+    if not polys.is_cuda or not polys.is_contiguous() or polys.shape[-1] != inf["ring_dim"]:
+        raise ValueError("polys must be a contiguous CUDA tensor [P][N]")
+    P = polys.numel() // inf["ring_dim"]
+    check(_lib.load().shelfi_dev_ntt(ckks._ctx, C.c_void_p(polys.data_ptr()), P, 1 if inverse else 0,
+                                     C.c_void_p(_stream_ptr(polys))), "dev_ntt")
+    return polys
+
+
+def from_bytes(ckks, blob: bytes, device=None):
+    """Blob payload -> device ciphertext tensor (one H2D copy)."""
+    import numpy as np
+
+    from . import blob_residues
+
+    torch = _torch()
+    inf = ckks.info()
+    arr = blob_residues(blob, inf["ring_dim"], inf["num_towers"]).view(np.int64)
+    if device is None:
+        device = "cuda:%d" % inf["device"]
+    return torch.from_numpy(arr.copy()).to(device)

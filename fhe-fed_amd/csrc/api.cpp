@@ -1,0 +1,985 @@
+// api.cpp — the C ABI (include/shelfi.h) over the HIP kernels.
+//
+// Mirrors the reference's CKKS scheme wrapper, palisade_pybind/SHELFI_FHE/src/ckks.cpp:
+//   shelfi_ctx_create        <- CKKS::CKKS                      (ckks.cpp:5-9)
+//   shelfi_load              <- CKKS::loadCryptoParams          (ckks.cpp:11-23)
+//   shelfi_keygen            <- CKKS::genCryptoContextAndKeyGen (ckks.cpp:25-59)
+//   shelfi_encrypt           <- CKKS::encrypt                   (ckks.cpp:61-104)
+//   shelfi_decrypt           <- CKKS::decrypt                   (ckks.cpp:170-213)
+//   shelfi_weighted_average  <- CKKS::computeWeightedAverage    (ckks.cpp:264-320)
+// Host code here only validates, moves bytes and precomputes constant tables; every
+// per-ciphertext operation is a kernel in kernels.hip.
+#include <sys/random.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <new>
+
+#include "palisade_io.h"
+#include "shelfi_internal.h"
+
+using namespace shelfi;
+
+namespace shelfi {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+// ------------------------------------------------------------ blob format ----
+// 64-byte little-endian header followed by K x 2 x L x N uint64 residues in the
+// device layout [ct][poly][tower][coeff] (EVALUATION, PALISADE bit-reversed order).
+struct BlobHeader {
+  char magic[4];           // "SHCT"
+  uint16_t version;        // 1
+  uint16_t header_bytes;   // 64
+  uint32_t logN;
+  uint32_t L;
+  uint64_t K;              // ciphertexts in the blob
+  uint32_t depth;          // PALISADE depth (1 fresh, 2 after EvalMult by constant)
+  uint32_t level;          // always 0 (no rescale on this path)
+  double scale;            // scaling factor (Delta for fresh, Delta^2 after EvalMult)
+  uint64_t params_id;      // hash of (N, L, q)
+  uint64_t key_id;         // hash of the public key (PALISADE keyTag analogue)
+  uint32_t batch;          // slots per ciphertext
+  uint32_t encoding;       // 4 = CKKSPacked (PALISADE PlaintextEncodings)
+};
+static_assert(sizeof(BlobHeader) == 64, "blob header must be 64 bytes");
+
+static uint64_t compute_params_id(const Params& p) {
+  uint64_t h = fnv1a(&p.N, sizeof(p.N));
+  h = fnv1a(&p.L, sizeof(p.L), h);
+  return fnv1a(p.q, sizeof(uint64_t) * p.L, h);
+}
+
+static BlobHeader parse_blob(const uint8_t* blob, size_t len, const shelfi_ctx* ctx) {
+  if (!blob || len < sizeof(BlobHeader)) throw Error{SHELFI_ERR_FORMAT, "ciphertext blob too short"};
+  BlobHeader h;
+  std::memcpy(&h, blob, sizeof(h));
+  if (std::memcmp(h.magic, "SHCT", 4) != 0 || h.version != 1 || h.header_bytes != 64)
+    throw Error{SHELFI_ERR_FORMAT, "not a SHELFI ciphertext blob (bad magic/version)"};
+  if (h.L == 0 || h.L > kMaxTowers || h.logN < 10 || h.logN > 17)
+    throw Error{SHELFI_ERR_FORMAT, "corrupt ciphertext blob header"};
+  const uint64_t need = sizeof(BlobHeader) + h.K * 2ull * h.L * (8ull << h.logN);
+  if (len != need) throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
+  if (ctx) {
+    if (h.logN != ctx->p.logN || h.L != ctx->p.L || h.params_id != ctx->params_id)
+      throw Error{SHELFI_ERR_FORMAT, "ciphertext was produced under different crypto parameters"};
+  }
+  return h;
+}
+
+// -------------------------------------------------------------- helpers ----
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    SHELFI_HIP(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+static std::mutex& ctx_mutex(const shelfi_ctx* ctx) {
+  // one mutex per context, kept in a side table to keep shelfi_ctx POD-like
+  static std::mutex table_mu;
+  static std::vector<std::pair<const shelfi_ctx*, std::mutex*>> table;
+  std::lock_guard<std::mutex> g(table_mu);
+  for (auto& e : table)
+    if (e.first == ctx) return *e.second;
+  table.emplace_back(ctx, new std::mutex());
+  return *table.back().second;
+}
+
+template <class F>
+static int guarded(F&& f) {
+  try {
+    f();
+    return SHELFI_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host out of memory");
+    return SHELFI_ERR_DEVICE;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return SHELFI_ERR_DEVICE;
+  }
+}
+
+static void dfree(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <class T>
+static void dfree_t(T*& p) {
+  void* v = p;
+  dfree(v);
+  p = nullptr;
+}
+
+static void* ensure(void*& buf, size_t& cap, size_t bytes) {
+  if (bytes <= cap && buf) return buf;
+  dfree(buf);
+  cap = 0;
+  size_t want = bytes < 64 ? 64 : bytes;
+  SHELFI_HIP(hipMalloc(&buf, want));
+  cap = want;
+  return buf;
+}
+
+static void seed_to_key(uint64_t seed, uint32_t key[8]) {
+  uint64_t st = seed;
+  for (int i = 0; i < 4; ++i) {
+    uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    key[2 * i] = (uint32_t)z;
+    key[2 * i + 1] = (uint32_t)(z >> 32);
+  }
+}
+
+static void os_random(void* buf, size_t n) {
+  uint8_t* p = (uint8_t*)buf;
+  while (n) {
+    ssize_t r = getrandom(p, n, 0);
+    if (r < 0) throw Error{SHELFI_ERR_DEVICE, "getrandom() failed"};
+    p += r;
+    n -= (size_t)r;
+  }
+}
+
+// encryption/keygen stream key + first ciphertext index for this call
+static void draw_key(shelfi_ctx* ctx, uint64_t count, uint32_t key[8], uint64_t* g0) {
+  if (ctx->seed) {
+    seed_to_key(ctx->seed, key);
+    *g0 = ctx->enc_counter;
+    ctx->enc_counter += count;
+  } else {
+    os_random(key, 32);
+    *g0 = 0;
+  }
+}
+
+// ------------------------------------------------------- tables / params ----
+static void validate_params(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
+                            uint32_t batch) {
+  if (L < 1 || L > (uint32_t)kMaxTowers) throw Error{SHELFI_ERR_ARG, "num_towers must be in [1,16]"};
+  if (N < 1024 || N > (1u << 17) || (N & (N - 1)))
+    throw Error{SHELFI_ERR_ARG, "ring dimension must be a power of two in [2^10, 2^17]"};
+  if (!batch || (batch & (batch - 1)) || 2ull * batch > N)
+    throw Error{SHELFI_ERR_ARG, "batchSize must be a power of two with 2*batchSize <= ring dimension"};
+  if (scale_bits < 10 || scale_bits > 58)
+    throw Error{SHELFI_ERR_ARG, "scaleFactorBits must be in [10, 58]"};
+  if (first_mod_bits < scale_bits || first_mod_bits > 60)
+    throw Error{SHELFI_ERR_ARG, "firstModBits must be in [scaleFactorBits, 60]"};
+}
+
+static void free_tables(shelfi_ctx* ctx) {
+  dfree_t(ctx->dt.tc);
+  dfree_t(ctx->dt.psi_rev);
+  dfree_t(ctx->dt.psi_rev_sh);
+  dfree_t(ctx->dt.ipsi_rev);
+  dfree_t(ctx->dt.ipsi_rev_sh);
+  dfree_t(ctx->dt.fft_inv);
+  dfree_t(ctx->dt.fft_fwd);
+  dfree_t(ctx->dt.cdt);
+}
+
+static void free_keys(shelfi_ctx* ctx) {
+  dfree_t(ctx->dk.pk);
+  dfree_t(ctx->dk.pk_sh);
+  dfree_t(ctx->dk.sk);
+  dfree_t(ctx->dk.sk_sh);
+  ctx->keys_loaded = false;
+  ctx->key_id = 0;
+  ctx->pk_host.clear();
+  ctx->sk_host.clear();
+}
+
+template <class T>
+static T* upload(const T* host, size_t count) {
+  void* d = nullptr;
+  SHELFI_HIP(hipMalloc(&d, sizeof(T) * (count ? count : 1)));
+  SHELFI_HIP(hipMemcpy(d, host, sizeof(T) * count, hipMemcpyHostToDevice));
+  return (T*)d;
+}
+
+static uint32_t bitrev_host(uint32_t x, uint32_t bits) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < bits; ++i) r = (r << 1) | ((x >> i) & 1);
+  return r;
+}
+
+// (Re)build every device table for ctx->p.
+static void build_tables(shelfi_ctx* ctx) {
+  free_tables(ctx);
+  Params& p = ctx->p;
+  const uint32_t N = p.N, L = p.L;
+  std::vector<TowerConst> tc(L);
+  std::vector<uint64_t> pr((size_t)L * N), prs((size_t)L * N), ipr((size_t)L * N), iprs((size_t)L * N);
+  u128 Q128 = 1;
+  for (uint32_t t = 0; t < L; ++t) Q128 *= p.q[t];  // Q mod 2^128
+  for (uint32_t t = 0; t < L; ++t) {
+    const uint64_t q = p.q[t];
+    TowerConst& c = tc[t];
+    std::memset(&c, 0, sizeof(c));
+    c.q = q;
+    c.one_shoup = (uint64_t)(((u128)1 << 64) / q);
+    c.r30 = (1ull << 30) % q;
+    c.r30_shoup = shoup(c.r30, q);
+    c.r60 = (1ull << 60) % q;
+    c.r60_shoup = shoup(c.r60, q);
+    c.r64 = (uint64_t)(((u128)1 << 64) % q);
+    c.r64_shoup = shoup(c.r64, q);
+    c.ninv = invmod(N % q, q);
+    c.ninv_shoup = shoup(c.ninv, q);
+    uint64_t qhat_mod = 1;
+    u128 qhat128 = 1;
+    for (uint32_t u = 0; u < L; ++u)
+      if (u != t) {
+        qhat_mod = (uint64_t)(((u128)qhat_mod * (p.q[u] % q)) % q);
+        qhat128 *= p.q[u];
+      }
+    c.qhat_inv = invmod(qhat_mod, q);
+    c.qhat_inv_shoup = shoup(c.qhat_inv, q);
+    c.qhat_lo = (uint64_t)qhat128;
+    c.qhat_hi = (uint64_t)(qhat128 >> 64);
+    c.inv_q = 1.0 / (double)q;
+    // twiddles: psi^bitrev(i), psi^-bitrev(i)
+    const uint64_t ipsi = invmod(p.psi[t], q);
+    uint64_t a = 1, b = 1;
+    for (uint32_t i = 0; i < N; ++i) {
+      const uint32_t r = bitrev_host(i, p.logN);
+      pr[(size_t)t * N + r] = a;
+      ipr[(size_t)t * N + r] = b;
+      a = (uint64_t)(((u128)a * p.psi[t]) % q);
+      b = (uint64_t)(((u128)b * ipsi) % q);
+    }
+    for (uint32_t i = 0; i < N; ++i) {
+      prs[(size_t)t * N + i] = shoup(pr[(size_t)t * N + i], q);
+      iprs[(size_t)t * N + i] = shoup(ipr[(size_t)t * N + i], q);
+    }
+  }
+  ctx->dt.qmod128_lo = (uint64_t)Q128;
+  ctx->dt.qmod128_hi = (uint64_t)(Q128 >> 64);
+  ctx->dt.tc = upload(tc.data(), L);
+  ctx->dt.psi_rev = upload(pr.data(), pr.size());
+  ctx->dt.psi_rev_sh = upload(prs.data(), prs.size());
+  ctx->dt.ipsi_rev = upload(ipr.data(), ipr.size());
+  ctx->dt.ipsi_rev_sh = upload(iprs.data(), iprs.size());
+  const uint32_t S = p.batch;
+  std::vector<double> ir(S), ii(S), fr(S), fi(S);
+  fft_twiddles(S, ir.data(), ii.data(), fr.data(), fi.data());
+  std::vector<double2> tinv(S), tfwd(S);
+  for (uint32_t i = 0; i < S; ++i) {
+    tinv[i] = make_double2(ir[i], ii[i]);
+    tfwd[i] = make_double2(fr[i], fi[i]);
+  }
+  ctx->dt.fft_inv = upload(tinv.data(), S);
+  ctx->dt.fft_fwd = upload(tfwd.data(), S);
+  uint64_t cdt[64];
+  ctx->dt.cdt_len = gauss_cdt(p.sigma, cdt, 64);
+  if (ctx->dt.cdt_len < 0) throw Error{SHELFI_ERR_ARG, "Gaussian table too large"};
+  ctx->dt.cdt = upload(cdt, (size_t)ctx->dt.cdt_len);
+  ctx->params_id = compute_params_id(p);
+}
+
+static void set_params(shelfi_ctx* ctx, uint32_t N, uint32_t L, uint32_t scale_bits,
+                       uint32_t first_mod_bits, uint32_t batch, const uint64_t* q,
+                       const uint64_t* psi) {
+  Params p;
+  p.N = N;
+  p.logN = (uint32_t)__builtin_ctz(N);
+  p.L = L;
+  p.batch = batch;
+  p.gap = N / (2 * batch);
+  p.scale_bits = scale_bits;
+  p.first_mod_bits = first_mod_bits;
+  for (uint32_t t = 0; t < L; ++t) {
+    if (q[t] >= (1ull << 60) || q[t] % (2ull * N) != 1)
+      throw Error{SHELFI_ERR_ARG, "modulus out of range (need q < 2^60, q = 1 mod 2N)"};
+    if (powmod(psi[t], N, q[t]) != q[t] - 1)
+      throw Error{SHELFI_ERR_ARG, "root of unity is not a primitive 2N-th root"};
+    p.q[t] = q[t];
+    p.psi[t] = psi[t];
+  }
+  // EXACTRESCALE level-0 scaling factor = (double)q_{L-1} (CT1.txt@265059).
+  p.delta = (double)q[L - 1];
+  ctx->p = p;
+  build_tables(ctx);
+}
+
+// keys: host copies -> device (+ Shoup companions)
+static void install_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk, bool palisade) {
+  const Params& p = ctx->p;
+  const size_t LN = (size_t)p.L * p.N;
+  for (size_t i = 0; i < 2 * LN; ++i)
+    if (pk[i] >= p.q[(i / p.N) % p.L]) throw Error{SHELFI_ERR_FORMAT, "public key residue >= q"};
+  for (size_t i = 0; i < LN; ++i)
+    if (sk[i] >= p.q[i / p.N]) throw Error{SHELFI_ERR_FORMAT, "secret key residue >= q"};
+  free_keys(ctx);
+  std::vector<uint64_t> pks(2 * LN), sks(LN);
+  for (size_t i = 0; i < 2 * LN; ++i) pks[i] = shoup(pk[i], p.q[(i / p.N) % p.L]);
+  for (size_t i = 0; i < LN; ++i) sks[i] = shoup(sk[i], p.q[i / p.N]);
+  ctx->dk.pk = upload(pk, 2 * LN);
+  ctx->dk.pk_sh = upload(pks.data(), 2 * LN);
+  ctx->dk.sk = upload(sk, LN);
+  ctx->dk.sk_sh = upload(sks.data(), LN);
+  ctx->pk_host.assign(pk, pk + 2 * LN);
+  ctx->sk_host.assign(sk, sk + LN);
+  ctx->key_id = fnv1a(pk, sizeof(uint64_t) * 2 * LN, ctx->params_id);
+  ctx->keys_loaded = true;
+  ctx->palisade_keys = palisade;
+}
+
+static void require_keys(const shelfi_ctx* ctx) {
+  if (!ctx->keys_loaded)
+    throw Error{SHELFI_ERR_STATE,
+                "no keys: call loadCryptoParams() or genCryptoContextAndKeyGen() first"};
+}
+
+// -------------------------------------------------- own key-file format ----
+// cryptocontext.txt: "SHCC" u32 version, u32 N, L, batch, scale_bits, first_mod_bits,
+//                    f64 sigma, u64 q[L], u64 psi[L]
+// key-public.txt:    "SHPK" u32 version, u64 params_id, u64 [2][L][N]
+// key-private.txt:   "SHSK" u32 version, u64 params_id, u64 [L][N]
+static void write_file(const std::string& path, const std::string& data) {
+  std::ofstream f(path, std::ios::binary | std::ios::trunc);
+  if (!f) throw Error{SHELFI_ERR_IO, "cannot open " + path + " for writing"};
+  f.write(data.data(), (std::streamsize)data.size());
+  if (!f) throw Error{SHELFI_ERR_IO, "error writing " + path};
+}
+static std::string read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error{SHELFI_ERR_IO, "could not read " + path};
+  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+template <class T>
+static void put(std::string& s, const T& v) {
+  s.append(reinterpret_cast<const char*>(&v), sizeof(T));
+}
+template <class T>
+static T get(const std::string& s, size_t& off) {
+  if (off + sizeof(T) > s.size()) throw Error{SHELFI_ERR_FORMAT, "truncated key file"};
+  T v;
+  std::memcpy(&v, s.data() + off, sizeof(T));
+  off += sizeof(T);
+  return v;
+}
+
+}  // namespace shelfi
+
+// ============================================================== C ABI ======
+extern "C" {
+
+int shelfi_abi_version(void) { return SHELFI_ABI_VERSION; }
+const char* shelfi_last_error(void) { return g_last_error.c_str(); }
+void shelfi_free(void* p) { std::free(p); }
+
+int shelfi_params_generate(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bits,
+                           uint32_t first_mod_bits, uint32_t batch, uint32_t* ring_dim_out,
+                           uint64_t* moduli_out, uint64_t* roots_out) {
+  return guarded([&] {
+    uint32_t N = ring_dim ? ring_dim
+                          : default_ring_dim(num_towers, scale_bits, first_mod_bits, batch);
+    if (!N) throw Error{SHELFI_ERR_ARG, "no ring dimension satisfies the security/batch constraints"};
+    validate_params(N, num_towers, scale_bits, first_mod_bits, batch);
+    uint64_t q[kMaxTowers], psi[kMaxTowers];
+    generate_chain(N, num_towers, scale_bits, first_mod_bits, q, psi);
+    if (ring_dim_out) *ring_dim_out = N;
+    for (uint32_t t = 0; t < num_towers; ++t) {
+      if (moduli_out) moduli_out[t] = q[t];
+      if (roots_out) roots_out[t] = psi[t];
+    }
+  });
+}
+
+int shelfi_read_palisade(const char* cryptodir, uint32_t* ring_dim, uint32_t* num_towers,
+                         uint64_t* moduli, uint64_t* roots, uint64_t* pk, uint64_t* sk) {
+  if (!cryptodir) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    const std::string dir(cryptodir);
+    PalisadeContext pc = palisade_read_context(read_file(dir + "cryptocontext.txt"));
+    const uint32_t L = (uint32_t)pc.q.size();
+    if (ring_dim) *ring_dim = pc.N;
+    if (num_towers) *num_towers = L;
+    for (uint32_t t = 0; t < L; ++t) {
+      if (moduli) moduli[t] = pc.q[t];
+      if (roots) roots[t] = pc.psi[t];
+    }
+    if (pk || sk) {
+      std::vector<uint64_t> p, s;
+      palisade_read_keys(read_file(dir + "key-public.txt"), read_file(dir + "key-private.txt"),
+                         pc.N, pc.q, p, s);
+      if (pk) std::memcpy(pk, p.data(), p.size() * 8);
+      if (sk) std::memcpy(sk, s.data(), s.size() * 8);
+    }
+  });
+}
+
+int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bits,
+                      uint32_t first_mod_bits, uint32_t batch, int device, shelfi_ctx** out) {
+  if (!out) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  shelfi_ctx* ctx = new (std::nothrow) shelfi_ctx();
+  if (!ctx) return SHELFI_ERR_DEVICE;
+  int rc = guarded([&] {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+      throw Error{SHELFI_ERR_DEVICE, "no HIP device available (libshelfi requires an MI355X / gfx950)"};
+    if (device < 0 || device >= count) throw Error{SHELFI_ERR_ARG, "device ordinal out of range"};
+    hipDeviceProp_t prop;
+    SHELFI_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      throw Error{SHELFI_ERR_DEVICE, std::string("device is ") + prop.gcnArchName +
+                                         "; libshelfi is built for gfx950 only"};
+    ctx->device = device;
+    DeviceGuard g(device);
+    uint32_t N = ring_dim ? ring_dim
+                          : default_ring_dim(num_towers, scale_bits, first_mod_bits, batch);
+    if (!N) throw Error{SHELFI_ERR_ARG, "no ring dimension satisfies the security/batch constraints"};
+    validate_params(N, num_towers, scale_bits, first_mod_bits, batch);
+    uint64_t q[kMaxTowers], psi[kMaxTowers];
+    generate_chain(N, num_towers, scale_bits, first_mod_bits, q, psi);
+    SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    SHELFI_HIP(hipMalloc(&ctx->dev_flag, 16));
+    set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
+  });
+  if (rc != SHELFI_OK) {
+    shelfi_ctx_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return SHELFI_OK;
+}
+
+void shelfi_ctx_destroy(shelfi_ctx* ctx) {
+  if (!ctx) return;
+  {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_keys(ctx);
+    free_tables(ctx);
+    dfree(ctx->scratch);
+    dfree(ctx->io);
+    dfree_t(ctx->dev_flag);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  delete ctx;
+}
+
+int shelfi_ctx_info(const shelfi_ctx* ctx, shelfi_info* o) {
+  if (!ctx || !o) return SHELFI_ERR_ARG;
+  std::memset(o, 0, sizeof(*o));
+  o->ring_dim = ctx->p.N;
+  o->num_towers = ctx->p.L;
+  o->batch = ctx->p.batch;
+  o->scale_bits = ctx->p.scale_bits;
+  o->first_mod_bits = ctx->p.first_mod_bits;
+  o->device = ctx->device;
+  for (uint32_t t = 0; t < ctx->p.L; ++t) {
+    o->moduli[t] = ctx->p.q[t];
+    o->roots[t] = ctx->p.psi[t];
+  }
+  o->delta = ctx->p.delta;
+  o->key_id = ctx->key_id;
+  o->keys_loaded = ctx->keys_loaded ? 1 : 0;
+  o->palisade_keys = ctx->palisade_keys ? 1 : 0;
+  return SHELFI_OK;
+}
+
+int shelfi_set_seed(shelfi_ctx* ctx, uint64_t seed) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  ctx->seed = seed;
+  ctx->enc_counter = 0;
+  return SHELFI_OK;
+}
+
+int shelfi_set_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk) {
+  if (!ctx || !pk || !sk) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    install_keys(ctx, pk, sk, false);
+  });
+}
+
+int shelfi_get_keys(const shelfi_ctx* ctx, uint64_t* pk, uint64_t* sk) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  if (!ctx->keys_loaded) {
+    set_error("no keys loaded");
+    return SHELFI_ERR_STATE;
+  }
+  if (pk) std::memcpy(pk, ctx->pk_host.data(), ctx->pk_host.size() * sizeof(uint64_t));
+  if (sk) std::memcpy(sk, ctx->sk_host.data(), ctx->sk_host.size() * sizeof(uint64_t));
+  return SHELFI_OK;
+}
+
+int shelfi_keygen(shelfi_ctx* ctx, const char* cryptodir) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    const size_t LN = (size_t)p.L * p.N;
+    uint32_t key[8];
+    if (ctx->seed)
+      seed_to_key(ctx->seed, key);
+    else
+      os_random(key, 32);
+    void* sk_d = nullptr;
+    void* pk_d = nullptr;
+    SHELFI_HIP(hipMalloc(&sk_d, LN * 8));
+    SHELFI_HIP(hipMalloc(&pk_d, 2 * LN * 8));
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, keygen_scratch_bytes(p));
+    std::vector<uint64_t> sk(LN), pk(2 * LN);
+    try {
+      launch_keygen(p, ctx->dt, key, (uint64_t*)sk_d, (uint64_t*)pk_d, scratch, ctx->stream);
+      SHELFI_HIP(hipMemcpyAsync(sk.data(), sk_d, LN * 8, hipMemcpyDeviceToHost, ctx->stream));
+      SHELFI_HIP(hipMemcpyAsync(pk.data(), pk_d, 2 * LN * 8, hipMemcpyDeviceToHost, ctx->stream));
+      SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+      (void)hipFree(sk_d);
+      (void)hipFree(pk_d);
+      throw;
+    }
+    (void)hipFree(sk_d);
+    (void)hipFree(pk_d);
+    std::memset(key, 0, sizeof(key));
+    install_keys(ctx, pk.data(), sk.data(), false);
+    if (cryptodir && *cryptodir) {
+      const std::string dir(cryptodir);
+      std::string cc("SHCC", 4), ps("SHPK", 4), ss("SHSK", 4);
+      const uint32_t ver = 1;
+      put(cc, ver);
+      put(cc, p.N);
+      put(cc, p.L);
+      put(cc, p.batch);
+      put(cc, p.scale_bits);
+      put(cc, p.first_mod_bits);
+      put(cc, p.sigma);
+      for (uint32_t t = 0; t < p.L; ++t) put(cc, p.q[t]);
+      for (uint32_t t = 0; t < p.L; ++t) put(cc, p.psi[t]);
+      put(ps, ver);
+      put(ps, ctx->params_id);
+      ps.append(reinterpret_cast<const char*>(pk.data()), pk.size() * 8);
+      put(ss, ver);
+      put(ss, ctx->params_id);
+      ss.append(reinterpret_cast<const char*>(sk.data()), sk.size() * 8);
+      // ckks.cpp:36-56: context first, then public, then private key
+      write_file(dir + "cryptocontext.txt", cc);
+      write_file(dir + "key-public.txt", ps);
+      write_file(dir + "key-private.txt", ss);
+    }
+  });
+}
+
+int shelfi_load(shelfi_ctx* ctx, const char* cryptodir) {
+  if (!ctx || !cryptodir) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    const std::string dir(cryptodir);
+    const std::string cc = read_file(dir + "cryptocontext.txt");
+    if (cc.size() >= 4 && cc.compare(0, 4, "SHCC") == 0) {
+      size_t off = 4;
+      if (get<uint32_t>(cc, off) != 1) throw Error{SHELFI_ERR_FORMAT, "unsupported context version"};
+      const uint32_t N = get<uint32_t>(cc, off), L = get<uint32_t>(cc, off);
+      const uint32_t batch = get<uint32_t>(cc, off), sb = get<uint32_t>(cc, off);
+      const uint32_t fb = get<uint32_t>(cc, off);
+      const double sigma = get<double>(cc, off);
+      if (L < 1 || L > (uint32_t)kMaxTowers) throw Error{SHELFI_ERR_FORMAT, "bad tower count"};
+      uint64_t q[kMaxTowers], psi[kMaxTowers];
+      for (uint32_t t = 0; t < L; ++t) q[t] = get<uint64_t>(cc, off);
+      for (uint32_t t = 0; t < L; ++t) psi[t] = get<uint64_t>(cc, off);
+      validate_params(N, L, sb, fb, batch);
+      free_keys(ctx);
+      set_params(ctx, N, L, sb, fb, batch, q, psi);
+      ctx->p.sigma = sigma;
+      const size_t LN = (size_t)L * N;
+      const std::string ps = read_file(dir + "key-public.txt");
+      const std::string ss = read_file(dir + "key-private.txt");
+      size_t po = 4, so = 4;
+      if (ps.compare(0, 4, "SHPK") != 0 || ss.compare(0, 4, "SHSK") != 0)
+        throw Error{SHELFI_ERR_FORMAT, "key files do not match the context format"};
+      (void)get<uint32_t>(ps, po);
+      (void)get<uint32_t>(ss, so);
+      if (get<uint64_t>(ps, po) != ctx->params_id || get<uint64_t>(ss, so) != ctx->params_id)
+        throw Error{SHELFI_ERR_FORMAT, "key files were generated for a different context"};
+      if (ps.size() != po + 2 * LN * 8 || ss.size() != so + LN * 8)
+        throw Error{SHELFI_ERR_FORMAT, "key file size mismatch"};
+      install_keys(ctx, reinterpret_cast<const uint64_t*>(ps.data() + po),
+                   reinterpret_cast<const uint64_t*>(ss.data() + so), false);
+    } else {
+      // PALISADE 1.11 cereal-binary files (the reference's committed key material)
+      PalisadeContext pc = palisade_read_context(cc);
+      const uint32_t N = pc.N, L = (uint32_t)pc.q.size();
+      const uint32_t batch = std::min<uint32_t>(ctx->p.batch, N / 2);
+      validate_params(N, L, ctx->p.scale_bits, ctx->p.first_mod_bits < ctx->p.scale_bits
+                                                   ? ctx->p.scale_bits
+                                                   : ctx->p.first_mod_bits,
+                      batch);
+      free_keys(ctx);
+      set_params(ctx, N, L, ctx->p.scale_bits, ctx->p.first_mod_bits, batch, pc.q.data(),
+                 pc.psi.data());
+      std::vector<uint64_t> pk, sk;
+      palisade_read_keys(read_file(dir + "key-public.txt"), read_file(dir + "key-private.txt"),
+                         N, pc.q, pk, sk);
+      install_keys(ctx, pk.data(), sk.data(), true);
+    }
+  });
+}
+
+// ------------------------------------------------------------- bytes API ----
+int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, size_t* out_len) {
+  if (!ctx || !out || !out_len || (n && !x)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  *out = nullptr;
+  *out_len = 0;
+  return guarded([&] {
+    require_keys(ctx);
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    for (size_t i = 0; i < n; ++i)
+      if (!std::isfinite(x[i])) throw Error{SHELFI_ERR_RANGE, "encrypt: input contains NaN/inf"};
+    // ckks.cpp:65 cipherSize = ceil(size / batchSize)
+    const uint64_t K = (n + p.batch - 1) / p.batch;
+    const size_t ct_bytes = 2ull * p.L * p.N * 8;
+    const size_t total = sizeof(BlobHeader) + K * ct_bytes;
+    uint8_t* blob = (uint8_t*)std::malloc(total);
+    if (!blob) throw std::bad_alloc();
+    BlobHeader h;
+    std::memset(&h, 0, sizeof(h));
+    std::memcpy(h.magic, "SHCT", 4);
+    h.version = 1;
+    h.header_bytes = 64;
+    h.logN = p.logN;
+    h.L = p.L;
+    h.K = K;
+    h.depth = 1;
+    h.level = 0;
+    h.scale = p.delta;
+    h.params_id = ctx->params_id;
+    h.key_id = ctx->key_id;
+    h.batch = p.batch;
+    h.encoding = 4;
+    std::memcpy(blob, &h, sizeof(h));
+    try {
+      if (K) {
+        uint32_t key[8];
+        uint64_t g0;
+        draw_key(ctx, K, key, &g0);
+        const uint64_t chunk = std::max<uint64_t>(1, (512ull << 20) / encrypt_scratch_bytes(p, 1));
+        const uint64_t kc_max = std::min<uint64_t>(chunk, K);
+        const size_t xin = kc_max * p.batch * 8, cto = kc_max * ct_bytes;
+        uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, xin + cto);
+        void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
+        SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, ctx->stream));
+        for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
+          const uint64_t kc = std::min(kc_max, K - k0);
+          const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kc * p.batch);
+          SHELFI_HIP(hipMemcpyAsync(io, x + xs, xn * 8, hipMemcpyHostToDevice, ctx->stream));
+          launch_encrypt(p, ctx->dt, ctx->dk, (const double*)io, xn, kc, (uint64_t*)(io + xin),
+                         scratch, key, g0 + k0, ctx->dev_flag, ctx->stream);
+          SHELFI_HIP(hipMemcpyAsync(blob + sizeof(h) + k0 * ct_bytes, io + xin, kc * ct_bytes,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+          SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        std::memset(key, 0, sizeof(key));
+        uint32_t flag = 0;
+        SHELFI_HIP(hipMemcpy(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost));
+        if (flag)
+          throw Error{SHELFI_ERR_RANGE,
+                      "encrypt: |value * scale| exceeds 2^61 (PALISADE approxFactor range)"};
+      }
+    } catch (...) {
+      std::free(blob);
+      throw;
+    }
+    *out = blob;
+    *out_len = total;
+  });
+}
+
+int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                            const float* weights, size_t C, uint8_t** out, size_t* out_len) {
+  if (!ctx || !out || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  *out = nullptr;
+  *out_len = 0;
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    if (C == 0) throw Error{SHELFI_ERR_ARG, "computeWeightedAverage: no learners"};
+    BlobHeader h0 = parse_blob(blobs[0], lens[0], ctx);
+    for (size_t c = 1; c < C; ++c) {
+      BlobHeader h = parse_blob(blobs[c], lens[c], ctx);
+      if (h.K != h0.K)
+        throw Error{SHELFI_ERR_FORMAT, "learners hold different numbers of ciphertexts"};
+      if (h.key_id != h0.key_id)
+        throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts were encrypted under different keys"};
+      if (h.depth != h0.depth || h.scale != h0.scale)
+        throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts have different depth/scale"};
+    }
+    const uint64_t K = h0.K;
+    const size_t ct_bytes = 2ull * p.L * p.N * 8, payload = K * ct_bytes;
+    BlobHeader ho = h0;
+    ho.depth = h0.depth + 1;     // EvalMult by a constant: depth + 1, no rescale
+    ho.scale = h0.scale * p.delta;  // scalingFactor * scFactor(level 0)
+    const size_t total = sizeof(BlobHeader) + payload;
+    uint8_t* blob = (uint8_t*)std::malloc(total);
+    if (!blob) throw std::bad_alloc();
+    std::memcpy(blob, &ho, sizeof(ho));
+    try {
+      if (K) {
+        // learners in groups of 16 (one launch each, accumulating)
+        const size_t group = std::min<size_t>(C, kWavgMaxLearners);
+        uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, (group + 1) * payload);
+        uint64_t* dout = (uint64_t*)(io + group * payload);
+        for (size_t c0 = 0; c0 < C; c0 += group) {
+          const size_t gc = std::min(group, C - c0);
+          WavgArgs a;
+          std::memset(&a, 0, sizeof(a));
+          for (size_t c = 0; c < gc; ++c) {
+            SHELFI_HIP(hipMemcpyAsync(io + c * payload, blobs[c0 + c] + sizeof(BlobHeader),
+                                      payload, hipMemcpyHostToDevice, ctx->stream));
+            a.ptrs[c] = (const uint64_t*)(io + c * payload);
+            const int64_t W = (int64_t)((double)weights[c0 + c] * p.delta + 0.5);  // ckks.cpp:287-288
+            for (uint32_t t = 0; t < p.L; ++t) {
+              const uint64_t wt = mod_signed(W, p.q[t]);
+              a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
+              a.wl[c][t][1] = (uint32_t)(wt >> 30);
+            }
+          }
+          a.out = dout;
+          a.rows = K * 2 * p.L;
+          a.C = (uint32_t)gc;
+          a.L = p.L;
+          a.logN = p.logN;
+          a.accumulate = c0 ? 1 : 0;
+          launch_wavg(a, ctx->dt.tc, ctx->stream);
+          SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        SHELFI_HIP(hipMemcpyAsync(blob + sizeof(BlobHeader), dout, payload, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+        SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+      }
+    } catch (...) {
+      std::free(blob);
+      throw;
+    }
+    *out = blob;
+    *out_len = total;
+  });
+}
+
+int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out) {
+  if (!ctx || (n && !out)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    require_keys(ctx);
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    BlobHeader h = parse_blob(blob, len, ctx);
+    if (h.key_id != ctx->key_id)
+      throw Error{SHELFI_ERR_FORMAT, "ciphertext was encrypted under a different key"};
+    if (n > h.K * (uint64_t)p.batch)
+      throw Error{SHELFI_ERR_ARG, "decrypt: data_dimensions exceeds the slots in the ciphertexts"};
+    if (!n) return;
+    // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
+    const uint64_t K = (n + p.batch - 1) / p.batch;
+    const size_t ct_bytes = 2ull * p.L * p.N * 8;
+    const uint64_t chunk = std::max<uint64_t>(1, (512ull << 20) / decrypt_scratch_bytes(p, 1));
+    const uint64_t kc_max = std::min<uint64_t>(chunk, K);
+    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, kc_max * ct_bytes + kc_max * p.batch * 8);
+    double* dout = (double*)(io + kc_max * ct_bytes);
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
+    for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
+      const uint64_t kc = std::min(kc_max, K - k0);
+      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
+      SHELFI_HIP(hipMemcpyAsync(io, blob + sizeof(BlobHeader) + k0 * ct_bytes, kc * ct_bytes,
+                                hipMemcpyHostToDevice, ctx->stream));
+      launch_decrypt(p, ctx->dt, ctx->dk, (const uint64_t*)io, kc, h.scale, on, dout, scratch,
+                     ctx->stream);
+      SHELFI_HIP(hipMemcpyAsync(out + o0, dout, on * 8, hipMemcpyDeviceToHost, ctx->stream));
+      SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+    }
+  });
+}
+
+int shelfi_blob_info(const uint8_t* blob, size_t len, uint64_t* num_cts, uint32_t* depth,
+                     double* scale, uint64_t* key_id) {
+  return guarded([&] {
+    BlobHeader h = parse_blob(blob, len, nullptr);
+    if (num_cts) *num_cts = h.K;
+    if (depth) *depth = h.depth;
+    if (scale) *scale = h.scale;
+    if (key_id) *key_id = h.key_id;
+  });
+}
+
+size_t shelfi_blob_header_bytes(void) { return sizeof(BlobHeader); }
+
+int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t K, uint32_t depth,
+                     double scale, uint8_t** out, size_t* out_len) {
+  if (!ctx || !out || !out_len || (K && !residues)) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    const Params& p = ctx->p;
+    const size_t payload = K * 2ull * p.L * p.N * 8;
+    BlobHeader h;
+    std::memset(&h, 0, sizeof(h));
+    std::memcpy(h.magic, "SHCT", 4);
+    h.version = 1;
+    h.header_bytes = 64;
+    h.logN = p.logN;
+    h.L = p.L;
+    h.K = K;
+    h.depth = depth;
+    h.scale = scale;
+    h.params_id = ctx->params_id;
+    h.key_id = ctx->key_id;
+    h.batch = p.batch;
+    h.encoding = 4;
+    uint8_t* blob = (uint8_t*)std::malloc(sizeof(h) + payload);
+    if (!blob) throw std::bad_alloc();
+    std::memcpy(blob, &h, sizeof(h));
+    if (payload) std::memcpy(blob + sizeof(h), residues, payload);
+    *out = blob;
+    *out_len = sizeof(h) + payload;
+  });
+}
+
+// ------------------------------------------------------------ device API ----
+int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float* w, size_t C,
+                    size_t K, uint64_t* out_dev, void* stream) {
+  if (!ctx || !out_dev || (C && (!in_dev || !w))) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    for (size_t c0 = 0; c0 < C; c0 += kWavgMaxLearners) {
+      const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
+      WavgArgs a;
+      std::memset(&a, 0, sizeof(a));
+      for (size_t c = 0; c < gc; ++c) {
+        a.ptrs[c] = in_dev[c0 + c];
+        const int64_t W = (int64_t)((double)w[c0 + c] * p.delta + 0.5);
+        for (uint32_t t = 0; t < p.L; ++t) {
+          const uint64_t wt = mod_signed(W, p.q[t]);
+          a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
+          a.wl[c][t][1] = (uint32_t)(wt >> 30);
+        }
+      }
+      a.out = out_dev;
+      a.rows = (uint64_t)K * 2 * p.L;
+      a.C = (uint32_t)gc;
+      a.L = p.L;
+      a.logN = p.logN;
+      a.accumulate = c0 ? 1 : 0;
+      launch_wavg(a, ctx->dt.tc, s);
+    }
+  });
+}
+
+int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream) {
+  if (!ctx || !buf_dev) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    launch_modq(buf_dev, (uint64_t)K * 2 * ctx->p.L, ctx->p.L, ctx->p.logN, ctx->dt.tc, s);
+  });
+}
+
+int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
+                       void* stream) {
+  if (!ctx || (n && (!x_dev || !ct_dev))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    require_keys(ctx);
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    const uint64_t K = (n + p.batch - 1) / p.batch;
+    if (!K) return;
+    uint32_t key[8];
+    uint64_t g0;
+    draw_key(ctx, K, key, &g0);
+    const uint64_t chunk = std::max<uint64_t>(1, (1024ull << 20) / encrypt_scratch_bytes(p, 1));
+    const uint64_t kc_max = std::min<uint64_t>(chunk, K);
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
+    SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, s));
+    const size_t ct_words = 2ull * p.L * p.N;
+    for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
+      const uint64_t kc = std::min(kc_max, K - k0);
+      const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kc * p.batch);
+      launch_encrypt(p, ctx->dt, ctx->dk, x_dev + xs, xn, kc, ct_dev + k0 * ct_words, scratch,
+                     key, g0 + k0, ctx->dev_flag, s);
+    }
+    std::memset(key, 0, sizeof(key));
+    uint32_t flag = 0;
+    SHELFI_HIP(hipMemcpyAsync(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));
+    SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
+    if (flag)
+      throw Error{SHELFI_ERR_RANGE, "encrypt: |value * scale| exceeds 2^61 (approxFactor range)"};
+  });
+}
+
+int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double scale, size_t n,
+                       double* out_dev, void* stream) {
+  if (!ctx || (n && (!ct_dev || !out_dev))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    require_keys(ctx);
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    if (n > (uint64_t)K * p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    const uint64_t Kn = (n + p.batch - 1) / p.batch;
+    if (!Kn) return;
+    const uint64_t chunk = std::max<uint64_t>(1, (1024ull << 20) / decrypt_scratch_bytes(p, 1));
+    const uint64_t kc_max = std::min<uint64_t>(chunk, Kn);
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
+    const size_t ct_words = 2ull * p.L * p.N;
+    for (uint64_t k0 = 0; k0 < Kn; k0 += kc_max) {
+      const uint64_t kc = std::min(kc_max, Kn - k0);
+      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
+      launch_decrypt(p, ctx->dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0,
+                     scratch, s);
+    }
+    SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
+  });
+}
+
+int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, void* stream) {
+  if (!ctx || (P && !polys_dev)) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    launch_ntt(polys_dev, P, ctx->p.L, ctx->p.logN, inverse != 0, ctx->dt, s);
+  });
+}
+
+int shelfi_fft_twiddles(uint32_t slots, double* ir, double* ii, double* fr, double* fi) {
+  if (!slots || (slots & (slots - 1)) || !ir || !ii || !fr || !fi) return SHELFI_ERR_ARG;
+  fft_twiddles(slots, ir, ii, fr, fi);
+  return SHELFI_OK;
+}
+
+int shelfi_gauss_cdt(double sigma, uint64_t* cdt, int max_entries) {
+  if (!cdt) return SHELFI_ERR_ARG;
+  return gauss_cdt(sigma, cdt, max_entries);
+}
+
+}  // extern "C"

@@ -1,0 +1,906 @@
+// kernels.hip — hand-written gfx950 kernels for the RNS-CKKS aggregation path.
+//
+// Data layout in HBM (all uint64 residues, EVALUATION domain, PALISADE's
+// bit-reversed order):  ciphertext batch [K][2][L][N]  (ct, poly, tower, coeff) —
+// the order of a serialized vector<Ciphertext<DCRTPoly>> (ckks.cpp:98-100).
+//
+// Kernels (roofline class in DESIGN.md):
+//   wavg_kernel        EvalMult(ct, (float)w) + EvalAdd over C learners
+//                      (ckks.cpp:286-297)                              HBM-bound
+//   modq_kernel        fold a collective's uint64 sum of partials back to [0,q)
+//   ntt_*              negacyclic NTT/INTT, 2 passes (register columns + LDS blocks)
+//   fft_*              CKKS special FFT / inverse (encode / decode), 2 passes
+//   enc_prep_kernel    round/scale/reduce the encoded slots + ChaCha20 sampling of
+//                      (v, e0, e1) (ckks.cpp:80-81)
+//   enc_combine_kernel c0 = v*b + (m + e0), c1 = v*a + e1
+//   dec_combine_kernel c0 + c1*s (ckks.cpp:189)
+//   crt_decode_kernel  exact centered CRT -> double / scale, bit-reversed scatter
+//   keygen_*           ternary s, Gaussian e, uniform a; b = e - a*s
+//
+// 64-bit modular arithmetic: CDNA4 has no 64x64->128 multiply; products are
+// built from v_mad_u64_u32 / v_mul_hi_u32 by the compiler (__umul64hi).  Constant
+// multiplications use Shoup's precomputed quotient (w' = floor(w 2^64 / q)).
+#include <hip/hip_runtime.h>
+
+#include "shelfi_internal.h"
+
+namespace shelfi {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------ modular ops ----
+__device__ __forceinline__ uint64_t addmod(uint64_t a, uint64_t b, uint64_t q) {
+  uint64_t s = a + b;
+  return s >= q ? s - q : s;
+}
+__device__ __forceinline__ uint64_t submod(uint64_t a, uint64_t b, uint64_t q) {
+  return a >= b ? a - b : a + q - b;
+}
+// x * w mod q, w < q, w' = floor(w 2^64 / q), any 64-bit x.
+__device__ __forceinline__ uint64_t shoup_mul(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
+  uint64_t hi = __umul64hi(x, wp);
+  uint64_t r = x * w - hi * q;
+  return r >= q ? r - q : r;
+}
+// x mod q for any 64-bit x (Shoup with w = 1).
+__device__ __forceinline__ uint64_t red64(uint64_t x, uint64_t q, uint64_t one_sh) {
+  uint64_t hi = __umul64hi(x, one_sh);
+  uint64_t r = x - hi * q;
+  return r >= q ? r - q : r;
+}
+// a * b mod q for arbitrary a, b < q (no precomputed companion).
+__device__ __forceinline__ uint64_t mulmod_generic(uint64_t a, uint64_t b, const TowerConst& c) {
+  uint64_t hi = __umul64hi(a, b), lo = a * b;
+  return addmod(shoup_mul(hi, c.r64, c.r64_shoup, c.q), red64(lo, c.q, c.one_shoup), c.q);
+}
+__device__ __forceinline__ uint64_t mod_signed_dev(int64_t v, const TowerConst& c) {
+  if (v >= 0) return red64((uint64_t)v, c.q, c.one_shoup);
+  uint64_t r = red64((uint64_t)0 - (uint64_t)v, c.q, c.one_shoup);
+  return r ? c.q - r : 0;
+}
+__device__ __forceinline__ uint32_t bitrev_dev(uint32_t x, uint32_t bits) {
+  return bits ? (__brev(x) >> (32 - bits)) : 0;
+}
+// llround (ties away from zero), the oracle's or_round_half_away.
+__device__ __forceinline__ int64_t round_half_away(double x) {
+  double t = trunc(x);
+  double d = __dsub_rn(x, t);
+  if (d >= 0.5) t = __dadd_rn(t, 1.0);
+  else if (d <= -0.5) t = __dsub_rn(t, 1.0);
+  return (int64_t)t;
+}
+// complex helpers: (a+bi)(c+di) = (ac - bd, ad + bc), each op rounded (no FMA).
+__device__ __forceinline__ double2 cmul(double2 v, double2 w) {
+  return make_double2(__dsub_rn(__dmul_rn(v.x, w.x), __dmul_rn(v.y, w.y)),
+                      __dadd_rn(__dmul_rn(v.x, w.y), __dmul_rn(v.y, w.x)));
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) {
+  return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
+}
+__device__ __forceinline__ double2 csub(double2 a, double2 b) {
+  return make_double2(__dsub_rn(a.x, b.x), __dsub_rn(a.y, b.y));
+}
+
+// ------------------------------------------------------------------ wavg ----
+// One thread = 2 adjacent residues (one 16-byte load per learner); one block =
+// 512 residues of a single (ct, poly, tower) row, so the tower — and with it
+// q and every learner's weight — is block-uniform and lives in SGPRs.  Up to 16
+// learners per launch travel in the kernel-argument segment (pointers + weight
+// limbs, read with s_load); more learners accumulate over further launches.
+//
+// Lazy accumulation without carries: x = x1*2^30 + x0 and W = w1*2^30 + w0
+// (x, W < q < 2^60, so all four limbs are < 2^30).  Each limb product is < 2^60,
+// so 16 of them fit a u64: per learner 4 v_mad_u64_u32 and no reduction.  After
+// the (<= 16) learners of a launch the four sums are folded: T = S00 + 2^30 (S01 + S10) +
+// 2^60 S11 mod q.  Bit-exact with sum_c (W_c x_c mod q) in any order.
+constexpr int kWavgThreads = 256;
+constexpr int kWavgPerBlock = 2 * kWavgThreads;
+
+__device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64_t s10,
+                                              uint64_t s11, const TowerConst& c) {
+  uint64_t a = red64(s00, c.q, c.one_shoup);
+  uint64_t m = red64(s01, c.q, c.one_shoup) + red64(s10, c.q, c.one_shoup);  // < 2q
+  uint64_t b = shoup_mul(m, c.r30, c.r30_shoup, c.q);
+  uint64_t d = shoup_mul(red64(s11, c.q, c.one_shoup), c.r60, c.r60_shoup, c.q);
+  return addmod(addmod(a, b, c.q), d, c.q);
+}
+
+__global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
+                                                            const TowerConst* __restrict__ tcs) {
+  const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
+  const uint32_t t = (uint32_t)((base >> a.logN) % a.L);  // block-uniform tower
+  const TowerConst c = tcs[t];
+  const uint64_t e = base + 2u * threadIdx.x;
+  const uint32_t M30 = (1u << 30) - 1;
+
+  uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
+  uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
+#pragma unroll 8
+  for (uint32_t k = 0; k < a.C; ++k) {
+    const uint64_t* __restrict__ p = a.ptrs[k];
+    const uint32_t w0 = a.wl[k][t][0], w1 = a.wl[k][t][1];
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + e));
+    // element a: (v.x, v.y), element b: (v.z, v.w); 30-bit limbs
+    const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
+    const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
+    s00a += (uint64_t)xa0 * w0;
+    s01a += (uint64_t)xa0 * w1;
+    s10a += (uint64_t)xa1 * w0;
+    s11a += (uint64_t)xa1 * w1;
+    s00b += (uint64_t)xb0 * w0;
+    s01b += (uint64_t)xb0 * w1;
+    s10b += (uint64_t)xb1 * w0;
+    s11b += (uint64_t)xb1 * w1;
+  }
+  uint64_t r0 = wavg_fold(s00a, s01a, s10a, s11a, c);
+  uint64_t r1 = wavg_fold(s00b, s01b, s10b, s11b, c);
+  if (a.accumulate) {  // learners beyond the first 16: fold into the running sum
+    const uint4 o = *reinterpret_cast<const uint4*>(a.out + e);
+    r0 = addmod(r0, (uint64_t)o.x | ((uint64_t)o.y << 32), c.q);
+    r1 = addmod(r1, (uint64_t)o.z | ((uint64_t)o.w << 32), c.q);
+  }
+  u32x4 o;
+  o.x = (uint32_t)r0;
+  o.y = (uint32_t)(r0 >> 32);
+  o.z = (uint32_t)r1;
+  o.w = (uint32_t)(r1 >> 32);
+  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(a.out + e));
+}
+
+void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
+  const uint64_t total = a.rows << a.logN;
+  const uint64_t blocks = total / kWavgPerBlock;
+  if (!blocks) return;
+  if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  hipLaunchKernelGGL(wavg_kernel, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+  SHELFI_HIP(hipGetLastError());
+}
+
+// A collective's uint64 sum of G <= 15 partial sums (each < q < 2^60) -> [0, q).
+__global__ __launch_bounds__(256) void modq_kernel(uint64_t* buf, uint32_t L, uint32_t logN,
+                                                   const TowerConst* __restrict__ tcs) {
+  const uint64_t base = (uint64_t)blockIdx.x * 512;
+  const uint32_t t = (uint32_t)((base >> logN) % L);
+  const uint64_t q = tcs[t].q, osh = tcs[t].one_shoup;
+  uint64_t* p = buf + base + 2u * threadIdx.x;
+  p[0] = red64(p[0], q, osh);
+  p[1] = red64(p[1], q, osh);
+}
+
+void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
+                 hipStream_t s) {
+  const uint64_t blocks = (rows << logN) / 512;
+  if (!blocks) return;
+  hipLaunchKernelGGL(modq_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, buf, L, logN, tc);
+  SHELFI_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------- NTT ----
+// Forward (Cooley-Tukey, natural -> bit-reversed), stage m (= 2^s) pairs
+// (j, j + N/2m) with twiddle psi_rev[m + j/(N/m)].  The first LOGR stages pair
+// elements R = 2^LOGR apart in the top bits: each thread holds one column of R
+// elements (stride N/R) in registers, all twiddles wave-uniform.  The remaining
+// stages act inside contiguous blocks of N/R elements, staged in LDS.
+template <int LOGR>
+__global__ __launch_bounds__(256) void ntt_fwd_cols(uint64_t* __restrict__ polys, uint32_t L,
+                                                    uint32_t logN, const uint64_t* __restrict__ tw,
+                                                    const uint64_t* __restrict__ twp,
+                                                    const TowerConst* __restrict__ tcs) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t N = 1u << logN;
+  const uint32_t BLK = N >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t poly = blockIdx.x / bpp;
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  const uint32_t t = (uint32_t)(poly % L);
+  const uint64_t q = tcs[t].q;
+  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+  uint64_t* __restrict__ a = polys + poly * N + col;
+  uint64_t x[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) x[r] = a[(uint64_t)r * BLK];
+#pragma unroll
+  for (int s = 0; s < LOGR; ++s) {
+    const int m = 1 << s, tr = R >> (s + 1);
+#pragma unroll
+    for (int i = 0; i < m; ++i) {
+      const uint64_t W = w[m + i], Wp = wp[m + i];
+#pragma unroll
+      for (int jj = 0; jj < tr; ++jj) {
+        const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+        const uint64_t U = x[r0], V = shoup_mul(x[r1], W, Wp, q);
+        x[r0] = addmod(U, V, q);
+        x[r1] = submod(U, V, q);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) a[(uint64_t)r * BLK] = x[r];
+}
+
+// Blocks pass, stages s = sstart .. logN-1 on contiguous blocks of 2^(logN-sstart).
+__global__ __launch_bounds__(256) void ntt_fwd_blocks(uint64_t* __restrict__ polys, uint32_t L,
+                                                      uint32_t logN, uint32_t sstart,
+                                                      const uint64_t* __restrict__ tw,
+                                                      const uint64_t* __restrict__ twp,
+                                                      const TowerConst* __restrict__ tcs) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << logN, blkLog = logN - sstart, blk = 1u << blkLog;
+  const uint32_t nb = 1u << sstart;
+  const uint64_t poly = blockIdx.x >> sstart;
+  const uint32_t b = blockIdx.x & (nb - 1);
+  const uint32_t t = (uint32_t)(poly % L);
+  const uint64_t q = tcs[t].q;
+  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+  uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
+  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
+    reinterpret_cast<ulonglong2*>(sm)[i] = reinterpret_cast<const ulonglong2*>(a)[i];
+  __syncthreads();
+  for (uint32_t s = sstart; s < logN; ++s) {
+    const uint32_t m = 1u << s, tlog = logN - 1 - s, tt = 1u << tlog;
+    for (uint32_t k = threadIdx.x; k < blk / 2; k += 256) {
+      const uint32_t j = ((k >> tlog) << (tlog + 1)) | (k & (tt - 1));
+      const uint32_t gi = (b << (blkLog - tlog - 1)) + (k >> tlog);
+      const uint64_t W = w[m + gi], Wp = wp[m + gi];
+      const uint64_t U = sm[j], V = shoup_mul(sm[j + tt], W, Wp, q);
+      sm[j] = addmod(U, V, q);
+      sm[j + tt] = submod(U, V, q);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
+    reinterpret_cast<ulonglong2*>(a)[i] = reinterpret_cast<const ulonglong2*>(sm)[i];
+}
+
+// Inverse (Gentleman-Sande, bit-reversed -> natural), stage with half-size tt
+// pairs (j, j+tt), twiddle ipsi_rev[N/(2tt) + j/(2tt)]; small tt first (LDS
+// blocks), then the top LOGR stages on register columns, scaled by N^-1.
+__global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ polys, uint32_t L,
+                                                      uint32_t logN, uint32_t blkLog,
+                                                      const uint64_t* __restrict__ tw,
+                                                      const uint64_t* __restrict__ twp,
+                                                      const TowerConst* __restrict__ tcs,
+                                                      int scale_ninv) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << logN, blk = 1u << blkLog;
+  const uint32_t sh = logN - blkLog, nb = 1u << sh;
+  const uint64_t poly = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & (nb - 1);
+  const uint32_t t = (uint32_t)(poly % L);
+  const TowerConst& c = tcs[t];
+  const uint64_t q = c.q;
+  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+  uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
+  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
+    reinterpret_cast<ulonglong2*>(sm)[i] = reinterpret_cast<const ulonglong2*>(a)[i];
+  __syncthreads();
+  for (uint32_t u = 0; u < blkLog; ++u) {
+    const uint32_t tt = 1u << u;
+    const uint32_t h = N >> (u + 1);
+    for (uint32_t k = threadIdx.x; k < blk / 2; k += 256) {
+      const uint32_t j = ((k >> u) << (u + 1)) | (k & (tt - 1));
+      const uint32_t gi = (b << (blkLog - u - 1)) + (k >> u);
+      const uint64_t W = w[h + gi], Wp = wp[h + gi];
+      const uint64_t U = sm[j], V = sm[j + tt];
+      sm[j] = addmod(U, V, q);
+      sm[j + tt] = shoup_mul(submod(U, V, q), W, Wp, q);
+    }
+    __syncthreads();
+  }
+  if (scale_ninv) {
+    const uint64_t ni = c.ninv, nip = c.ninv_shoup;
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) a[i] = shoup_mul(sm[i], ni, nip, q);
+  } else {
+    for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
+      reinterpret_cast<ulonglong2*>(a)[i] = reinterpret_cast<const ulonglong2*>(sm)[i];
+  }
+}
+
+template <int LOGR>
+__global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys, uint32_t L,
+                                                    uint32_t logN, const uint64_t* __restrict__ tw,
+                                                    const uint64_t* __restrict__ twp,
+                                                    const TowerConst* __restrict__ tcs) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t N = 1u << logN;
+  const uint32_t BLK = N >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t poly = blockIdx.x / bpp;
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  const uint32_t t = (uint32_t)(poly % L);
+  const TowerConst& c = tcs[t];
+  const uint64_t q = c.q;
+  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+  uint64_t* __restrict__ a = polys + poly * N + col;
+  uint64_t x[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) x[r] = a[(uint64_t)r * BLK];
+#pragma unroll
+  for (int v = 0; v < LOGR; ++v) {
+    const int tr = 1 << v, h = R >> (v + 1);
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const uint64_t W = w[h + i], Wp = wp[h + i];
+#pragma unroll
+      for (int jj = 0; jj < tr; ++jj) {
+        const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+        const uint64_t U = x[r0], V = x[r1];
+        x[r0] = addmod(U, V, q);
+        x[r1] = shoup_mul(submod(U, V, q), W, Wp, q);
+      }
+    }
+  }
+  const uint64_t ni = c.ninv, nip = c.ninv_shoup;
+#pragma unroll
+  for (int r = 0; r < R; ++r) a[(uint64_t)r * BLK] = shoup_mul(x[r], ni, nip, q);
+}
+
+#define NTT_DISPATCH(LOGRV, KERNEL, ...)                                                   \
+  switch (LOGRV) {                                                                       \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                           \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                           \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                           \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                           \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break;                           \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                           \
+    default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};                  \
+  }
+
+void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
+                const DeviceTables& dt, hipStream_t s) {
+  if (!P) return;
+  const uint32_t N = 1u << logN;
+  const uint32_t blkLog = logN < (uint32_t)kNttBlockLog ? logN : (uint32_t)kNttBlockLog;
+  const int logR = (int)(logN - blkLog);
+  const uint32_t blk = 1u << blkLog;
+  const size_t lds = (size_t)blk * sizeof(uint64_t);
+  const uint64_t nbBlocks = P << logR;
+  const uint64_t nbCols = P * ((N >> logR) / 256);
+  if (nbBlocks > 0x7FFFFFFFull || nbCols > 0x7FFFFFFFull)
+    throw Error{SHELFI_ERR_ARG, "NTT batch too large"};
+  if (!inverse) {
+    if (logR > 0) {
+      NTT_DISPATCH(logR, ntt_fwd_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
+                   dt.psi_rev, dt.psi_rev_sh, dt.tc);
+    }
+    hipLaunchKernelGGL(ntt_fwd_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
+                       logN, (uint32_t)logR, dt.psi_rev, dt.psi_rev_sh, dt.tc);
+  } else {
+    hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
+                       logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0);
+    if (logR > 0) {
+      NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
+                   dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
+    }
+  }
+  SHELFI_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------- special FFT (f64) ----
+// FFTSpecialInv (encode): DIF stages len = S..2 with twiddle finv[len/2 + (x mod
+// len)], then BitReverse and /S (both folded into enc_prep).  First LOGR stages
+// on register columns (reading the learner's real vector directly), the rest in
+// LDS blocks of 2^kFftBlockLog complex values.
+template <int LOGR>
+__global__ __launch_bounds__(256) void fft_inv_cols(const double* __restrict__ x, uint64_t n,
+                                                    double2* __restrict__ buf, uint32_t logS,
+                                                    const double2* __restrict__ tw) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t S = 1u << logS;
+  const uint32_t BLK = S >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t k = blockIdx.x / bpp;
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  double2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t gi = k * S + col + (uint64_t)r * BLK;
+    v[r] = make_double2(gi < n ? x[gi] : 0.0, 0.0);
+  }
+#pragma unroll
+  for (int s = 0; s < LOGR; ++s) {
+    const uint32_t len = S >> s, lenh = len >> 1;
+    const int trr = R >> (s + 1);
+#pragma unroll
+    for (int r0 = 0; r0 < R; ++r0) {
+      if ((r0 / trr) % 2) continue;
+      const int r1 = r0 + trr;
+      const uint32_t j = (col + (uint32_t)r0 * BLK) & (len - 1);
+      const double2 W = tw[lenh + j];
+      const double2 u = cadd(v[r0], v[r1]);
+      const double2 d = csub(v[r0], v[r1]);
+      v[r0] = u;
+      v[r1] = cmul(d, W);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) buf[k * S + col + (uint64_t)r * BLK] = v[r];
+}
+
+__global__ __launch_bounds__(256) void fft_inv_blocks(const double* __restrict__ x, uint64_t n,
+                                                      double2* __restrict__ buf, uint32_t logS,
+                                                      uint32_t blkLog, int from_x,
+                                                      const double2* __restrict__ tw) {
+  extern __shared__ __attribute__((aligned(16))) double2 smc[];
+  const uint32_t S = 1u << logS, blk = 1u << blkLog;
+  const uint32_t sh = logS - blkLog;
+  const uint64_t k = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint64_t off = k * S + ((uint64_t)b << blkLog);
+  for (uint32_t i = threadIdx.x; i < blk; i += 256) {
+    if (from_x) {
+      const uint64_t gi = off + i;
+      smc[i] = make_double2(gi < n ? x[gi] : 0.0, 0.0);
+    } else {
+      smc[i] = buf[off + i];
+    }
+  }
+  __syncthreads();
+  for (uint32_t len = blk; len >= 2; len >>= 1) {
+    const uint32_t lenh = len >> 1;
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const uint32_t j = p & (lenh - 1);
+      const uint32_t i0 = (p - j) * 2 + j;
+      const double2 W = tw[lenh + j];
+      const double2 a0 = smc[i0], a1 = smc[i0 + lenh];
+      smc[i0] = cadd(a0, a1);
+      smc[i0 + lenh] = cmul(csub(a0, a1), W);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
+}
+
+// FFTSpecial (decode): input already bit-reversed by crt_decode's scatter; DIT
+// stages len = 2..S with twiddle ffwd[len/2 + (x mod len)].  Small len in LDS
+// blocks, the top LOGR stages on register columns; the last pass writes the real
+// parts of the first `n` slots straight into the caller's output vector.
+__global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf, uint32_t logS,
+                                                      uint32_t blkLog, const double2* __restrict__ tw,
+                                                      double* __restrict__ out, uint64_t n,
+                                                      int final_pass) {
+  extern __shared__ __attribute__((aligned(16))) double2 smc[];
+  const uint32_t S = 1u << logS, blk = 1u << blkLog;
+  const uint32_t sh = logS - blkLog;
+  const uint64_t k = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint64_t off = k * S + ((uint64_t)b << blkLog);
+  for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];
+  __syncthreads();
+  for (uint32_t len = 2; len <= blk; len <<= 1) {
+    const uint32_t lenh = len >> 1;
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const uint32_t j = p & (lenh - 1);
+      const uint32_t i0 = (p - j) * 2 + j;
+      const double2 W = tw[lenh + j];
+      const double2 u = smc[i0];
+      const double2 v = cmul(smc[i0 + lenh], W);
+      smc[i0] = cadd(u, v);
+      smc[i0 + lenh] = csub(u, v);
+    }
+    __syncthreads();
+  }
+  if (final_pass) {
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) {
+      const uint64_t gi = off + i;
+      if (gi < n) out[gi] = smc[i].x;
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
+  }
+}
+
+template <int LOGR>
+__global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ buf, uint32_t logS,
+                                                    const double2* __restrict__ tw,
+                                                    double* __restrict__ out, uint64_t n) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t S = 1u << logS;
+  const uint32_t BLK = S >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t k = blockIdx.x / bpp;
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  double2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = buf[k * S + col + (uint64_t)r * BLK];
+#pragma unroll
+  for (int s = 0; s < LOGR; ++s) {
+    const uint32_t lenh = BLK << s, len = lenh << 1;
+    const int tr = 1 << s;
+#pragma unroll
+    for (int r0 = 0; r0 < R; ++r0) {
+      if ((r0 >> s) & 1) continue;
+      const int r1 = r0 + tr;
+      const uint32_t j = (col + (uint32_t)r0 * BLK) & (len - 1);
+      const double2 W = tw[lenh + j];
+      const double2 u = v[r0];
+      const double2 w = cmul(v[r1], W);
+      v[r0] = cadd(u, w);
+      v[r1] = csub(u, w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t gi = k * S + col + (uint64_t)r * BLK;
+    if (gi < n) out[gi] = v[r].x;
+  }
+}
+
+#define FFT_DISPATCH(LOGRV, KERNEL, ...)                                                   \
+  switch (LOGRV) {                                                                       \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                           \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                           \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                           \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                           \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break;                           \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                           \
+    default: throw Error{SHELFI_ERR_ARG, "unsupported batch size"};                      \
+  }
+
+// ---------------------------------------------------------------- ChaCha20 ----
+struct Key8 {
+  uint32_t k[8];
+};
+#define CH_QR(a, b, c, d)                      \
+  a += b; d ^= a; d = __builtin_rotateleft32(d, 16); \
+  c += d; b ^= c; b = __builtin_rotateleft32(b, 12); \
+  a += b; d ^= a; d = __builtin_rotateleft32(d, 8);  \
+  c += d; b ^= c; b = __builtin_rotateleft32(b, 7);
+
+// RFC 8439 block function with a 64-bit counter (words 12-13) and 64-bit nonce
+// (words 14-15); out = 8 u64 words (2i, 2i+1).
+__device__ __forceinline__ void chacha20_block(const Key8& key, uint64_t counter, uint64_t nonce,
+                                               uint64_t out[8]) {
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
+                    (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce,
+                    (uint32_t)(nonce >> 32)};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = s[i];
+#pragma unroll 2
+  for (int i = 0; i < 10; ++i) {
+    CH_QR(x[0], x[4], x[8], x[12]);
+    CH_QR(x[1], x[5], x[9], x[13]);
+    CH_QR(x[2], x[6], x[10], x[14]);
+    CH_QR(x[3], x[7], x[11], x[15]);
+    CH_QR(x[0], x[5], x[10], x[15]);
+    CH_QR(x[1], x[6], x[11], x[12]);
+    CH_QR(x[2], x[7], x[8], x[13]);
+    CH_QR(x[3], x[4], x[9], x[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    out[i] = (uint64_t)(x[2 * i] + s[2 * i]) | ((uint64_t)(x[2 * i + 1] + s[2 * i + 1]) << 32);
+}
+
+__device__ __forceinline__ int64_t gauss_sample(uint64_t r, const uint64_t* __restrict__ cdt,
+                                                int T) {
+  const uint64_t u = r >> 1;
+  int64_t k = 0;
+  for (int i = 0; i < T; ++i) k += (u >= cdt[i]) ? 1 : 0;
+  return (r & 1) ? -k : k;
+}
+__device__ __forceinline__ int64_t ternary_sample(uint64_t r) { return (int64_t)(r % 3) - 1; }
+
+// -------------------------------------------------------------- encrypt ----
+// One thread = 8 consecutive coefficients of one ciphertext (one ChaCha20 block
+// per sampled polynomial).  m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at
+// j = i*gap (real) and N/2 + i*gap (imag) (CKKSPackedEncoding::Encode layout).
+// Writes [K][3][L][N]: v, m + e0, e1 reduced per tower (COEFFICIENT domain).
+__global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
+                                                       uint64_t K, uint32_t logN, uint32_t logS,
+                                                       uint32_t L, double delta,
+                                                       const TowerConst* __restrict__ tcs,
+                                                       const uint64_t* __restrict__ cdt, int T,
+                                                       Key8 key, uint64_t g0,
+                                                       uint64_t* __restrict__ out,
+                                                       uint32_t* __restrict__ flag) {
+  const uint32_t N = 1u << logN, S = 1u << logS;
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = gid >> (logN - 3);
+  if (k >= K) return;
+  const uint32_t j0 = (uint32_t)(gid & ((N >> 3) - 1)) * 8;
+  const uint64_t nonce = (1ull << 56) | (g0 + k);
+  uint64_t rv[8], re0[8], re1[8];
+  chacha20_block(key, j0 >> 3, nonce, rv);
+  chacha20_block(key, (N >> 3) + (j0 >> 3), nonce, re0);
+  chacha20_block(key, 2 * (N >> 3) + (j0 >> 3), nonce, re1);
+  const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
+  const double dS = (double)S;
+  const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
+  int64_t mv[8], vv[8], e1v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t j = j0 + u;
+    const uint32_t jj = j < half ? j : j - half;
+    int64_t m = 0;
+    if ((jj & ((1u << gapLog) - 1)) == 0) {
+      const uint32_t i = jj >> gapLog;
+      const double2 cv = fbuf[k * S + bitrev_dev(i, logS)];
+      const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
+      if (fabs(val) > lim) atomicOr(flag, 1u);
+      m = round_half_away(val);
+    }
+    vv[u] = ternary_sample(rv[u]);
+    mv[u] = m + gauss_sample(re0[u], cdt, T);
+    e1v[u] = gauss_sample(re1[u], cdt, T);
+  }
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst c = tcs[t];
+    ulonglong2* o0 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 0) * L + t) * N + j0);
+    ulonglong2* o1 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 1) * L + t) * N + j0);
+    ulonglong2* o2 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 2) * L + t) * N + j0);
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      o0[u / 2] = make_ulonglong2(mod_signed_dev(vv[u], c), mod_signed_dev(vv[u + 1], c));
+      o1[u / 2] = make_ulonglong2(mod_signed_dev(mv[u], c), mod_signed_dev(mv[u + 1], c));
+      o2[u / 2] = make_ulonglong2(mod_signed_dev(e1v[u], c), mod_signed_dev(e1v[u + 1], c));
+    }
+  }
+}
+
+// c0 = v*b + (m + e0), c1 = v*a + e1 (all EVALUATION).  One thread = 2 residues.
+__global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __restrict__ pbuf,
+                                                          uint64_t K, uint32_t logN, uint32_t L,
+                                                          const uint64_t* __restrict__ pk,
+                                                          const uint64_t* __restrict__ pksh,
+                                                          const TowerConst* __restrict__ tcs,
+                                                          uint64_t* __restrict__ ct) {
+  const uint32_t N = 1u << logN;
+  const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;  // over [K][L][N]
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t k = e / LN;
+  if (k >= K) return;
+  const uint64_t rem = e - k * LN;  // t*N + j
+  const uint32_t t = (uint32_t)(rem >> logN);
+  const uint64_t q = tcs[t].q;
+  const ulonglong2 V = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 0) * LN + rem);
+  const ulonglong2 M = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 1) * LN + rem);
+  const ulonglong2 E = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 2) * LN + rem);
+  const ulonglong2 B = *reinterpret_cast<const ulonglong2*>(pk + rem);
+  const ulonglong2 Bs = *reinterpret_cast<const ulonglong2*>(pksh + rem);
+  const ulonglong2 A = *reinterpret_cast<const ulonglong2*>(pk + LN + rem);
+  const ulonglong2 As = *reinterpret_cast<const ulonglong2*>(pksh + LN + rem);
+  ulonglong2 c0, c1;
+  c0.x = addmod(shoup_mul(V.x, B.x, Bs.x, q), M.x, q);
+  c0.y = addmod(shoup_mul(V.y, B.y, Bs.y, q), M.y, q);
+  c1.x = addmod(shoup_mul(V.x, A.x, As.x, q), E.x, q);
+  c1.y = addmod(shoup_mul(V.y, A.y, As.y, q), E.y, q);
+  *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 0) * LN + rem) = c0;
+  *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 1) * LN + rem) = c1;
+  (void)N;
+}
+
+size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
+  return K * (uint64_t)p.batch * sizeof(double2) + K * 3ull * p.L * p.N * sizeof(uint64_t);
+}
+
+void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
+                    uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
+                    uint64_t g0, uint32_t* flag, hipStream_t s) {
+  if (!K) return;
+  const uint32_t logS = __builtin_ctz(p.batch);
+  double2* fbuf = reinterpret_cast<double2*>(scratch);
+  uint64_t* pbuf = reinterpret_cast<uint64_t*>(fbuf + K * (uint64_t)p.batch);
+  // 1. FFTSpecialInv of each ciphertext's slot vector
+  const uint32_t blkLog = logS < (uint32_t)kFftBlockLog ? logS : (uint32_t)kFftBlockLog;
+  const int logR = (int)(logS - blkLog);
+  const size_t lds = sizeof(double2) << blkLog;
+  if (logR > 0) {
+    const uint64_t nb = K * ((p.batch >> logR) / 256);
+    FFT_DISPATCH(logR, fft_inv_cols, dim3((uint32_t)nb), dim3(256), 0, s, x, n, fbuf, logS,
+                 dt.fft_inv);
+    hipLaunchKernelGGL(fft_inv_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, x, n, fbuf,
+                       logS, blkLog, 0, dt.fft_inv);
+  } else {
+    hipLaunchKernelGGL(fft_inv_blocks, dim3((uint32_t)K), dim3(256), lds, s, x, n, fbuf, logS,
+                       blkLog, 1, dt.fft_inv);
+  }
+  SHELFI_HIP(hipGetLastError());
+  // 2. scale/round/reduce + sample
+  Key8 k8;
+  for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
+  const uint64_t threads = K * (p.N / 8);
+  hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
+                     fbuf, K, p.logN, logS, p.L, p.delta, dt.tc, dt.cdt, dt.cdt_len, k8, g0, pbuf,
+                     flag);
+  SHELFI_HIP(hipGetLastError());
+  // 3. NTT of the 3 L polynomials per ciphertext
+  launch_ntt(pbuf, K * 3 * p.L, p.L, p.logN, false, dt, s);
+  // 4. combine with the public key
+  const uint64_t pairs = K * (uint64_t)p.L * p.N / 2;
+  hipLaunchKernelGGL(enc_combine_kernel, dim3((uint32_t)((pairs + 255) / 256)), dim3(256), 0, s,
+                     pbuf, K, p.logN, p.L, dk.pk, dk.pk_sh, dt.tc, ct);
+  SHELFI_HIP(hipGetLastError());
+}
+
+// -------------------------------------------------------------- decrypt ----
+__global__ __launch_bounds__(256) void dec_combine_kernel(const uint64_t* __restrict__ ct,
+                                                          uint64_t K, uint32_t logN, uint32_t L,
+                                                          const uint64_t* __restrict__ sk,
+                                                          const uint64_t* __restrict__ sksh,
+                                                          const TowerConst* __restrict__ tcs,
+                                                          uint64_t* __restrict__ dbuf) {
+  const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;  // over [K][L][N]
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t k = e / LN;
+  if (k >= K) return;
+  const uint64_t rem = e - k * LN;
+  const uint32_t t = (uint32_t)(rem >> logN);
+  const uint64_t q = tcs[t].q;
+  const ulonglong2 c0 = *reinterpret_cast<const ulonglong2*>(ct + (k * 2 + 0) * LN + rem);
+  const ulonglong2 c1 = *reinterpret_cast<const ulonglong2*>(ct + (k * 2 + 1) * LN + rem);
+  const ulonglong2 s = *reinterpret_cast<const ulonglong2*>(sk + rem);
+  const ulonglong2 ss = *reinterpret_cast<const ulonglong2*>(sksh + rem);
+  ulonglong2 d;
+  d.x = addmod(c0.x, shoup_mul(c1.x, s.x, ss.x, q), q);
+  d.y = addmod(c0.y, shoup_mul(c1.y, s.y, ss.y, q), q);
+  *reinterpret_cast<ulonglong2*>(dbuf + e) = d;
+}
+
+// Exact centered CRT: y_t = b_t (Q/q_t)^-1 mod q_t; X = sum y_t (Q/q_t) - k Q with
+// k = round(sum y_t / q_t) (exact while |X| << Q/2), evaluated mod 2^128 and read
+// as a signed 128-bit integer; then (double)X * (1/scale) (PALISADE Decode:
+// ConvertToDouble * scalingFactorPre * 2^-p).  Written at bitrev(i) for FFTSpecial.
+__global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restrict__ dbuf,
+                                                         uint64_t K, uint32_t logN, uint32_t logS,
+                                                         uint32_t L,
+                                                         const TowerConst* __restrict__ tcs,
+                                                         uint64_t Qlo, uint64_t Qhi,
+                                                         double inv_scale,
+                                                         double2* __restrict__ fbuf) {
+  const uint32_t N = 1u << logN, S = 1u << logS;
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = gid >> logS;
+  if (k >= K) return;
+  const uint32_t i = (uint32_t)(gid & (S - 1));
+  const uint32_t gapLog = logN - 1 - logS;
+  const uint64_t* __restrict__ d = dbuf + k * ((uint64_t)L << logN);
+  double res[2];
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    const uint32_t j = (part ? (N >> 1) : 0) + (i << gapLog);
+    double frac = 0.0;
+    uint64_t xlo = 0, xhi = 0;
+    for (uint32_t t = 0; t < L; ++t) {
+      const TowerConst& c = tcs[t];
+      const uint64_t y = shoup_mul(d[((uint64_t)t << logN) + j], c.qhat_inv, c.qhat_inv_shoup, c.q);
+      frac += (double)y * c.inv_q;
+      const uint64_t plo = y * c.qhat_lo;
+      const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
+      xlo += plo;
+      xhi += phi + (xlo < plo ? 1 : 0);
+    }
+    const uint64_t kk = (uint64_t)(frac + 0.5);
+    const uint64_t slo = kk * Qlo;
+    const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
+    const uint64_t borrow = xlo < slo ? 1 : 0;
+    xlo -= slo;
+    xhi = xhi - shi - borrow;
+    // sign-magnitude -> double (the oracle's or_i128_to_double)
+    const bool neg = (int64_t)xhi < 0;
+    if (neg) {
+      xlo = ~xlo + 1;
+      xhi = ~xhi + (xlo == 0 ? 1 : 0);
+    }
+    double v = __dadd_rn(__dmul_rn((double)xhi, 18446744073709551616.0), (double)xlo);
+    if (neg) v = -v;
+    res[part] = __dmul_rn(v, inv_scale);
+  }
+  fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
+}
+
+size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
+  return K * (uint64_t)p.L * p.N * sizeof(uint64_t) + K * (uint64_t)p.batch * sizeof(double2);
+}
+
+void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
+                    const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
+                    void* scratch, hipStream_t s) {
+  if (!K) return;
+  const uint32_t logS = __builtin_ctz(p.batch);
+  uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
+  double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
+  const uint64_t pairs = K * (uint64_t)p.L * p.N / 2;
+  hipLaunchKernelGGL(dec_combine_kernel, dim3((uint32_t)((pairs + 255) / 256)), dim3(256), 0, s,
+                     ct, K, p.logN, p.L, dk.sk, dk.sk_sh, dt.tc, dbuf);
+  SHELFI_HIP(hipGetLastError());
+  launch_ntt(dbuf, K * p.L, p.L, p.logN, true, dt, s);
+  const uint64_t slots = K * (uint64_t)p.batch;
+  hipLaunchKernelGGL(crt_decode_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, s,
+                     dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
+                     fbuf);
+  SHELFI_HIP(hipGetLastError());
+  const uint32_t blkLog = logS < (uint32_t)kFftBlockLog ? logS : (uint32_t)kFftBlockLog;
+  const int logR = (int)(logS - blkLog);
+  const size_t lds = sizeof(double2) << blkLog;
+  hipLaunchKernelGGL(fft_fwd_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, fbuf, logS,
+                     blkLog, dt.fft_fwd, out, n, logR == 0 ? 1 : 0);
+  SHELFI_HIP(hipGetLastError());
+  if (logR > 0) {
+    const uint64_t nb = K * ((p.batch >> logR) / 256);
+    FFT_DISPATCH(logR, fft_fwd_cols, dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd,
+                 out, n);
+    SHELFI_HIP(hipGetLastError());
+  }
+}
+
+// --------------------------------------------------------------- keygen ----
+// s ternary (nonce 2<<56, words [0,N)), e Gaussian (words [N,2N)), a_t uniform
+// (nonce (2<<56)|(1+t), word pair (2j, 2j+1) -> 128-bit value mod q_t).
+__global__ __launch_bounds__(256) void keygen_sample_kernel(uint32_t logN, uint32_t L,
+                                                            const TowerConst* __restrict__ tcs,
+                                                            const uint64_t* __restrict__ cdt, int T,
+                                                            Key8 key, uint64_t* __restrict__ se,
+                                                            uint64_t* __restrict__ a_out) {
+  const uint32_t N = 1u << logN;
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (N >> 3)) return;
+  const uint32_t j0 = gid * 8;
+  const uint64_t nonce = 2ull << 56;
+  uint64_t rs[8], re[8];
+  chacha20_block(key, j0 >> 3, nonce, rs);
+  chacha20_block(key, (N >> 3) + (j0 >> 3), nonce, re);
+  int64_t sv[8], ev[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    sv[u] = ternary_sample(rs[u]);
+    ev[u] = gauss_sample(re[u], cdt, T);
+  }
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst c = tcs[t];
+    uint64_t ra[16];
+    chacha20_block(key, j0 >> 2, nonce | (1 + t), ra);
+    chacha20_block(key, (j0 >> 2) + 1, nonce | (1 + t), ra + 8);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      se[((uint64_t)0 * L + t) * N + j0 + u] = mod_signed_dev(sv[u], c);
+      se[((uint64_t)1 * L + t) * N + j0 + u] = mod_signed_dev(ev[u], c);
+      const uint64_t lo = ra[2 * u], hi = ra[2 * u + 1];
+      a_out[(uint64_t)t * N + j0 + u] =
+          addmod(shoup_mul(red64(hi, c.q, c.one_shoup), c.r64, c.r64_shoup, c.q),
+                 red64(lo, c.q, c.one_shoup), c.q);
+    }
+  }
+}
+
+// sk = NTT(s); b = NTT(e) - a * NTT(s)
+__global__ __launch_bounds__(256) void keygen_combine_kernel(const uint64_t* __restrict__ se,
+                                                             uint32_t logN, uint32_t L,
+                                                             const TowerConst* __restrict__ tcs,
+                                                             uint64_t* __restrict__ sk,
+                                                             uint64_t* __restrict__ pk) {
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= LN) return;
+  const uint32_t t = (uint32_t)(e >> logN);
+  const TowerConst c = tcs[t];
+  const uint64_t s = se[e], er = se[LN + e], a = pk[LN + e];
+  sk[e] = s;
+  pk[e] = submod(er, mulmod_generic(a, s, c), c.q);
+}
+
+size_t keygen_scratch_bytes(const Params& p) { return 2ull * p.L * p.N * sizeof(uint64_t); }
+
+void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
+                   uint64_t* pk, void* scratch, hipStream_t s) {
+  Key8 k8;
+  for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
+  uint64_t* se = reinterpret_cast<uint64_t*>(scratch);
+  const uint32_t th = p.N / 8;
+  hipLaunchKernelGGL(keygen_sample_kernel, dim3((th + 255) / 256), dim3(256), 0, s, p.logN, p.L,
+                     dt.tc, dt.cdt, dt.cdt_len, k8, se, pk + (uint64_t)p.L * p.N);
+  SHELFI_HIP(hipGetLastError());
+  launch_ntt(se, 2ull * p.L, p.L, p.logN, false, dt, s);
+  const uint64_t LN = (uint64_t)p.L * p.N;
+  hipLaunchKernelGGL(keygen_combine_kernel, dim3((uint32_t)((LN + 255) / 256)), dim3(256), 0, s,
+                     se, p.logN, p.L, dt.tc, sk, pk);
+  SHELFI_HIP(hipGetLastError());
+}
+
+}  // namespace shelfi

@@ -1,0 +1,142 @@
+// shelfi_internal.h — shared host-side declarations of libshelfi (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/shelfi.h"
+
+namespace shelfi {
+
+typedef unsigned __int128 u128;
+
+// ---------------------------------------------------------------- errors ----
+void set_error(const std::string& msg);
+struct Error {
+  int code;
+  std::string msg;
+};
+#define SHELFI_HIP(expr)                                                             \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      throw ::shelfi::Error{SHELFI_ERR_DEVICE, std::string(#expr) + ": " +           \
+                                                 hipGetErrorString(_e)};             \
+  } while (0)
+
+// ----------------------------------------------------------- host params ----
+constexpr int kMaxTowers = 16;
+constexpr int kFftBlockLog = 10;  // complex f64 block staged in LDS by FFT pass 2
+constexpr int kNttBlockLog = 11;  // u64 block staged in LDS by NTT pass 2
+
+struct Params {
+  uint32_t N = 0, logN = 0, L = 0, batch = 0, gap = 0, scale_bits = 0, first_mod_bits = 0;
+  uint64_t q[kMaxTowers] = {0};
+  uint64_t psi[kMaxTowers] = {0};
+  double delta = 0.0;  // (double)q[L-1]
+  double sigma = 3.19;
+};
+
+uint64_t powmod(uint64_t a, uint64_t e, uint64_t q);
+uint64_t invmod(uint64_t a, uint64_t q);
+uint64_t shoup(uint64_t w, uint64_t q);  // floor(w * 2^64 / q)
+uint64_t mod_signed(int64_t v, uint64_t q);
+bool is_prime(uint64_t n);
+uint32_t default_ring_dim(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits, uint32_t batch);
+void generate_chain(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
+                    uint64_t* q, uint64_t* psi);
+uint64_t min_root(uint64_t m, uint64_t q);
+void fft_twiddles(uint32_t slots, double* inv_re, double* inv_im, double* fwd_re, double* fwd_im);
+int gauss_cdt(double sigma, uint64_t* cdt, int max_entries);
+uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull);
+
+// ------------------------------------------------------- device constants ----
+// Per-tower constants, laid out for scalar (SGPR) loads in the kernels.
+struct TowerConst {
+  uint64_t q;
+  uint64_t one_shoup;     // floor(2^64 / q): x mod q for any u64 x via Shoup-by-1
+  uint64_t r30, r30_shoup;  // 2^30 mod q
+  uint64_t r60, r60_shoup;  // 2^60 mod q
+  uint64_t r64, r64_shoup;  // 2^64 mod q
+  uint64_t ninv, ninv_shoup;  // N^-1 mod q
+  uint64_t qhat_inv, qhat_inv_shoup;  // (Q/q_t)^-1 mod q_t
+  uint64_t qhat_lo, qhat_hi;  // (Q/q_t) mod 2^128
+  double inv_q;               // 1.0 / q (CRT k estimate)
+  uint64_t pad;
+};
+
+struct DeviceTables {
+  TowerConst* tc = nullptr;         // [L]
+  uint64_t* psi_rev = nullptr;      // [L][N]  psi^bitrev(i)
+  uint64_t* psi_rev_sh = nullptr;   // [L][N]  Shoup companions
+  uint64_t* ipsi_rev = nullptr;     // [L][N]  psi^-bitrev(i)
+  uint64_t* ipsi_rev_sh = nullptr;  // [L][N]
+  double2* fft_inv = nullptr;       // [B] flat special-FFT twiddles (FFTSpecialInv)
+  double2* fft_fwd = nullptr;       // [B] (FFTSpecial)
+  uint64_t* cdt = nullptr;          // Gaussian CDT [64]
+  int cdt_len = 0;
+  uint64_t qmod128_lo = 0, qmod128_hi = 0;  // Q mod 2^128
+};
+
+struct DeviceKeys {
+  uint64_t* pk = nullptr;     // [2][L][N]
+  uint64_t* pk_sh = nullptr;  // [2][L][N]
+  uint64_t* sk = nullptr;     // [L][N]
+  uint64_t* sk_sh = nullptr;  // [L][N]
+};
+
+}  // namespace shelfi
+
+struct shelfi_ctx {
+  shelfi::Params p;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  shelfi::DeviceTables dt;
+  shelfi::DeviceKeys dk;
+  std::vector<uint64_t> pk_host, sk_host;
+  bool keys_loaded = false;
+  bool palisade_keys = false;
+  uint64_t key_id = 0;
+  uint64_t params_id = 0;
+  uint64_t seed = 0;          // 0 -> OS entropy per call
+  uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
+  uint32_t* dev_flag = nullptr;  // device error flag (encode range)
+  // scratch arena (grown on demand, never shrunk)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* io = nullptr;            // bytes-API staging arena (inputs/outputs)
+  size_t io_bytes = 0;
+};
+
+namespace shelfi {
+
+// device-side launchers (kernels.hip)
+constexpr int kWavgMaxLearners = 16;  // per launch (limb sums stay < 2^64)
+struct WavgArgs {
+  const uint64_t* ptrs[kWavgMaxLearners];          // learner ciphertext batches (device)
+  uint32_t wl[kWavgMaxLearners][kMaxTowers][2];    // 30-bit limbs of W_{c,t}
+  uint64_t* out;
+  uint64_t rows;  // K * 2 * L
+  uint32_t C, L, logN, accumulate;
+};
+void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
+void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
+                 hipStream_t s);
+void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
+                const DeviceTables& dt, hipStream_t s);
+void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
+                    const double* x, uint64_t n, uint64_t K, uint64_t* ct, void* scratch,
+                    const uint32_t key[8], uint64_t g0, uint32_t* flag, hipStream_t s);
+size_t encrypt_scratch_bytes(const Params& p, uint64_t K);
+void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
+                    const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
+                    void* scratch, hipStream_t s);
+size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
+void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
+                   uint64_t* pk, void* scratch, hipStream_t s);
+size_t keygen_scratch_bytes(const Params& p);
+
+}  // namespace shelfi

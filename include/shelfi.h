@@ -1,0 +1,145 @@
+/*
+ * shelfi.h — C ABI of the MI355X-native CKKS weighted-average aggregator.
+ *
+ * Drop-in replacement for the compute behind the reference's pybind11 module
+ * SHELFI_FHE (palisade_pybind/SHELFI_FHE/src/binding.cpp:14-31, class CKKS in
+ * include/ckks.h:27-54 implementing Scheme in include/scheme.h:15-32).  Each
+ * entry point below names the reference method it replaces.  Plain C: opaque
+ * context, raw pointers and sizes, int status codes (0 = OK), a thread-local
+ * message via shelfi_last_error().  Caller-owned inputs are never retained;
+ * library-owned outputs are released with shelfi_free().
+ *
+ * All arithmetic runs in hand-written HIP kernels on an AMD Instinct MI355X
+ * (gfx950).  There is no CPU compute path: on a host without a usable gfx950
+ * device, shelfi_ctx_create() fails with SHELFI_ERR_DEVICE.
+ */
+#ifndef SHELFI_H_
+#define SHELFI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHELFI_ABI_VERSION 1
+
+/* status codes */
+#define SHELFI_OK 0
+#define SHELFI_ERR_ARG -1      /* bad argument (maps to ValueError) */
+#define SHELFI_ERR_DEVICE -2   /* HIP / device failure (RuntimeError) */
+#define SHELFI_ERR_IO -3       /* file read/write failure */
+#define SHELFI_ERR_FORMAT -4   /* malformed / mismatched ciphertext or key blob */
+#define SHELFI_ERR_STATE -5    /* keys not loaded, etc. */
+#define SHELFI_ERR_RANGE -6    /* value outside the CKKS encoding/decoding range */
+
+typedef struct shelfi_ctx shelfi_ctx;
+
+/* Parameters of a context (filled by shelfi_ctx_info). */
+typedef struct shelfi_info {
+  uint32_t ring_dim;       /* N */
+  uint32_t num_towers;     /* L = multDepth + 1 */
+  uint32_t batch;          /* slots per ciphertext (ckks.h:31 batchSize) */
+  uint32_t scale_bits;     /* ckks.h:32 scaleFactorBits */
+  uint32_t first_mod_bits; /* bits of q_0 */
+  int32_t device;          /* HIP device ordinal */
+  uint64_t moduli[16];     /* q_0 .. q_{L-1} */
+  uint64_t roots[16];      /* minimal primitive 2N-th roots psi_t */
+  double delta;            /* level-0 scaling factor = (double)q_{L-1} (EXACTRESCALE) */
+  uint64_t key_id;         /* 0 until keys are loaded/generated */
+  int32_t keys_loaded;
+  int32_t palisade_keys;   /* 1 if the keys came from PALISADE-format files */
+} shelfi_info;
+
+/* ---- library ------------------------------------------------------------ */
+int shelfi_abi_version(void);
+const char* shelfi_last_error(void);
+void shelfi_free(void* p);
+
+/* Host-only parameter generation (no device needed): PALISADE ParamsGen rule for
+ * EXACTRESCALE chains, as called by ckks.cpp:28 genCryptoContextCKKS(multDepth,
+ * scaleFactorBits, batchSize).  ring_dim = 0 picks the PALISADE ring dimension
+ * (HE-standard 128-bit classic, N >= 2*batch).  Writes L moduli and roots. */
+int shelfi_params_generate(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bits,
+                           uint32_t first_mod_bits, uint32_t batch, uint32_t* ring_dim_out,
+                           uint64_t* moduli_out, uint64_t* roots_out);
+
+/* Host-only PALISADE reader (no device needed): parses a reference cryptodir
+ * (cryptocontext.txt / key-public.txt / key-private.txt, ckks.cpp:11-23).  Call with
+ * q/psi/pk/sk = NULL to query N and L first; q/psi hold 16 entries, pk 2*L*N, sk L*N. */
+int shelfi_read_palisade(const char* cryptodir, uint32_t* ring_dim, uint32_t* num_towers,
+                         uint64_t* moduli, uint64_t* roots, uint64_t* pk, uint64_t* sk);
+
+/* ---- context lifecycle (ckks.cpp:5-9 CKKS::CKKS) -------------------------- */
+/* num_towers = multDepth + 1 (reference: multDepth = 1, ckks.cpp:26). */
+int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bits,
+                      uint32_t first_mod_bits, uint32_t batch, int device, shelfi_ctx** out);
+void shelfi_ctx_destroy(shelfi_ctx* ctx);
+int shelfi_ctx_info(const shelfi_ctx* ctx, shelfi_info* out);
+/* Deterministic ("parity") mode: encryption/keygen randomness derived from `seed`
+ * (ChaCha20 stream spec in DESIGN.md).  seed = 0 restores OS-entropy seeding. */
+int shelfi_set_seed(shelfi_ctx* ctx, uint64_t seed);
+
+/* ---- keys ----------------------------------------------------------------- */
+/* ckks.cpp:25-59 genCryptoContextAndKeyGen: generates keys on the device and writes
+ * cryptodir/{cryptocontext,key-public,key-private}.txt (this library's format). */
+int shelfi_keygen(shelfi_ctx* ctx, const char* cryptodir);
+/* ckks.cpp:11-23 loadCryptoParams: reads either this library's key files or the
+ * reference's PALISADE 1.11 cereal-binary files (code/resources/cryptoparams/). */
+int shelfi_load(shelfi_ctx* ctx, const char* cryptodir);
+/* Raw key import/export ([2][L][N] public (b, a), [L][N] secret, EVALUATION). */
+int shelfi_set_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk);
+int shelfi_get_keys(const shelfi_ctx* ctx, uint64_t* pk, uint64_t* sk);
+
+/* ---- bytes API (binding.cpp:26-31) ---------------------------------------- */
+/* ckks.cpp:61-104 encrypt: n doubles -> blob of ceil(n/batch) ciphertexts. */
+int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, size_t* out_len);
+/* ckks.cpp:264-320 computeWeightedAverage: C blobs, float32 weights (ckks.cpp:287). */
+int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                            const float* weights, size_t num_learners, uint8_t** out,
+                            size_t* out_len);
+/* ckks.cpp:170-213 decrypt: blob -> n doubles (caller-owned out[n]). */
+int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out);
+
+/* Blob inspection: number of ciphertexts, depth, scale, key id. */
+int shelfi_blob_info(const uint8_t* blob, size_t len, uint64_t* num_cts, uint32_t* depth,
+                     double* scale, uint64_t* key_id);
+/* Build a blob from raw residues [K][2][L][N] (host) with the given metadata. */
+int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t num_cts,
+                     uint32_t depth, double scale, uint8_t** out, size_t* out_len);
+/* Offset of the residue payload inside a blob (64-byte header). */
+size_t shelfi_blob_header_bytes(void);
+
+/* ---- device-resident batch API (HBM in, HBM out; `stream` = hipStream_t) ---- */
+/* Ciphertext batches are [K][2][L][N] uint64 in HBM (same order as the blob
+ * payload).  These calls enqueue work on `stream` and return without syncing. */
+
+/* sum_c W_c * in[c] mod q_t, W_c = (int64)((double)w[c] * delta + 0.5) (EvalMult +
+ * EvalAdd, ckks.cpp:286-297).  in_dev: host array of C device pointers. */
+int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float* w, size_t C,
+                    size_t K, uint64_t* out_dev, void* stream);
+/* Same arithmetic, result left unreduced in [0, 2^64) is NOT offered; instead the
+ * partial sum is reduced and a later shelfi_dev_modq() folds a collective's
+ * uint64 sum of G <= 16 partials back into [0, q_t). */
+int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream);
+/* encode + encrypt n doubles (device) into K = ceil(n/batch) ciphertexts. */
+int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
+                       void* stream);
+/* decrypt + decode K ciphertexts of scaling factor `scale` into n doubles (device). */
+int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double scale,
+                       size_t n, double* out_dev, void* stream);
+/* negacyclic NTT of P polys [P][N] whose tower is (p % L) (PALISADE order). */
+int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, void* stream);
+
+/* ---- test hooks (host-visible tables) ------------------------------------- */
+/* CKKS special-FFT twiddles (flat, index lenh + j) as used by the kernels. */
+int shelfi_fft_twiddles(uint32_t slots, double* inv_re, double* inv_im, double* fwd_re,
+                        double* fwd_im);
+/* Gaussian CDT thresholds used by the samplers; returns the entry count. */
+int shelfi_gauss_cdt(double sigma, uint64_t* cdt, int max_entries);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHELFI_H_ */

@@ -1,0 +1,817 @@
+/*
+ * ckks_oracle.c — CPU restatement of the SHELFI_FHE / PALISADE-1.11 CKKS hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker (or the timed
+ * CPU baseline).  The product (fhe-fed_amd/, libshelfi.so) never links, loads or
+ * calls it.
+ *
+ * Every routine is written for obviousness, not speed (u128 `%` for every modmul),
+ * except or_wavg_fast(), which is the Shoup-constant form used as the CPU baseline
+ * and is itself cross-checked against or_wavg() in tests.
+ *
+ * Citations are to /root/reference (palisade_pybind/SHELFI_FHE/...) and to
+ * PALISADE 1.11.7 behaviour, which is NOT vendored in the reference (see
+ * SURVEY.md App. A/B); PALISADE-only facts are tagged [PALISADE-1.11].
+ *
+ * Parity pinning:
+ *   - params (primes, minimal 2N-th roots) and NTT ordering are pinned by the
+ *     committed PALISADE context/key files (tests/golden/palisade*): the KAT
+ *     b + a*s == small e (test_oracle_kat.py) and the context's q/psi values;
+ *   - encode/decode floating-point order and decrypt noise flooding are NOT
+ *     pinned (PALISADE source absent) -> tolerance-level vs PALISADE;
+ *   - aggregation (EvalMult-by-constant + EvalAdd) is exact integer arithmetic,
+ *     pinned by construction once W = round((double)(float)w * q_last) is fixed.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+/* ------------------------------------------------------------------------ */
+/* integer helpers                                                          */
+/* ------------------------------------------------------------------------ */
+
+static inline uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) {
+  return (uint64_t)(((u128)a * b) % q);
+}
+static inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t q) {
+  uint64_t s = a + b;
+  return s >= q ? s - q : s;
+}
+static inline uint64_t submod(uint64_t a, uint64_t b, uint64_t q) {
+  return a >= b ? a - b : a + q - b;
+}
+uint64_t or_powmod(uint64_t a, uint64_t e, uint64_t q) {
+  uint64_t r = 1 % q;
+  a %= q;
+  while (e) {
+    if (e & 1) r = mulmod(r, a, q);
+    a = mulmod(a, a, q);
+    e >>= 1;
+  }
+  return r;
+}
+/* signed int64 -> [0,q).  PALISADE FitToNativeVector (ckkspackedencoding.cpp)
+ * maps negative v via (2^62-1+v) ModSub (2^62-1-q) == v mod q [PALISADE-1.11]. */
+uint64_t or_mod_signed(int64_t v, uint64_t q) {
+  if (v >= 0) return (uint64_t)v % q;
+  uint64_t m = (uint64_t)(-(v + 1)) + 1; /* |v| without overflow */
+  m %= q;
+  return m ? q - m : 0;
+}
+static uint64_t inv_mod(uint64_t a, uint64_t q) { return or_powmod(a, q - 2, q); }
+
+static uint32_t bitrev(uint32_t x, int bits) {
+  uint32_t r = 0;
+  for (int i = 0; i < bits; ++i) {
+    r = (r << 1) | (x & 1);
+    x >>= 1;
+  }
+  return r;
+}
+static int ilog2(uint64_t n) {
+  int l = 0;
+  while ((1ull << l) < n) ++l;
+  return l;
+}
+
+/* deterministic Miller-Rabin for all 64-bit n (bases = first 12 primes) */
+int or_is_prime(uint64_t n) {
+  static const uint64_t bases[12] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  if (n < 2) return 0;
+  for (int i = 0; i < 12; ++i) {
+    if (n == bases[i]) return 1;
+    if (n % bases[i] == 0) return 0;
+  }
+  uint64_t d = n - 1;
+  int s = 0;
+  while ((d & 1) == 0) {
+    d >>= 1;
+    ++s;
+  }
+  for (int i = 0; i < 12; ++i) {
+    uint64_t x = or_powmod(bases[i], d, n);
+    if (x == 1 || x == n - 1) continue;
+    int comp = 1;
+    for (int r = 1; r < s; ++r) {
+      x = mulmod(x, x, n);
+      if (x == n - 1) {
+        comp = 0;
+        break;
+      }
+    }
+    if (comp) return 0;
+  }
+  return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* parameter generation  (ckks.cpp:26-28 genCryptoContextCKKS(multDepth,...) */
+/* -> PALISADE ParamsGen; prime rule recovered in SURVEY App. A)             */
+/* ------------------------------------------------------------------------ */
+
+/* PALISADE FirstPrime(nBits, m): smallest prime q > 2^nBits with q == 1 mod m
+ * (m a power of two <= 2^nBits, so the search starts at 2^nBits + 1). */
+uint64_t or_first_prime(uint32_t bits, uint64_t m) {
+  uint64_t q = (1ull << bits) + 1;
+  while (!or_is_prime(q)) q += m;
+  return q;
+}
+uint64_t or_prev_prime(uint64_t q, uint64_t m) {
+  do { q -= m; } while (!or_is_prime(q));
+  return q;
+}
+uint64_t or_next_prime(uint64_t q, uint64_t m) {
+  do { q += m; } while (!or_is_prime(q));
+  return q;
+}
+
+/* PALISADE RootOfUnity(m, q): the MINIMUM primitive m-th root of unity
+ * (it cycles a found root over all powers co-prime to m and keeps the
+ * smallest) [PALISADE-1.11; verified against cryptocontext.txt@1935,@1984]. */
+uint64_t or_min_root(uint64_t m, uint64_t q) {
+  uint64_t r = 0;
+  for (uint64_t g = 2;; ++g) {
+    r = or_powmod(g, (q - 1) / m, q);
+    if (or_powmod(r, m / 2, q) == q - 1) break; /* order exactly m (m = 2^k) */
+  }
+  uint64_t r2 = mulmod(r, r, q), x = r, best = r;
+  for (uint64_t k = 1; k < m / 2; ++k) { /* x = r^(2k+1): all odd powers */
+    x = mulmod(x, r2, q);
+    if (x < best) best = x;
+  }
+  return best;
+}
+
+/* EXACTRESCALE chain: q[L-1] = FirstPrime(scaleBits, 2N); then alternately
+ * PreviousPrime / NextPrime walking outwards; q[0] = PreviousPrime(
+ * FirstPrime(firstModBits, 2N)).  Reproduces the committed 2-tower chain
+ * (cryptocontext.txt@1927,@1976) and TCT1's 3-tower chain [SURVEY App. A]. */
+int or_params_generate(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
+                       uint64_t* q, uint64_t* psi) {
+  if (L < 1 || L > 16 || N < 8 || (N & (N - 1))) return -1;
+  uint64_t m = 2ull * N;
+  q[L - 1] = or_first_prime(scale_bits, m);
+  uint64_t qprev = q[L - 1], qnext = q[L - 1];
+  unsigned cnt = 0;
+  for (int i = (int)L - 2; i >= 1; --i) {
+    if ((cnt % 2) == 0) {
+      qprev = or_prev_prime(qprev, m);
+      q[i] = qprev;
+    } else {
+      qnext = or_next_prime(qnext, m);
+      q[i] = qnext;
+    }
+    ++cnt;
+  }
+  if (L > 1) {
+    if (first_mod_bits == scale_bits)
+      q[0] = or_prev_prime(qprev, m);
+    else
+      q[0] = or_prev_prime(or_first_prime(first_mod_bits, m), m);
+  }
+  for (uint32_t i = 0; i < L; ++i) psi[i] = or_min_root(m, q[i]);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* negacyclic NTT, PALISADE convention (ChineseRemainderTransformFTT)        */
+/* forward: out[i] = a(psi^(2*bitrev(i)+1)) (bit-reversed evaluation order), */
+/* inverse: natural-order coefficients.  Pinned by the key KAT.              */
+/* ------------------------------------------------------------------------ */
+
+void or_ntt_fwd(uint64_t* a, uint32_t N, uint64_t q, uint64_t psi) {
+  int logN = ilog2(N);
+  uint64_t* tw = (uint64_t*)malloc(sizeof(uint64_t) * N);
+  uint64_t p = 1;
+  for (uint32_t i = 0; i < N; ++i) {
+    tw[bitrev(i, logN)] = p;
+    p = mulmod(p, psi, q);
+  }
+  uint32_t t = N;
+  for (uint32_t m = 1; m < N; m <<= 1) {
+    t >>= 1;
+    for (uint32_t i = 0; i < m; ++i) {
+      uint64_t S = tw[m + i];
+      uint32_t j1 = 2 * i * t;
+      for (uint32_t j = j1; j < j1 + t; ++j) {
+        uint64_t U = a[j], V = mulmod(a[j + t], S, q);
+        a[j] = addmod(U, V, q);
+        a[j + t] = submod(U, V, q);
+      }
+    }
+  }
+  free(tw);
+}
+
+void or_ntt_inv(uint64_t* a, uint32_t N, uint64_t q, uint64_t psi) {
+  int logN = ilog2(N);
+  uint64_t psi_inv = inv_mod(psi, q);
+  uint64_t* tw = (uint64_t*)malloc(sizeof(uint64_t) * N);
+  uint64_t p = 1;
+  for (uint32_t i = 0; i < N; ++i) {
+    tw[bitrev(i, logN)] = p;
+    p = mulmod(p, psi_inv, q);
+  }
+  uint32_t t = 1;
+  for (uint32_t m = N; m > 1; m >>= 1) {
+    uint32_t h = m >> 1, j1 = 0;
+    for (uint32_t i = 0; i < h; ++i) {
+      uint64_t S = tw[h + i];
+      for (uint32_t j = j1; j < j1 + t; ++j) {
+        uint64_t U = a[j], V = a[j + t];
+        a[j] = addmod(U, V, q);
+        a[j + t] = mulmod(submod(U, V, q), S, q);
+      }
+      j1 += 2 * t;
+    }
+    t <<= 1;
+  }
+  uint64_t ninv = inv_mod(N % q, q);
+  for (uint32_t j = 0; j < N; ++j) a[j] = mulmod(a[j], ninv, q);
+  free(tw);
+}
+
+/* ------------------------------------------------------------------------ */
+/* CKKS special FFT (PALISADE DiscreteFourierTransform::FFTSpecial[Inv],     */
+/* HEAAN layout).  M = 4*slots; ksi[j] = (cos 2pi j/M, sin 2pi j/M);          */
+/* rotGroup[j] = 5^j mod M.  Complex products are (ac-bd, ad+bc) with no FMA */
+/* contraction (built with -ffp-contract=off) — the product kernels follow   */
+/* the identical operation order, which is what makes encode/decode bit-exact */
+/* GPU-vs-oracle.  Oracle-vs-PALISADE float order: unpinned (tolerance).     */
+/* ------------------------------------------------------------------------ */
+
+/* Flat twiddle tables, index lenh + j (lenh = 1..slots/2, j < lenh):
+ *   inv: ksi[(lenq - rot[j] % lenq) * (M/lenq)],  fwd: ksi[(rot[j] % lenq) * (M/lenq)]
+ * with lenq = 4*len = 8*lenh.  Exported so the product library's tables can be
+ * compared value-for-value in tests. */
+void or_fft_twiddles(uint32_t slots, double* inv_re, double* inv_im, double* fwd_re,
+                     double* fwd_im) {
+  uint64_t M = 4ull * slots;
+  uint64_t* rot = (uint64_t*)malloc(sizeof(uint64_t) * (slots > 0 ? slots : 1));
+  uint64_t f = 1;
+  for (uint32_t j = 0; j < slots; ++j) {
+    rot[j] = f;
+    f = (f * 5) % M;
+  }
+  inv_re[0] = inv_im[0] = fwd_re[0] = fwd_im[0] = 0.0;
+  for (uint32_t lenh = 1; lenh < slots; lenh <<= 1) {
+    uint64_t lenq = 8ull * lenh;
+    uint64_t gap = M / lenq;
+    for (uint32_t j = 0; j < lenh; ++j) {
+      uint64_t ii = ((lenq - (rot[j] % lenq)) * gap) % M; /* ksi[M] == ksi[0] */
+      uint64_t fi = ((rot[j] % lenq) * gap) % M;
+      double ai = 2.0 * M_PI * (double)ii / (double)M;
+      double af = 2.0 * M_PI * (double)fi / (double)M;
+      inv_re[lenh + j] = cos(ai);
+      inv_im[lenh + j] = sin(ai);
+      fwd_re[lenh + j] = cos(af);
+      fwd_im[lenh + j] = sin(af);
+    }
+  }
+  free(rot);
+}
+
+static void bitrev_perm(double* re, double* im, uint32_t n) {
+  int lg = ilog2(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t r = bitrev(i, lg);
+    if (r > i) {
+      double t = re[i]; re[i] = re[r]; re[r] = t;
+      t = im[i]; im[i] = im[r]; im[r] = t;
+    }
+  }
+}
+
+/* FFTSpecialInv: DIF stages len = n..2, BitReverse, then /n. */
+void or_fft_special_inv(double* re, double* im, uint32_t n) {
+  double *tr = malloc(sizeof(double) * n), *ti = malloc(sizeof(double) * n);
+  double *fr = malloc(sizeof(double) * n), *fi = malloc(sizeof(double) * n);
+  or_fft_twiddles(n, tr, ti, fr, fi);
+  for (uint32_t len = n; len >= 2; len >>= 1) {
+    uint32_t lenh = len >> 1;
+    for (uint32_t i = 0; i < n; i += len) {
+      for (uint32_t j = 0; j < lenh; ++j) {
+        double ar = re[i + j], ai = im[i + j];
+        double br = re[i + j + lenh], bi = im[i + j + lenh];
+        double ur = ar + br, ui = ai + bi;
+        double vr = ar - br, vi = ai - bi;
+        double wr = tr[lenh + j], wi = ti[lenh + j];
+        double xr = vr * wr - vi * wi;
+        double xi = vr * wi + vi * wr;
+        re[i + j] = ur; im[i + j] = ui;
+        re[i + j + lenh] = xr; im[i + j + lenh] = xi;
+      }
+    }
+  }
+  bitrev_perm(re, im, n);
+  double dn = (double)n;
+  for (uint32_t i = 0; i < n; ++i) {
+    re[i] /= dn;
+    im[i] /= dn;
+  }
+  free(tr); free(ti); free(fr); free(fi);
+}
+
+/* FFTSpecial: BitReverse, then DIT stages len = 2..n. */
+void or_fft_special(double* re, double* im, uint32_t n) {
+  double *tr = malloc(sizeof(double) * n), *ti = malloc(sizeof(double) * n);
+  double *fr = malloc(sizeof(double) * n), *fi = malloc(sizeof(double) * n);
+  or_fft_twiddles(n, tr, ti, fr, fi);
+  bitrev_perm(re, im, n);
+  for (uint32_t len = 2; len <= n; len <<= 1) {
+    uint32_t lenh = len >> 1;
+    for (uint32_t i = 0; i < n; i += len) {
+      for (uint32_t j = 0; j < lenh; ++j) {
+        double ur = re[i + j], ui = im[i + j];
+        double br = re[i + j + lenh], bi = im[i + j + lenh];
+        double wr = fr[lenh + j], wi = fi[lenh + j];
+        double vr = br * wr - bi * wi;
+        double vi = br * wi + bi * wr;
+        re[i + j] = ur + vr; im[i + j] = ui + vi;
+        re[i + j + lenh] = ur - vr; im[i + j + lenh] = ui - vi;
+      }
+    }
+  }
+  free(tr); free(ti); free(fr); free(fi);
+}
+
+/* llround (ties away from zero) written so it is reproducible bit-for-bit by
+ * the GPU kernels: t = trunc(x); |x - t| >= 0.5 -> step away from zero. */
+int64_t or_round_half_away(double x) {
+  double t = trunc(x);
+  double d = x - t;
+  if (d >= 0.5) t += 1.0;
+  else if (d <= -0.5) t -= 1.0;
+  return (int64_t)t;
+}
+
+/* ------------------------------------------------------------------------ */
+/* encode  (ckks.cpp:80 MakeCKKSPackedPlaintext -> CKKSPackedEncoding::Encode)*/
+/* ------------------------------------------------------------------------ */
+
+/* x[0..n) (n <= slots) -> signed coefficient vector coeff[N] (COEFFICIENT
+ * domain, before the per-tower reduction).  Returns -2 if some scaled value
+ * exceeds 2^61 (PALISADE's approxFactor path; not implemented — the product
+ * rejects such inputs the same way). */
+int or_encode_coeffs(const double* x, size_t n, uint32_t N, uint32_t slots, double delta,
+                     int64_t* coeff) {
+  if (n > slots || 2ull * slots > N) return -1;
+  double* re = calloc(slots, sizeof(double));
+  double* im = calloc(slots, sizeof(double));
+  for (size_t i = 0; i < n; ++i) re[i] = x[i];
+  or_fft_special_inv(re, im, slots);
+  uint32_t gap = N / (2 * slots);
+  memset(coeff, 0, sizeof(int64_t) * N);
+  int rc = 0;
+  const double lim = 2305843009213693952.0; /* 2^61 */
+  for (uint32_t i = 0; i < slots; ++i) {
+    double vr = re[i] * delta, vi = im[i] * delta;
+    if (fabs(vr) > lim || fabs(vi) > lim) rc = -2;
+    coeff[i * gap] = or_round_half_away(vr);
+    coeff[N / 2 + i * gap] = or_round_half_away(vi);
+  }
+  free(re);
+  free(im);
+  return rc;
+}
+
+/* full encode: coeffs -> per-tower residues -> NTT (EVALUATION). out[L][N]. */
+int or_encode(const double* x, size_t n, uint32_t N, uint32_t slots, double delta, uint32_t L,
+              const uint64_t* q, const uint64_t* psi, uint64_t* out) {
+  int64_t* c = malloc(sizeof(int64_t) * N);
+  int rc = or_encode_coeffs(x, n, N, slots, delta, c);
+  if (rc) {
+    free(c);
+    return rc;
+  }
+  for (uint32_t t = 0; t < L; ++t) {
+    for (uint32_t j = 0; j < N; ++j) out[(size_t)t * N + j] = or_mod_signed(c[j], q[t]);
+    or_ntt_fwd(out + (size_t)t * N, N, q[t], psi[t]);
+  }
+  free(c);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* encrypt with injected randomness (ckks.cpp:81 cc->Encrypt(pk, pt))        */
+/* v ternary, e0/e1 Gaussian, all COEFFICIENT-domain signed, same integers in */
+/* every tower; c0 = NTT(v)*b + NTT(e0) + m, c1 = NTT(v)*a + NTT(e1)         */
+/* [PALISADE-1.11 LPAlgorithmCKKS::Encrypt].  pk[2][L][N], m[L][N] EVAL.      */
+/* ------------------------------------------------------------------------ */
+void or_encrypt(const uint64_t* pk, const uint64_t* m, const int64_t* v, const int64_t* e0,
+                const int64_t* e1, uint32_t N, uint32_t L, const uint64_t* q,
+                const uint64_t* psi, uint64_t* ct /* [2][L][N] */) {
+  uint64_t* V = malloc(sizeof(uint64_t) * N);
+  uint64_t* E0 = malloc(sizeof(uint64_t) * N);
+  uint64_t* E1 = malloc(sizeof(uint64_t) * N);
+  for (uint32_t t = 0; t < L; ++t) {
+    for (uint32_t j = 0; j < N; ++j) {
+      V[j] = or_mod_signed(v[j], q[t]);
+      E0[j] = or_mod_signed(e0[j], q[t]);
+      E1[j] = or_mod_signed(e1[j], q[t]);
+    }
+    or_ntt_fwd(V, N, q[t], psi[t]);
+    or_ntt_fwd(E0, N, q[t], psi[t]);
+    or_ntt_fwd(E1, N, q[t], psi[t]);
+    const uint64_t* b = pk + (size_t)t * N;
+    const uint64_t* a = pk + ((size_t)L + t) * N;
+    const uint64_t* mt = m + (size_t)t * N;
+    uint64_t* c0 = ct + (size_t)t * N;
+    uint64_t* c1 = ct + ((size_t)L + t) * N;
+    for (uint32_t j = 0; j < N; ++j) {
+      c0[j] = addmod(addmod(mulmod(V[j], b[j], q[t]), E0[j], q[t]), mt[j], q[t]);
+      c1[j] = addmod(mulmod(V[j], a[j], q[t]), E1[j], q[t]);
+    }
+  }
+  free(V);
+  free(E0);
+  free(E1);
+}
+
+/* keygen with injected randomness [PALISADE-1.11 LPAlgorithmCKKS::KeyGen]:
+ * s ternary, e Gaussian (coefficient domain, shared across towers), a uniform
+ * per tower (sampled directly in EVAL); b = NTT(e) - a*NTT(s).
+ * outputs: sk[L][N] = NTT(s), pk[2][L][N] = (b, a). a_eval given [L][N]. */
+void or_keygen(const int64_t* s, const int64_t* e, const uint64_t* a_eval, uint32_t N, uint32_t L,
+               const uint64_t* q, const uint64_t* psi, uint64_t* sk, uint64_t* pk) {
+  uint64_t* E = malloc(sizeof(uint64_t) * N);
+  for (uint32_t t = 0; t < L; ++t) {
+    uint64_t* S = sk + (size_t)t * N;
+    for (uint32_t j = 0; j < N; ++j) {
+      S[j] = or_mod_signed(s[j], q[t]);
+      E[j] = or_mod_signed(e[j], q[t]);
+    }
+    or_ntt_fwd(S, N, q[t], psi[t]);
+    or_ntt_fwd(E, N, q[t], psi[t]);
+    const uint64_t* a = a_eval + (size_t)t * N;
+    for (uint32_t j = 0; j < N; ++j) {
+      pk[(size_t)t * N + j] = submod(E[j], mulmod(a[j], S[j], q[t]), q[t]);
+      pk[((size_t)L + t) * N + j] = a[j];
+    }
+  }
+  free(E);
+}
+
+/* ------------------------------------------------------------------------ */
+/* weighted average  (ckks.cpp:264-320 computeWeightedAverage)               */
+/* per learner i: float sc = w_i (:287); EvalMult(ct, sc) (:288) scales every */
+/* residue by W_t = W mod q_t with W = (int64)((double)sc * Delta0 + 0.5)     */
+/* [PALISADE-1.11 EvalMult(ct,double)]; EvalAdd (:295-296) adds mod q_t.      */
+/* ------------------------------------------------------------------------ */
+
+int64_t or_weight_to_int(float w, double delta0) {
+  return (int64_t)((double)w * delta0 + 0.5);
+}
+
+/* cts[c] -> [K][2][L][N]; out [K][2][L][N].  Reference form (u128 %). */
+void or_wavg(const uint64_t* const* cts, const float* w, size_t C, size_t K, uint32_t N,
+             uint32_t L, const uint64_t* q, double delta0, uint64_t* out) {
+  uint64_t* W = malloc(sizeof(uint64_t) * C * L);
+  for (size_t c = 0; c < C; ++c) {
+    int64_t Wi = or_weight_to_int(w[c], delta0);
+    for (uint32_t t = 0; t < L; ++t) W[c * L + t] = or_mod_signed(Wi, q[t]);
+  }
+  size_t per_ct = 2ull * L * N;
+  for (size_t k = 0; k < K; ++k)
+    for (uint32_t p = 0; p < 2; ++p)
+      for (uint32_t t = 0; t < L; ++t) {
+        size_t base = k * per_ct + ((size_t)p * L + t) * N;
+        for (uint32_t j = 0; j < N; ++j) {
+          uint64_t acc = 0;
+          for (size_t c = 0; c < C; ++c)
+            acc = addmod(acc, mulmod(cts[c][base + j], W[c * L + t], q[t]), q[t]);
+          out[base + j] = acc;
+        }
+      }
+  free(W);
+}
+
+/* CPU-baseline form: Shoup constant multiplication (what PALISADE's
+ * NativeVector::ModMul-by-constant does per tower), optional OpenMP over the
+ * (ct, poly, tower) rows.  nthreads <= 0 -> single thread. */
+void or_wavg_fast(const uint64_t* const* cts, const float* w, size_t C, size_t K, uint32_t N,
+                  uint32_t L, const uint64_t* q, double delta0, uint64_t* out, int nthreads) {
+  uint64_t* W = malloc(sizeof(uint64_t) * C * L);
+  uint64_t* Wp = malloc(sizeof(uint64_t) * C * L);
+  for (size_t c = 0; c < C; ++c) {
+    int64_t Wi = or_weight_to_int(w[c], delta0);
+    for (uint32_t t = 0; t < L; ++t) {
+      W[c * L + t] = or_mod_signed(Wi, q[t]);
+      Wp[c * L + t] = (uint64_t)(((u128)W[c * L + t] << 64) / q[t]);
+    }
+  }
+  long rows = (long)(K * 2 * L);
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+  for (long r = 0; r < rows; ++r) {
+    uint32_t t = (uint32_t)(r % L);
+    uint64_t qt = q[t];
+    size_t base = (size_t)r * N;
+    uint64_t* o = out + base;
+    for (uint32_t j = 0; j < N; ++j) o[j] = 0;
+    for (size_t c = 0; c < C; ++c) {
+      const uint64_t* x = cts[c] + base;
+      uint64_t w0 = W[c * L + t], wp = Wp[c * L + t];
+      for (uint32_t j = 0; j < N; ++j) {
+        uint64_t hi = (uint64_t)(((u128)x[j] * wp) >> 64);
+        uint64_t rr = x[j] * w0 - hi * qt;
+        if (rr >= qt) rr -= qt;
+        uint64_t s = o[j] + rr;
+        o[j] = s >= qt ? s - qt : s;
+      }
+    }
+  }
+  free(W);
+  free(Wp);
+}
+
+/* ------------------------------------------------------------------------ */
+/* decrypt + decode  (ckks.cpp:170-213 -> cc->Decrypt(sk, ct, &pt) :189,    */
+/* SetLength :198, GetRealPackedValue :199).                                 */
+/* b = c0 + c1*s (EVAL) -> INTT -> exact CRT to the centered integer mod Q   */
+/* -> (double)X * (1/scale) -> FFTSpecial -> real parts.  PALISADE's Decode   */
+/* additionally symmetrises and adds Gaussian flooding noise [PALISADE-1.11]; */
+/* the restatement returns the noise-free value (Re of the slot), which is    */
+/* what the symmetrisation computes before the noise.                         */
+/* ------------------------------------------------------------------------ */
+
+/* multiword helpers for the exact CRT (little-endian u64 limbs) */
+#define MW 10
+static void mw_mul_small(const uint64_t* a, uint64_t b, uint64_t* r) {
+  u128 carry = 0;
+  for (int i = 0; i < MW; ++i) {
+    u128 p = (u128)a[i] * b + carry;
+    r[i] = (uint64_t)p;
+    carry = p >> 64;
+  }
+}
+static void mw_add(uint64_t* a, const uint64_t* b) {
+  u128 carry = 0;
+  for (int i = 0; i < MW; ++i) {
+    u128 s = (u128)a[i] + b[i] + carry;
+    a[i] = (uint64_t)s;
+    carry = s >> 64;
+  }
+}
+static int mw_cmp(const uint64_t* a, const uint64_t* b) {
+  for (int i = MW - 1; i >= 0; --i) {
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  }
+  return 0;
+}
+static void mw_sub(uint64_t* a, const uint64_t* b) {
+  uint64_t borrow = 0;
+  for (int i = 0; i < MW; ++i) {
+    u128 d = (u128)a[i] - b[i] - borrow;
+    a[i] = (uint64_t)d;
+    borrow = (uint64_t)((d >> 64) & 1);
+  }
+}
+
+/* i128 -> double, the conversion the product kernels use: sign-magnitude, then
+ * (double)mag_hi * 2^64 + (double)mag_lo (exact for |X| < 2^64). */
+double or_i128_to_double(int64_t hi, uint64_t lo) {
+  int neg = hi < 0;
+  uint64_t mh = (uint64_t)hi, ml = lo;
+  if (neg) { /* two's-complement negate of (hi, lo) */
+    ml = ~ml + 1;
+    mh = ~mh + (ml == 0 ? 1 : 0);
+  }
+  double d = (double)mh * 18446744073709551616.0 + (double)ml;
+  return neg ? -d : d;
+}
+
+/* exact centered CRT of residues r[t] (t < L) -> (hi, lo) two's complement
+ * i128; returns 0, or -3 if |X| >= 2^127 (out of the product's range). */
+int or_crt_centered(const uint64_t* r, uint32_t L, const uint64_t* q, int64_t* hi,
+                    uint64_t* lo) {
+  uint64_t Q[MW] = {0}, X[MW] = {0}, tmp[MW], qhat[MW];
+  Q[0] = 1;
+  for (uint32_t t = 0; t < L; ++t) {
+    mw_mul_small(Q, q[t], tmp);
+    memcpy(Q, tmp, sizeof(Q));
+  }
+  for (uint32_t t = 0; t < L; ++t) {
+    memset(qhat, 0, sizeof(qhat));
+    qhat[0] = 1;
+    uint64_t qhat_mod = 1;
+    for (uint32_t u = 0; u < L; ++u)
+      if (u != t) {
+        mw_mul_small(qhat, q[u], tmp);
+        memcpy(qhat, tmp, sizeof(qhat));
+        qhat_mod = mulmod(qhat_mod, q[u] % q[t], q[t]);
+      }
+    uint64_t y = mulmod(r[t], inv_mod(qhat_mod, q[t]), q[t]);
+    mw_mul_small(qhat, y, tmp);
+    mw_add(X, tmp);
+  }
+  while (mw_cmp(X, Q) >= 0) mw_sub(X, Q);
+  /* center: X > Q/2 -> X - Q (negative) */
+  uint64_t half[MW];
+  memcpy(half, Q, sizeof(Q));
+  for (int i = 0; i < MW; ++i) half[i] = (Q[i] >> 1) | (i + 1 < MW ? Q[i + 1] << 63 : 0);
+  int neg = mw_cmp(X, half) > 0;
+  if (neg) { /* |X| = Q - X */
+    uint64_t A[MW];
+    memcpy(A, Q, sizeof(Q));
+    mw_sub(A, X);
+    memcpy(X, A, sizeof(A));
+  }
+  for (int i = 2; i < MW; ++i)
+    if (X[i]) return -3;
+  if (X[1] >> 63) return -3;
+  u128 mag = ((u128)X[1] << 64) | X[0];
+  i128 v = neg ? -(i128)mag : (i128)mag;
+  *hi = (int64_t)(v >> 64);
+  *lo = (uint64_t)v;
+  return 0;
+}
+
+/* decrypt one ciphertext ct[2][L][N] with sk[L][N] (EVAL).  Writes the first
+ * `n` real slot values to out.  Returns 0 / negative on error. */
+int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
+               const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
+               size_t n, double* out) {
+  if (n > slots) return -1;
+  uint64_t* b = malloc(sizeof(uint64_t) * L * N);
+  for (uint32_t t = 0; t < L; ++t) {
+    const uint64_t* c0 = ct + (size_t)t * N;
+    const uint64_t* c1 = ct + ((size_t)L + t) * N;
+    const uint64_t* s = sk + (size_t)t * N;
+    uint64_t* bt = b + (size_t)t * N;
+    for (uint32_t j = 0; j < N; ++j) bt[j] = addmod(c0[j], mulmod(c1[j], s[j], q[t]), q[t]);
+    or_ntt_inv(bt, N, q[t], psi[t]);
+  }
+  double inv_scale = 1.0 / scale;
+  uint32_t gap = N / (2 * slots);
+  double* re = malloc(sizeof(double) * slots);
+  double* im = malloc(sizeof(double) * slots);
+  uint64_t r[16];
+  int rc = 0;
+  for (uint32_t i = 0; i < slots && !rc; ++i) {
+    for (int part = 0; part < 2 && !rc; ++part) {
+      uint32_t j = (part ? N / 2 : 0) + i * gap;
+      for (uint32_t t = 0; t < L; ++t) r[t] = b[(size_t)t * N + j];
+      int64_t hi;
+      uint64_t lo;
+      rc = or_crt_centered(r, L, q, &hi, &lo);
+      double v = or_i128_to_double(hi, lo) * inv_scale;
+      if (part) im[i] = v; else re[i] = v;
+    }
+  }
+  if (!rc) {
+    or_fft_special(re, im, slots);
+    for (size_t i = 0; i < n; ++i) out[i] = re[i];
+  }
+  free(re);
+  free(im);
+  free(b);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Randomness spec of the product (NOT PALISADE's Blake2 PRNG, which is      */
+/* seeded from std::random_device and cannot be reproduced).  Restated here  */
+/* so GPU encrypt/keygen with a fixed seed can be checked bit-for-bit.       */
+/*   ChaCha20 block (RFC 8439 rounds), state = consts | key[8] |              */
+/*   counter64 (words 12,13) | nonce64 (words 14,15).                         */
+/*   key[8] = splitmix64(seed) x4, each split lo/hi.                          */
+/*   Stream (nonce, counter): u64 word w = block(w/8) words (2(w%8), 2(w%8)+1)*/
+/*   ternary: r % 3 - 1;  Gaussian: k = #{i : (r>>1) >= cdt[i]}, sign r&1.    */
+/* ------------------------------------------------------------------------ */
+
+#define ROTL32(v, n) (((v) << (n)) | ((v) >> (32 - (n))))
+#define QR(a, b, c, d)            \
+  a += b; d ^= a; d = ROTL32(d, 16); \
+  c += d; b ^= c; b = ROTL32(b, 12); \
+  a += b; d ^= a; d = ROTL32(d, 8);  \
+  c += d; b ^= c; b = ROTL32(b, 7);
+
+void or_chacha20_block(const uint32_t key[8], uint64_t counter, uint64_t nonce, uint32_t out[16]) {
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                    (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce,
+                    (uint32_t)(nonce >> 32)};
+  uint32_t x[16];
+  memcpy(x, s, sizeof(x));
+  for (int i = 0; i < 10; ++i) {
+    QR(x[0], x[4], x[8], x[12]);
+    QR(x[1], x[5], x[9], x[13]);
+    QR(x[2], x[6], x[10], x[14]);
+    QR(x[3], x[7], x[11], x[15]);
+    QR(x[0], x[5], x[10], x[15]);
+    QR(x[1], x[6], x[11], x[12]);
+    QR(x[2], x[7], x[8], x[13]);
+    QR(x[3], x[4], x[9], x[14]);
+  }
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+
+static uint64_t splitmix64(uint64_t* st) {
+  uint64_t z = (*st += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+void or_seed_to_key(uint64_t seed, uint32_t key[8]) {
+  uint64_t st = seed;
+  for (int i = 0; i < 4; ++i) {
+    uint64_t z = splitmix64(&st);
+    key[2 * i] = (uint32_t)z;
+    key[2 * i + 1] = (uint32_t)(z >> 32);
+  }
+}
+/* u64 words [w0, w0+cnt) of stream (key, nonce) */
+void or_stream_words(const uint32_t key[8], uint64_t nonce, uint64_t w0, size_t cnt,
+                     uint64_t* out) {
+  uint32_t blk[16];
+  uint64_t cur = (uint64_t)-1;
+  for (size_t i = 0; i < cnt; ++i) {
+    uint64_t w = w0 + i;
+    if (w / 8 != cur) {
+      cur = w / 8;
+      or_chacha20_block(key, cur, nonce, blk);
+    }
+    uint32_t k = (uint32_t)(w % 8);
+    out[i] = (uint64_t)blk[2 * k] | ((uint64_t)blk[2 * k + 1] << 32);
+  }
+}
+
+/* Cumulative distribution table for the discrete Gaussian D_{Z,sigma}
+ * (P(x) ~ exp(-x^2 / (2 sigma^2)), sigma = 3.19 from cryptocontext.txt@2502),
+ * folded to |x|: thresholds on 63-bit uniforms.  cdt[k] = floor(P(|x| <= k) *
+ * 2^63) for k = 0..T-1 (T = ceil(13 sigma) + 1); value = #{k : u >= cdt[k]}. */
+int or_gauss_cdt(double sigma, uint64_t* cdt, int max_entries) {
+  int T = (int)ceil(13.0 * sigma) + 1;
+  if (T > max_entries) return -1;
+  long double S = 1.0L;
+  for (int k = 1; k <= T; ++k) S += 2.0L * expl(-(long double)k * k / (2.0L * sigma * sigma));
+  long double acc = 1.0L / S;
+  for (int k = 0; k < T; ++k) {
+    long double v = acc * 9223372036854775808.0L;
+    cdt[k] = v >= 9223372036854775807.0L ? 0x7FFFFFFFFFFFFFFFull : (uint64_t)v;
+    acc += 2.0L * expl(-(long double)(k + 1) * (k + 1) / (2.0L * sigma * sigma)) / S;
+  }
+  return T;
+}
+static inline int64_t gauss_from_word(uint64_t r, const uint64_t* cdt, int T) {
+  uint64_t u = r >> 1;
+  int64_t k = 0;
+  for (int i = 0; i < T; ++i) k += (u >= cdt[i]);
+  return (r & 1) ? -k : k;
+}
+static inline int64_t ternary_from_word(uint64_t r) { return (int64_t)(r % 3) - 1; }
+
+/* Encrypt randomness for global ciphertext index g: nonce = (1<<56)|g,
+ * v from counter words [0,N), e0 from [N,2N), e1 from [2N,3N). */
+void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int64_t* v,
+                       int64_t* e0, int64_t* e1) {
+  uint32_t key[8];
+  or_seed_to_key(seed, key);
+  uint64_t cdt[64];
+  int T = or_gauss_cdt(sigma, cdt, 64);
+  uint64_t* w = malloc(sizeof(uint64_t) * 3 * N);
+  or_stream_words(key, (1ull << 56) | g, 0, 3ull * N, w);
+  for (uint32_t j = 0; j < N; ++j) {
+    v[j] = ternary_from_word(w[j]);
+    e0[j] = gauss_from_word(w[N + j], cdt, T);
+    e1[j] = gauss_from_word(w[2ull * N + j], cdt, T);
+  }
+  free(w);
+}
+
+/* uniform residue mod q from two words (bias < 2^-67) */
+static uint64_t uniform_mod(uint64_t lo, uint64_t hi, uint64_t q) {
+  return (uint64_t)((((u128)hi << 64) | lo) % q);
+}
+
+/* KeyGen randomness: nonce = (2<<56): s words [0,N), e words [N,2N);
+ * a for tower t: nonce = (2<<56)|(1+t), words [0,2N) -> (lo,hi) pairs. */
+void or_sample_keygen(uint64_t seed, uint32_t N, uint32_t L, const uint64_t* q, double sigma,
+                      int64_t* s, int64_t* e, uint64_t* a_eval) {
+  uint32_t key[8];
+  or_seed_to_key(seed, key);
+  uint64_t cdt[64];
+  int T = or_gauss_cdt(sigma, cdt, 64);
+  uint64_t* w = malloc(sizeof(uint64_t) * 2 * N);
+  or_stream_words(key, 2ull << 56, 0, 2ull * N, w);
+  for (uint32_t j = 0; j < N; ++j) {
+    s[j] = ternary_from_word(w[j]);
+    e[j] = gauss_from_word(w[N + j], cdt, T);
+  }
+  for (uint32_t t = 0; t < L; ++t) {
+    or_stream_words(key, (2ull << 56) | (1 + t), 0, 2ull * N, w);
+    for (uint32_t j = 0; j < N; ++j) a_eval[(size_t)t * N + j] = uniform_mod(w[2 * j], w[2 * j + 1], q[t]);
+  }
+  free(w);
+}

@@ -1,0 +1,334 @@
+"""HIP path (libshelfi.so through the C ABI) vs the CPU restatement (oracle/).
+
+Integer work (NTT, aggregation, encryption with the seeded sampler, key generation)
+must match bit-for-bit; decode is a fixed-order f64 computation and must match the
+oracle bit-for-bit too; decrypt(aggregate(encrypt(x))) vs plain FedAvg is checked
+against the CKKS error bound (tolerance stated per test).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import palisade_fixture as P
+from conftest import PALISADE_DIR
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+
+def _ctx_arrays(ck):
+    inf = ck.info()
+    return (inf, np.array(inf["moduli"], np.uint64), np.array(inf["roots"], np.uint64),
+            inf["ring_dim"], inf["batch"], inf["delta"])
+
+
+@pytest.fixture(scope="module")
+def cfg1():
+    """BASELINE config 1: the reference's own PALISADE keys (N=2^13, L=2, batch 4096)."""
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42)
+    ck.loadCryptoParams()
+    assert ck.info()["keys_loaded"]
+    return ck
+
+
+@pytest.fixture(scope="module")
+def cfg2(tmp_path_factory):
+    """BASELINE config 2/3/5 parameters: N=2^15, L=4 (multDepth 3), batch 16384."""
+    d = str(tmp_path_factory.mktemp("keys_c2")) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    return ck
+
+
+@pytest.fixture(scope="module")
+def cfg4(tmp_path_factory):
+    """BASELINE config 4 parameters: N=2^16, L=6 (multDepth 5), batch 32768."""
+    d = str(tmp_path_factory.mktemp("keys_c4")) + os.sep
+    ck = m.CKKS("ckks", 32768, 52, d, multDepth=5, seed=9)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    return ck
+
+
+CFGS = ["cfg1", "cfg2", "cfg4"]
+
+
+# --------------------------------------------------------------- setup -----
+def test_palisade_keys_loaded(cfg1):
+    ctx, pk, sk = P.read_keys(PALISADE_DIR)
+    inf = cfg1.info()
+    assert inf["ring_dim"] == 8192 and inf["num_towers"] == 2 and inf["palisade_keys"]
+    assert inf["moduli"] == ctx["q"] and inf["roots"] == ctx["psi"]
+    gpk, gsk = cfg1.get_keys()
+    assert np.array_equal(gpk, pk) and np.array_equal(gsk, sk)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_params_and_keygen_match_oracle(cfg, request):
+    ck = request.getfixturevalue(cfg)
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    qo, psio = O.params_generate(N, inf["num_towers"], 52, 60)
+    assert np.array_equal(q, qo) and np.array_equal(psi, psio)
+    seed = {"cfg2": 7, "cfg4": 9}[cfg]
+    s, e, a = O.sample_keygen(seed, N, q)
+    sk_o, pk_o = O.keygen(s, e, a, q, psi)
+    pk, sk = ck.get_keys()
+    assert np.array_equal(sk, sk_o)
+    assert np.array_equal(pk, pk_o)
+
+
+def test_keyfiles_roundtrip(cfg2):
+    ck2 = m.CKKS("ckks", 16384, 52, cfg2.cryptodir, multDepth=3)
+    ck2.loadCryptoParams()
+    a, b = ck2.get_keys(), cfg2.get_keys()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert ck2.info()["key_id"] == cfg2.info()["key_id"]
+
+
+# ----------------------------------------------------------------- NTT -----
+@pytest.mark.parametrize("cfg", CFGS)
+def test_ntt_bitexact(cfg, request):
+    ck = request.getfixturevalue(cfg)
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    L = len(q)
+    P_ = 2 * L
+    rng = np.random.default_rng(5)
+    host = np.stack([rng.integers(0, int(q[p % L]), N, dtype=np.uint64) for p in range(P_)])
+    dev = torch.from_numpy(host.view(np.int64).copy()).cuda()
+    D.ntt(ck, dev, inverse=False)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy().view(np.uint64)
+    for p in range(P_):
+        assert np.array_equal(got[p], O.ntt_fwd(host[p], int(q[p % L]), int(psi[p % L]))), p
+    D.ntt(ck, dev, inverse=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+
+
+# ----------------------------------------------------------- aggregation ----
+@pytest.mark.parametrize("cfg,C,K", [("cfg1", 4, 1), ("cfg1", 3, 3), ("cfg2", 16, 4),
+                                     ("cfg2", 20, 2), ("cfg4", 5, 2), ("cfg2", 1, 1)])
+def test_wavg_device_bitexact(cfg, C, K, request):
+    """EvalMult(ct, (float)w) + EvalAdd (ckks.cpp:286-297) on raw residues."""
+    ck = request.getfixturevalue(cfg)
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    L = len(q)
+    rng = np.random.default_rng(C * 100 + K)
+    cts = []
+    for _ in range(C):
+        a = np.empty((K, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+        cts.append(a)
+    w = list(rng.dirichlet(np.ones(C)))
+    if C > 2:
+        w[1] = -0.125  # negative weights reduce mod q (unpinned vs PALISADE, pinned vs oracle)
+        w[2] = 0.0
+    dev = [torch.from_numpy(c.view(np.int64)).cuda() for c in cts]
+    out = D.wavg(ck, dev, w)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    ref = O.wavg(cts, w, q, delta)
+    assert np.array_equal(got, ref)
+
+
+def test_wavg_extremes(cfg2):
+    """Residues at q-1 and 0, weights 1.0 (W = Delta = q_{L-1}) and tiny."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    L = len(q)
+    C = 16
+    cts = []
+    for c in range(C):
+        a = np.empty((1, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = np.uint64(int(q[t]) - 1) if c % 2 == 0 else np.uint64(0)
+        cts.append(a)
+    w = [1.0] * 8 + [2.0 ** -30] * 8
+    out = D.wavg(cfg2, [torch.from_numpy(c.view(np.int64)).cuda() for c in cts], w)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+
+
+# -------------------------------------------------------- encrypt/decrypt ----
+@pytest.mark.parametrize("cfg,n", [("cfg1", 1000), ("cfg1", 9000), ("cfg2", 20000), ("cfg4", 40000)])
+def test_encrypt_bitexact(cfg, n, request):
+    """ckks.cpp:61-104 with the seeded sampler: residues equal the oracle's encode +
+    Encrypt(pk, pt) with the same (v, e0, e1)."""
+    ck = request.getfixturevalue(cfg)
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    seed = 1234 + n
+    ck.set_seed(seed)
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, n).astype(np.float32)  # torch weights arrive as float32
+    blob = ck.encrypt(x)
+    bi = m.blob_info(blob)
+    K = -(-n // S)
+    assert bi["num_cts"] == K and bi["depth"] == 1 and bi["scale"] == delta
+    got = m.blob_residues(blob, N, len(q))
+    pk, sk = ck.get_keys()
+    ref = O.encrypt_vector(x.astype(np.float64), pk, q, psi, N, S, delta, seed=seed, g0=0)
+    assert np.array_equal(got, ref)
+    # decrypt: bit-exact against the oracle's fixed-order decode, and close to x
+    dec = ck.decrypt(blob, n)
+    ref_dec = O.decrypt_vector(ref, sk, q, psi, S, delta, n)
+    assert np.array_equal(dec, ref_dec)
+    assert np.abs(dec - x).max() < 1e-7
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+def test_e2e_weighted_average(cfg, request):
+    """pythonApi/ckks_example.py:8-111 flow (3 learners, weights [0.5, 0.2, 0.3]),
+    checked (the reference only prints).  Tolerance 1e-7 absolute at Delta ~ 2^52."""
+    ck = request.getfixturevalue(cfg)
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    ck.set_seed(77)
+    n = 100000 if cfg == "cfg1" else 3 * S + 17
+    rng = np.random.default_rng(8)
+    xs = [rng.random(n) for _ in range(3)]
+    w = [0.5, 0.2, 0.3]
+    encs = [ck.encrypt(x) for x in xs]
+    agg = ck.computeWeightedAverage(encs, w)
+    bi = m.blob_info(agg)
+    assert bi["depth"] == 2 and bi["scale"] == delta * delta
+    dec = ck.decrypt(agg, n)
+    exp = sum(float(np.float32(wi)) * x for wi, x in zip(w, xs))
+    assert np.abs(dec - exp).max() < 1e-7
+    # residues of the aggregate equal the oracle aggregation of the same blobs
+    res = [m.blob_residues(b, N, len(q)) for b in encs]
+    assert np.array_equal(m.blob_residues(agg, N, len(q)), O.wavg(res, w, q, delta))
+    # and the decode is bit-exact vs the oracle
+    pk, sk = ck.get_keys()
+    K = res[0].shape[0]
+    k = K - 1
+    ln = n - k * S
+    ref = O.decrypt(m.blob_residues(agg, N, len(q))[k], sk, q, psi, S, delta * delta, ln)
+    assert np.array_equal(dec[k * S:], ref)
+
+
+def test_main_cpp_flow(cfg1):
+    """src/main.cpp:26-82: 100 values U[0,100), the same blob three times with weights
+    0.5/0.3/0.5.  Sums near 130 exceed the depth-2 headroom Q/(2 Delta^2) ~ 128 of
+    N=2^13/L=2 and wrap (as they do in the reference); the rest must be exact."""
+    rng = np.random.default_rng(0)
+    x = rng.uniform(0, 100, 100)
+    enc = cfg1.encrypt_cpp(x)
+    res = cfg1.computeWeightedAverage_cpp([enc, enc, enc], [0.5, 0.3, 0.5])
+    out = cfg1.decrypt_cpp(res, 100)
+    exp = 1.3 * x
+    ok = exp < 127.0
+    assert ok.sum() > 90
+    assert np.abs(out[ok] - exp[ok]).max() < 1e-6
+
+
+# -------------------------------------------------------------- API edges ----
+def test_api_behaviour(cfg1, cfg2, capsys):
+    enc = cfg1.encrypt(np.ones(10))
+    # ckks.cpp:265-268: size mismatch prints and returns ""
+    assert cfg1.computeWeightedAverage([enc, enc], [0.5]) == b""
+    assert "size mismatch" in capsys.readouterr().out
+    # other context / key -> RuntimeError
+    enc2 = cfg2.encrypt(np.ones(10))
+    with pytest.raises(RuntimeError):
+        cfg1.computeWeightedAverage([enc, enc2], [0.5, 0.5])
+    with pytest.raises(RuntimeError):
+        cfg1.decrypt(enc2, 10)
+    # unequal ciphertext counts (UB in the reference, ckks.cpp:294-297) -> RuntimeError
+    enc_long = cfg1.encrypt(np.ones(5000))
+    with pytest.raises(RuntimeError):
+        cfg1.computeWeightedAverage([enc, enc_long], [0.5, 0.5])
+    # more outputs than slots -> ValueError
+    with pytest.raises(ValueError):
+        cfg1.decrypt(enc, 5000)
+    # empty input -> zero ciphertexts, decrypts to an empty vector
+    e0 = cfg1.encrypt(np.zeros(0))
+    assert m.blob_info(e0)["num_cts"] == 0
+    assert cfg1.decrypt(e0, 0).shape == (0,)
+    # float32 / list inputs are widened like py::array_t<double> forcecast
+    d = cfg1.decrypt(cfg1.encrypt([0.25, -0.5, 1.0]), 3)
+    assert np.allclose(d, [0.25, -0.5, 1.0], atol=1e-9)
+    # out-of-range values are rejected rather than silently wrapped
+    with pytest.raises(ValueError):
+        cfg1.encrypt(np.array([1e9]))
+    # no keys
+    ck = m.CKKS("ckks", 4096, 52, "/nonexistent/")
+    ck.loadCryptoParams()
+    assert "Could not read" in capsys.readouterr().out
+    with pytest.raises(RuntimeError):
+        ck.encrypt(np.ones(3))
+
+
+def test_decrypt_partial_lengths(cfg1):
+    """ckks.cpp:192-196: last chunk length n - i*batch; any n <= K*batch is accepted."""
+    x = np.linspace(-1, 1, 3 * 4096)
+    enc = cfg1.encrypt(x)
+    for n in (1, 4096, 4097, 8191, 3 * 4096):
+        assert np.abs(cfg1.decrypt(enc, n) - x[:n]).max() < 1e-8
+
+
+# ------------------------------------------------------- device pipeline ----
+def test_device_encrypt_decrypt(cfg2):
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    x = torch.linspace(-1, 1, 2 * S + 5, dtype=torch.float64, device="cuda")
+    ct = D.encrypt(cfg2, x)
+    out = D.decrypt(cfg2, ct, x.numel(), delta)
+    torch.cuda.synchronize()
+    assert (out - x).abs().max().item() < 1e-8
+
+
+def test_modq_after_sum(cfg2):
+    """RCCL reduce semantics: uint64 sum of G partials then modq == wavg of all."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    L = len(q)
+    G, K = 8, 2
+    rng = np.random.default_rng(3)
+    parts = []
+    for _ in range(G):
+        a = np.empty((K, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+        parts.append(a)
+    s = np.zeros_like(parts[0])
+    for a in parts:
+        s += a  # wraps mod 2^64 exactly like ncclSum on uint64/int64
+    dev = torch.from_numpy(s.view(np.int64).copy()).cuda()
+    D.modq(cfg2, dev)
+    torch.cuda.synchronize()
+    ref = parts[0].copy()
+    for a in parts[1:]:
+        for t in range(L):
+            ref[:, :, t] = (ref[:, :, t] + a[:, :, t]) % q[t]
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), ref)
+
+
+# ------------------------------------------------------- full-size check ----
+@pytest.mark.slow
+def test_full_size_cfg3_shard_bitexact(cfg2):
+    """BASELINE config 3 per-GPU shard at full size: 16 learners x 714 ciphertexts
+    (ResNet-18, 11,689,512 params at batch 16384), N=2^15, L=4 — 22.3 GiB of input.
+    One device aggregation over everything, then every ciphertext checked against the
+    oracle (Shoup form, 16 threads) chunk by chunk."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    L = len(q)
+    C, K = 16, 714
+    g = torch.Generator(device="cuda")
+    g.manual_seed(2024)
+    cts = []
+    for _ in range(C):
+        t_ = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
+        for t in range(L):
+            t_[:, :, t, :] = torch.randint(0, int(q[t]), (K, 2, N), generator=g, device="cuda",
+                                           dtype=torch.int64)
+        cts.append(t_)
+    w = [1.0 / C] * C
+    out = D.wavg(cfg2, cts, w)
+    torch.cuda.synchronize()
+    step = 64
+    for k0 in range(0, K, step):
+        k1 = min(K, k0 + step)
+        host = [c[k0:k1].cpu().numpy().view(np.uint64) for c in cts]
+        ref = O.wavg_fast(host, w, q, delta, nthreads=16)
+        assert np.array_equal(out[k0:k1].cpu().numpy().view(np.uint64), ref), k0

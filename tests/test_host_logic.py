@@ -1,0 +1,193 @@
+"""CPU tests of the product's host side: the C ABI loads and exports every symbol of
+include/shelfi.h, the host-only entry points agree with the oracle, and the
+distributed combine logic (SHELFI_FHE.dist) is exact over gloo with world_size 2."""
+import ctypes as C
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+import oracle as O
+import palisade_fixture as P
+from conftest import PALISADE_DIR, PALISADE_PYBIND_DIR, ROOT
+
+import SHELFI_FHE as m
+from SHELFI_FHE import _lib
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "shelfi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(shelfi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_header_symbol_is_exported_and_bound():
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, s
+    assert lib.shelfi_abi_version() == 1
+    assert lib.shelfi_blob_header_bytes() == 64
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("batch,sb,depth,fb", [(4096, 52, 1, 60), (16384, 52, 3, 60), (32768, 52, 5, 60),
+                                               (1024, 52, 1, 60), (4096, 14, 1, 60), (4096, 33, 1, 60),
+                                               (2048, 40, 2, 60), (4096, 50, 1, 50)])
+def test_params_generate_matches_oracle(batch, sb, depth, fb):
+    N, q, psi = m.params_generate(batch, sb, depth, fb)
+    L = depth + 1
+    logq = (fb if L > 1 else sb) + (L - 1) * sb
+    assert N == O.min_ring_dim(logq, batch)
+    qo, psio = O.params_generate(N, L, sb, fb)
+    assert q == [int(x) for x in qo]
+    assert psi == [int(x) for x in psio]
+
+
+@pytest.mark.parametrize("d", [PALISADE_DIR, PALISADE_PYBIND_DIR])
+def test_product_palisade_reader_matches_test_reader(d):
+    lib = _lib.load()
+    N, L = C.c_uint32(), C.c_uint32()
+    _lib.check(lib.shelfi_read_palisade(d.encode(), C.byref(N), C.byref(L), None, None, None, None))
+    assert (N.value, L.value) == (8192, 2)
+    q = np.zeros(16, np.uint64)
+    psi = np.zeros(16, np.uint64)
+    pk = np.zeros((2, 2, 8192), np.uint64)
+    sk = np.zeros((2, 8192), np.uint64)
+    u64p = _lib.u64p
+    _lib.check(lib.shelfi_read_palisade(d.encode(), None, None, q.ctypes.data_as(u64p),
+                                        psi.ctypes.data_as(u64p), pk.ctypes.data_as(u64p),
+                                        sk.ctypes.data_as(u64p)))
+    ctx, pk_t, sk_t = P.read_keys(d)
+    assert [int(x) for x in q[:2]] == ctx["q"] and [int(x) for x in psi[:2]] == ctx["psi"]
+    assert np.array_equal(pk, pk_t) and np.array_equal(sk, sk_t)
+
+
+def test_palisade_reader_rejects_garbage(tmp_path):
+    lib = _lib.load()
+    (tmp_path / "cryptocontext.txt").write_bytes(b"\x01" + b"x" * 100)
+    rc = lib.shelfi_read_palisade((str(tmp_path) + "/").encode(), None, None, None, None, None, None)
+    assert rc == _lib.SHELFI_ERR_FORMAT
+    rc = lib.shelfi_read_palisade(b"/nonexistent/", None, None, None, None, None, None)
+    assert rc == _lib.SHELFI_ERR_IO
+
+
+@pytest.mark.parametrize("S", [1, 2, 16, 4096, 16384])
+def test_fft_twiddles_match_oracle(S):
+    lib = _lib.load()
+    a = [np.zeros(S) for _ in range(4)]
+    _lib.check(lib.shelfi_fft_twiddles(S, *[x.ctypes.data_as(_lib.f64p) for x in a]))
+    for x, y in zip(a, O.fft_twiddles(S)):
+        assert np.array_equal(x, y)
+
+
+def test_gauss_cdt_matches_oracle():
+    lib = _lib.load()
+    cdt = np.zeros(64, np.uint64)
+    T = lib.shelfi_gauss_cdt(O.SIGMA, cdt.ctypes.data_as(_lib.u64p), 64)
+    assert T == len(O.gauss_cdt())
+    assert np.array_equal(cdt[:T], O.gauss_cdt())
+
+
+def test_blob_info_validation():
+    lib = _lib.load()
+    hdr = bytearray(64)
+    hdr[0:4] = b"SHCT"
+    struct.pack_into("<HHIIQIIdQQII", hdr, 4, 1, 64, 13, 2, 1, 1, 0, 2.0 ** 52, 1, 2, 4096, 4)
+    blob = bytes(hdr) + bytes(2 * 2 * 8192 * 8)
+    info = m.blob_info(blob)
+    assert info == {"num_cts": 1, "depth": 1, "scale": 2.0 ** 52, "key_id": 2}
+    with pytest.raises(RuntimeError):
+        m.blob_info(blob[:-8])
+    with pytest.raises(RuntimeError):
+        m.blob_info(b"XXXX" + blob[4:])
+
+
+def test_no_gpu_fails_loudly():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        m.CKKS()
+
+
+def test_shard_helpers():
+    from SHELFI_FHE import dist
+
+    assert dist.learner_shard(10, 1, 4) == [1, 5, 9]
+    assert sum(len(dist.learner_shard(128, g, 8)) for g in range(8)) == 128
+    assert dist.ct_slices(714, 8)[0] == (0, 90) and dist.ct_slices(714, 8)[-1][1] == 714
+    assert dist.slice_of_rank(714, 8, 7) == (630, 714)
+
+
+def _gloo_worker(rank, world, port, mode, result_q):
+    import torch
+    import torch.distributed as dist_
+
+    import oracle as O_
+    from SHELFI_FHE import dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist_.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, L, K, C_ = 1024, 3, 5, 7
+        q, psi = O_.params_generate(N, L, 40, 50)
+        delta = float(int(q[-1]))
+        rng = np.random.default_rng(99)  # same learners on every rank
+        cts = []
+        for _ in range(C_):
+            a = np.empty((K, 2, L, N), np.uint64)
+            for t in range(L):
+                a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+            cts.append(a)
+        w = list(rng.dirichlet(np.ones(C_)))
+        mine = dist.learner_shard(C_, rank, world)
+        # the per-rank wavg kernel's result, computed here by the oracle
+        part = O_.wavg([cts[i] for i in mine], [w[i] for i in mine], q, delta)
+        t_ = torch.from_numpy(part.view(np.int64).copy())
+        share = dist.reduce_partials(t_, mode=mode)
+        got = share.numpy().view(np.uint64).copy()
+        for t in range(L):  # the modq kernel
+            got[:, :, t, :] %= q[t]
+        full = O_.wavg(cts, w, q, delta)
+        if mode == "reduce_scatter":
+            s0, s1 = dist.slice_of_rank(K, world, rank)
+            ok = np.array_equal(got, full[s0:s1])
+        elif mode == "reduce":
+            ok = np.array_equal(got, full) if rank == 0 else True
+        else:
+            ok = np.array_equal(got, full)
+        result_q.put((rank, bool(ok)))
+    finally:
+        dist_.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["reduce_scatter", "reduce", "all_reduce"])
+def test_distributed_combine_gloo_world2(mode):
+    """world_size-2 gloo run of the multi-GPU combine: learner sharding + int64 SUM
+    collective + mod-q fold == the single-process aggregation, bit-exact."""
+    import multiprocessing as mp
+    import socket
+
+    pytest.importorskip("torch")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q_ = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, mode, q_)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q_.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]
