@@ -83,12 +83,13 @@ class CKKS(Scheme):
     # ------------------------------------------------------------ lifecycle --
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
-        if ctx is not None and ctx.value:
+        lib = getattr(self, "_lib", None)
+        if ctx is not None and lib is not None and getattr(ctx, "value", None):
             try:
-                self._lib.shelfi_ctx_destroy(ctx)
+                lib.shelfi_ctx_destroy(ctx)
             except Exception:
                 pass
-            self._ctx = C.c_void_p()
+            self._ctx = None
 
     def info(self) -> dict:
         inf = _lib.Info()

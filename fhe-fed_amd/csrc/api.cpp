@@ -868,7 +868,7 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     for (size_t c0 = 0; c0 < C; c0 += kWavgMaxLearners) {
       const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
       WavgArgs a;
@@ -897,7 +897,7 @@ int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream) 
   if (!ctx || !buf_dev) return SHELFI_ERR_ARG;
   return guarded([&] {
     DeviceGuard g(ctx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     launch_modq(buf_dev, (uint64_t)K * 2 * ctx->p.L, ctx->p.L, ctx->p.logN, ctx->dt.tc, s);
   });
 }
@@ -910,7 +910,7 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
     require_keys(ctx);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     const uint64_t K = (n + p.batch - 1) / p.batch;
     if (!K) return;
     uint32_t key[8];
@@ -945,7 +945,7 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     if (n > (uint64_t)K * p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     const uint64_t Kn = (n + p.batch - 1) / p.batch;
     if (!Kn) return;
     const uint64_t chunk = std::max<uint64_t>(1, (1024ull << 20) / decrypt_scratch_bytes(p, 1));
@@ -966,7 +966,7 @@ int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, 
   if (!ctx || (P && !polys_dev)) return SHELFI_ERR_ARG;
   return guarded([&] {
     DeviceGuard g(ctx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     launch_ntt(polys_dev, P, ctx->p.L, ctx->p.logN, inverse != 0, ctx->dt, s);
   });
 }

@@ -113,15 +113,17 @@ size_t shelfi_blob_header_bytes(void);
 
 /* ---- device-resident batch API (HBM in, HBM out; `stream` = hipStream_t) ---- */
 /* Ciphertext batches are [K][2][L][N] uint64 in HBM (same order as the blob
- * payload).  These calls enqueue work on `stream` and return without syncing. */
+ * payload).  Work is enqueued on `stream` exactly as given (NULL = the legacy
+ * default stream, e.g. PyTorch's default stream); wavg/modq/ntt return without
+ * syncing, encrypt/decrypt synchronise `stream` before returning (they reuse the
+ * context's scratch arena). */
 
 /* sum_c W_c * in[c] mod q_t, W_c = (int64)((double)w[c] * delta + 0.5) (EvalMult +
  * EvalAdd, ckks.cpp:286-297).  in_dev: host array of C device pointers. */
 int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float* w, size_t C,
                     size_t K, uint64_t* out_dev, void* stream);
-/* Same arithmetic, result left unreduced in [0, 2^64) is NOT offered; instead the
- * partial sum is reduced and a later shelfi_dev_modq() folds a collective's
- * uint64 sum of G <= 16 partials back into [0, q_t). */
+/* Folds a collective's uint64 SUM of G <= 15 reduced partial sums back into [0, q_t)
+ * (multi-GPU combine: local shelfi_dev_wavg -> RCCL reduce/reduce_scatter -> this). */
 int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream);
 /* encode + encrypt n doubles (device) into K = ceil(n/batch) ciphertexts. */
 int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
