@@ -132,13 +132,18 @@ def main():
         enc_times.append(time.perf_counter() - t0)
         del x
     weights = [1.0 / (Cl * world)] * Cl
-    out = torch.empty_like(cts[0])
+    # partial-sum buffer padded to a multiple of world ciphertexts (zero tail, the
+    # additive identity) so reduce_scatter needs no per-step concatenation
+    Kpad = -(-K // world) * world
+    out_full = torch.zeros((Kpad,) + tuple(cts[0].shape[1:]), dtype=torch.int64, device=dev)
+    out = out_full[:K]
 
     def full_step():
         if world == 1:
             D.wavg(ck, cts, weights, out=out)
             return out
-        share = SD.reduce_partials(D.wavg(ck, cts, weights, out=out), mode=args.mode)
+        D.wavg(ck, cts, weights, out=out)
+        share = SD.reduce_partials(out_full, mode=args.mode)
         if share.shape[0]:
             D.modq(ck, share)
         return share
@@ -160,7 +165,7 @@ def main():
         D.wavg(ck, cts, weights, out=out)
         ev[i][1].record(stream)
         if world > 1:
-            share = SD.reduce_partials(out, mode=args.mode)
+            share = SD.reduce_partials(out_full, mode=args.mode)
             if share.shape[0]:
                 D.modq(ck, share)
     torch.cuda.synchronize()
