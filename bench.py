@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--workload", choices=["cfg3", "cfg2"], default="cfg3")
     ap.add_argument("--learners-per-gpu", type=int, default=16)
     ap.add_argument("--mode", choices=["reduce_scatter", "reduce", "all_reduce"], default="reduce_scatter")
+    ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
+                    help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
@@ -132,17 +134,31 @@ def main():
         enc_times.append(time.perf_counter() - t0)
         del x
     weights = [1.0 / (Cl * world)] * Cl
+    # the aggregator's resident layout: learners interleaved in one arena (placed once,
+    # before the timed region)
+    arena = D.Arena(ck, Cl, K, device=dev)
+    for i, ct in enumerate(cts):
+        arena.put(i, ct)
+    torch.cuda.synchronize()
+    if args.layout == "arena":
+        del cts
+        cts = None
     # partial-sum buffer padded to a multiple of world ciphertexts (zero tail, the
     # additive identity) so reduce_scatter needs no per-step concatenation
     Kpad = -(-K // world) * world
-    out_full = torch.zeros((Kpad,) + tuple(cts[0].shape[1:]), dtype=torch.int64, device=dev)
+    out_full = torch.zeros((Kpad, 2, L, N), dtype=torch.int64, device=dev)
     out = out_full[:K]
 
-    def full_step():
-        if world == 1:
+    def local_wavg():
+        if args.layout == "arena":
+            arena.wavg(weights, out=out)
+        else:
             D.wavg(ck, cts, weights, out=out)
+
+    def full_step():
+        local_wavg()
+        if world == 1:
             return out
-        D.wavg(ck, cts, weights, out=out)
         share = SD.reduce_partials(out_full, mode=args.mode)
         if share.shape[0]:
             D.modq(ck, share)
@@ -162,7 +178,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        D.wavg(ck, cts, weights, out=out)
+        local_wavg()
         ev[i][1].record(stream)
         if world > 1:
             share = SD.reduce_partials(out_full, mode=args.mode)
@@ -186,7 +202,7 @@ def main():
 
     # correctness spot check of this rank's aggregate (decrypt one ciphertext) and
     # device-resident decrypt+decode timing over the K aggregated ciphertexts
-    D.wavg(ck, cts, weights, out=out)
+    local_wavg()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     dec = D.decrypt(ck, out, K * batch, delta * delta)
@@ -223,7 +239,7 @@ def main():
                                                  params, K, batch,
                                                  "" if world == 1 else ", RCCL %s" % args.mode),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
-                   "parallelism": "learner-sharded dp%d" % world},
+                   "parallelism": "learner-sharded dp%d" % world, "layout": args.layout},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(1e3 * sorted(enc_times)[len(enc_times) // 2] / K, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),

@@ -229,6 +229,22 @@ def blob_info(blob: bytes) -> dict:
             "key_id": int(kid.value)}
 
 
+def blob_pack(ckks: "CKKS", residues: np.ndarray, depth: int = 1, scale: float | None = None) -> bytes:
+    """Wrap raw residues [K][2][L][N] (host) into a blob under `ckks`'s params/key id."""
+    lib = _lib.load()
+    r = np.ascontiguousarray(residues, dtype=np.uint64)
+    if scale is None:
+        scale = ckks.info()["delta"] ** depth
+    out = _lib.u8p()
+    n = C.c_size_t()
+    check(lib.shelfi_blob_pack(ckks._ctx, r.ctypes.data_as(_lib.u64p), r.shape[0], int(depth),
+                               float(scale), C.byref(out), C.byref(n)), "blob_pack")
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        lib.shelfi_free(out)
+
+
 def blob_residues(blob: bytes, ring_dim: int, num_towers: int) -> np.ndarray:
     """View of a blob's payload as [K][2][L][N] uint64 (host)."""
     hdr = _lib.load().shelfi_blob_header_bytes()

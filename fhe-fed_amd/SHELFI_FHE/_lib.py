@@ -73,6 +73,11 @@ SIGNATURES = {
     "shelfi_blob_header_bytes": (C.c_size_t, []),
     "shelfi_dev_wavg": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), f32p, C.c_size_t, C.c_size_t,
                                   C.c_void_p, C.c_void_p]),
+    "shelfi_arena_words": (C.c_size_t, [C.c_void_p, C.c_size_t, C.c_size_t]),
+    "shelfi_dev_arena_put": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_size_t, C.c_size_t, C.c_size_t,
+                                       C.c_void_p, C.c_void_p]),
+    "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
+                                        C.c_void_p]),
     "shelfi_dev_modq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "shelfi_dev_encrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_size_t,

@@ -374,6 +374,18 @@ static T get(const std::string& s, size_t& off) {
   return v;
 }
 
+// W = (int64)((double)(float)w * Delta + 0.5) per learner, split into 30-bit limbs
+static void fill_weights(WavgArgs& a, const Params& p, const float* w, size_t n) {
+  for (size_t c = 0; c < n; ++c) {
+    const int64_t W = (int64_t)((double)w[c] * p.delta + 0.5);  // ckks.cpp:287-288
+    for (uint32_t t = 0; t < p.L; ++t) {
+      const uint64_t wt = mod_signed(W, p.q[t]);
+      a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
+      a.wl[c][t][1] = (uint32_t)(wt >> 30);
+    }
+  }
+}
+
 }  // namespace shelfi
 
 // ============================================================== C ABI ======
@@ -755,13 +767,8 @@ int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const 
             SHELFI_HIP(hipMemcpyAsync(io + c * payload, blobs[c0 + c] + sizeof(BlobHeader),
                                       payload, hipMemcpyHostToDevice, ctx->stream));
             a.ptrs[c] = (const uint64_t*)(io + c * payload);
-            const int64_t W = (int64_t)((double)weights[c0 + c] * p.delta + 0.5);  // ckks.cpp:287-288
-            for (uint32_t t = 0; t < p.L; ++t) {
-              const uint64_t wt = mod_signed(W, p.q[t]);
-              a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
-              a.wl[c][t][1] = (uint32_t)(wt >> 30);
-            }
           }
+          fill_weights(a, p, weights + c0, gc);
           a.out = dout;
           a.rows = K * 2 * p.L;
           a.C = (uint32_t)gc;
@@ -873,15 +880,8 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
       const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
       WavgArgs a;
       std::memset(&a, 0, sizeof(a));
-      for (size_t c = 0; c < gc; ++c) {
-        a.ptrs[c] = in_dev[c0 + c];
-        const int64_t W = (int64_t)((double)w[c0 + c] * p.delta + 0.5);
-        for (uint32_t t = 0; t < p.L; ++t) {
-          const uint64_t wt = mod_signed(W, p.q[t]);
-          a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
-          a.wl[c][t][1] = (uint32_t)(wt >> 30);
-        }
-      }
+      for (size_t c = 0; c < gc; ++c) a.ptrs[c] = in_dev[c0 + c];
+      fill_weights(a, p, w + c0, gc);
       a.out = out_dev;
       a.rows = (uint64_t)K * 2 * p.L;
       a.C = (uint32_t)gc;
@@ -889,6 +889,52 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
       a.logN = p.logN;
       a.accumulate = c0 ? 1 : 0;
       launch_wavg(a, ctx->dt.tc, s);
+    }
+  });
+}
+
+size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K) {
+  if (!ctx) return 0;
+  return C * K * 2ull * ctx->p.L * ctx->p.N;
+}
+
+int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size_t K, size_t learner,
+                         size_t C, uint64_t* arena_dev, void* stream) {
+  if (!ctx || !arena_dev || (K && !src) || learner >= C) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    const size_t total = K * 2ull * ctx->p.L * ctx->p.N;  // residues per learner
+    if (!total) return;
+    const size_t rows = total / kArenaChunk, row_bytes = kArenaChunk * 8;
+    SHELFI_HIP(hipMemcpy2DAsync(arena_dev + learner * kArenaChunk, C * row_bytes, src, row_bytes,
+                                row_bytes, rows,
+                                src_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream));
+  });
+}
+
+int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
+                          size_t K, uint64_t* out_dev, void* stream) {
+  if (!ctx || !out_dev || (C && (!arena_dev || !w))) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    for (size_t c0 = 0; c0 < C; c0 += kWavgMaxLearners) {
+      const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
+      WavgArgs a;
+      std::memset(&a, 0, sizeof(a));
+      fill_weights(a, p, w + c0, gc);
+      a.arena = arena_dev;
+      a.arena_learners = (uint32_t)C;
+      a.first_learner = (uint32_t)c0;
+      a.out = out_dev;
+      a.rows = (uint64_t)K * 2 * p.L;
+      a.C = (uint32_t)gc;
+      a.L = p.L;
+      a.logN = p.logN;
+      a.accumulate = c0 ? 1 : 0;
+      launch_wavg(a, ctx->dt.tc, (hipStream_t)stream);
     }
   });
 }

@@ -105,6 +105,13 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
   return addmod(addmod(a, b, c.q), d, c.q);
 }
 
+// Two input layouts, one kernel body:
+//  * SEPARATE: each learner's batch is its own buffer (ptrs[k] + e);
+//  * INTERLEAVED (the aggregator's resident layout, shelfi_dev_arena_*): one arena
+//    [chunk][learner][512 residues]; a block then reads one contiguous C x 4 KiB
+//    region instead of C separate streams — measured 6.35 vs 5.80 TB/s at C = 16
+//    (tools/wavg_variants.py), the gap being DRAM row locality across 16 streams.
+template <bool INTERLEAVED>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
   const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
@@ -112,14 +119,19 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   const TowerConst c = tcs[t];
   const uint64_t e = base + 2u * threadIdx.x;
   const uint32_t M30 = (1u << 30) - 1;
+  // interleaved: this block's chunk, learner slice k at src + k * 512
+  const uint64_t* __restrict__ src =
+      INTERLEAVED ? a.arena + ((uint64_t)blockIdx.x * a.arena_learners + a.first_learner) * kWavgPerBlock +
+                        2u * threadIdx.x
+                  : nullptr;
 
   uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
   uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
 #pragma unroll 8
   for (uint32_t k = 0; k < a.C; ++k) {
-    const uint64_t* __restrict__ p = a.ptrs[k];
+    const uint64_t* __restrict__ p = INTERLEAVED ? src + (uint64_t)k * kWavgPerBlock : a.ptrs[k] + e;
     const uint32_t w0 = a.wl[k][t][0], w1 = a.wl[k][t][1];
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + e));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     // element a: (v.x, v.y), element b: (v.z, v.w); 30-bit limbs
     const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
     const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   uint64_t r0 = wavg_fold(s00a, s01a, s10a, s11a, c);
   uint64_t r1 = wavg_fold(s00b, s01b, s10b, s11b, c);
   if (a.accumulate) {  // learners beyond the first 16: fold into the running sum
-    const uint4 o = *reinterpret_cast<const uint4*>(a.out + e);
+    const u32x4 o = *reinterpret_cast<const u32x4*>(a.out + e);
     r0 = addmod(r0, (uint64_t)o.x | ((uint64_t)o.y << 32), c.q);
     r1 = addmod(r1, (uint64_t)o.z | ((uint64_t)o.w << 32), c.q);
   }
@@ -152,7 +164,10 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t blocks = total / kWavgPerBlock;
   if (!blocks) return;
   if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  hipLaunchKernelGGL(wavg_kernel, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+  if (a.arena)
+    hipLaunchKernelGGL(wavg_kernel<true>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+  else
+    hipLaunchKernelGGL(wavg_kernel<false>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());
 }
 

@@ -115,12 +115,15 @@ namespace shelfi {
 
 // device-side launchers (kernels.hip)
 constexpr int kWavgMaxLearners = 16;  // per launch (limb sums stay < 2^64)
+constexpr int kArenaChunk = 512;      // residues per (chunk, learner) slice of an arena
 struct WavgArgs {
-  const uint64_t* ptrs[kWavgMaxLearners];          // learner ciphertext batches (device)
+  const uint64_t* ptrs[kWavgMaxLearners];          // SEPARATE layout: learner batches
   uint32_t wl[kWavgMaxLearners][kMaxTowers][2];    // 30-bit limbs of W_{c,t}
+  const uint64_t* arena;                           // INTERLEAVED layout (or null)
   uint64_t* out;
   uint64_t rows;  // K * 2 * L
   uint32_t C, L, logN, accumulate;
+  uint32_t arena_learners, first_learner;          // arena width, first learner of this pass
 };
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,

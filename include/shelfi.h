@@ -122,6 +122,17 @@ size_t shelfi_blob_header_bytes(void);
  * EvalAdd, ckks.cpp:286-297).  in_dev: host array of C device pointers. */
 int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float* w, size_t C,
                     size_t K, uint64_t* out_dev, void* stream);
+/* Learner-interleaved arena: the aggregator's resident layout for C learners' K
+ * ciphertexts, uint64 [K*2*L*N/512][C][512] (512-residue slices of every learner side
+ * by side), so one aggregation block reads one contiguous C x 4 KiB region.
+ * shelfi_arena_words() = C*K*2*L*N.  shelfi_dev_arena_put copies learner `learner`'s
+ * [K][2][L][N] batch (device memory, or host memory if src_on_host) into its slices. */
+size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K);
+int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size_t K, size_t learner,
+                         size_t C, uint64_t* arena_dev, void* stream);
+/* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
+int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
+                          size_t K, uint64_t* out_dev, void* stream);
 /* Folds a collective's uint64 SUM of G <= 15 reduced partial sums back into [0, q_t)
  * (multi-GPU combine: local shelfi_dev_wavg -> RCCL reduce/reduce_scatter -> this). */
 int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream);

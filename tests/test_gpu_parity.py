@@ -136,6 +136,30 @@ def test_wavg_device_bitexact(cfg, C, K, request):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("C,K", [(16, 3), (20, 2), (1, 1), (5, 4)])
+def test_wavg_arena_bitexact(cfg2, C, K):
+    """Learner-interleaved arena (device and host-blob placement) == oracle."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    L = len(q)
+    rng = np.random.default_rng(C * 7 + K)
+    cts = []
+    for _ in range(C):
+        a = np.empty((K, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+        cts.append(a)
+    w = list(rng.dirichlet(np.ones(C)))
+    ar = D.Arena(cfg2, C, K)
+    for c in range(C):
+        if c % 2:
+            ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
+        else:  # host bytes path: a blob holding these residues
+            ar.put(c, m.blob_pack(cfg2, cts[c]))
+    got = ar.wavg(w)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+
+
 def test_wavg_extremes(cfg2):
     """Residues at q-1 and 0, weights 1.0 (W = Delta = q_{L-1}) and tiny."""
     inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
