@@ -105,16 +105,23 @@ class Arena:
                                                int(learner), self.C, C.c_void_p(self.buf.data_ptr()),
                                                C.c_void_p(_stream_ptr(ct))), "arena_put")
 
-    def wavg(self, weights: Sequence[float], out=None):
+    def wavg(self, weights: Sequence[float], out=None, k0: int = 0, k1: int | None = None):
+        """Aggregate ciphertexts [k0, k1) of every learner into out[:k1-k0]."""
         torch = _torch()
         if len(weights) != self.C:
             raise ValueError("need one weight per learner")
+        k1 = self.K if k1 is None else int(k1)
+        if not (0 <= k0 <= k1 <= self.K):
+            raise ValueError("bad ciphertext range")
+        Kr = k1 - k0
         if out is None:
-            out = torch.empty((self.K, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
-        _check_ct(out, self.ckks, self.K)
+            out = torch.empty((Kr, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
+        _check_ct(out, self.ckks, Kr)
         w = (C.c_float * self.C)(*[float(x) for x in weights])
-        check(_lib.load().shelfi_dev_wavg_arena(self.ckks._ctx, C.c_void_p(self.buf.data_ptr()), w, self.C,
-                                                self.K, C.c_void_p(out.data_ptr()),
+        # ciphertexts [k0, k1) of an arena are themselves an arena of k1-k0 ciphertexts
+        base = self.buf.data_ptr() + k0 * 2 * self.L * self.N * self.C * 8
+        check(_lib.load().shelfi_dev_wavg_arena(self.ckks._ctx, C.c_void_p(base), w, self.C, Kr,
+                                                C.c_void_p(out.data_ptr()),
                                                 C.c_void_p(_stream_ptr(out))), "dev_wavg_arena")
         return out
 

@@ -92,6 +92,84 @@ def aggregate(ckks, local_cts: Sequence, local_weights: Sequence[float], mode: s
     return share
 
 
+def pipeline_pieces(K: int, world: int, pieces: int):
+    """Split K ciphertexts into up to `pieces` consecutive pieces [(k0, k1)], each
+    reduce-scattered on its own (its buffer padded to a multiple of `world`)."""
+    pieces = max(1, min(pieces, K))
+    base, extra = divmod(K, pieces)
+    out, s = [], 0
+    for j in range(pieces):
+        n = base + (1 if j < extra else 0)
+        out.append((s, s + n))
+        s += n
+    return out
+
+
+class PipelinedCombine:
+    """Learner-sharded aggregation with the collective overlapped with compute.
+
+    The K ciphertexts are cut into pieces; piece j's local wavg (on the current
+    stream) is followed by an async reduce_scatter of that piece, which runs on the
+    collective's own stream while piece j+1 is being aggregated.  Rank g ends up
+    owning slice g of every piece (owned_ranges()).  Buffers are allocated once:
+    `partial` holds every piece padded to a multiple of world (zero padding is the
+    additive identity and is written only at construction)."""
+
+    def __init__(self, K: int, ct_shape, pieces: int = 4, device=None, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > max_world():
+            raise ValueError("more than %d ranks would overflow the uint64 partial sum" % max_world())
+        self.K = K
+        self.pieces = pipeline_pieces(K, self.world, pieces)
+        self.padded = [-(-(k1 - k0) // self.world) * self.world for k0, k1 in self.pieces]
+        tot = sum(self.padded)
+        self.partial = torch.zeros((tot,) + tuple(ct_shape), dtype=torch.int64, device=device)
+        self.views, self.shares, off = [], [], 0
+        for (k0, k1), p in zip(self.pieces, self.padded):
+            self.views.append(self.partial[off:off + p])
+            self.shares.append(torch.empty((p // self.world,) + tuple(ct_shape), dtype=torch.int64,
+                                           device=device))
+            off += p
+
+    def owned_ranges(self):
+        """Global ciphertext ranges [(k0, k1)] this rank holds after run()."""
+        out = []
+        for (k0, k1), p in zip(self.pieces, self.padded):
+            per = p // self.world
+            a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
+            if b > a:
+                out.append((a, b))
+        return out
+
+    def run(self, compute_piece, fold_share=None):
+        """compute_piece(k0, k1, out_view) writes the local partial sums of
+        ciphertexts [k0, k1) into out_view[:k1-k0]; fold_share(share_view) reduces a
+        summed share mod q.  Returns [(k0, k1, share_view)] owned by this rank."""
+        import torch.distributed as dist
+
+        works = []
+        for (k0, k1), view, share in zip(self.pieces, self.views, self.shares):
+            compute_piece(k0, k1, view[:k1 - k0])
+            works.append(dist.reduce_scatter_tensor(share, view, op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+        owned = []
+        for (k0, k1), p, share, w in zip(self.pieces, self.padded, self.shares, works):
+            w.wait()
+            per = p // self.world
+            a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
+            if b > a:
+                sv = share[:b - a]
+                if fold_share is not None:
+                    fold_share(sv)
+                owned.append((a, b, sv))
+        return owned
+
+
 def slice_of_rank(K: int, world: int, rank: int):
     """Ciphertext range [start, stop) a rank holds after reduce_scatter (equal padded
     slices, the last rank possibly shorter)."""

@@ -171,6 +171,81 @@ def _gloo_worker(rank, world, port, mode, result_q):
         dist_.destroy_process_group()
 
 
+def _gloo_pipelined_worker(rank, world, port, pieces, result_q):
+    import torch
+    import torch.distributed as dist_
+
+    import oracle as O_
+    from SHELFI_FHE import dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist_.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, L, K, C_ = 1024, 2, 7, 5
+        q, psi = O_.params_generate(N, L, 40, 50)
+        delta = float(int(q[-1]))
+        rng = np.random.default_rng(5)
+        cts = []
+        for _ in range(C_):
+            a = np.empty((K, 2, L, N), np.uint64)
+            for t in range(L):
+                a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+            cts.append(a)
+        w = list(rng.dirichlet(np.ones(C_)))
+        mine = dist.learner_shard(C_, rank, world)
+        comb = dist.PipelinedCombine(K, (2, L, N), pieces=pieces)
+
+        def compute(k0, k1, view):  # the arena wavg kernel's job, by the oracle
+            part = O_.wavg([cts[i][k0:k1] for i in mine], [w[i] for i in mine], q, delta)
+            view.copy_(torch.from_numpy(part.view(np.int64).copy()))
+
+        def fold(share):  # the modq kernel's job
+            s = share.numpy().view(np.uint64)
+            for t in range(L):
+                s[:, :, t, :] %= q[t]
+
+        owned = comb.run(compute, fold)
+        full = O_.wavg(cts, w, q, delta)
+        ok = all(np.array_equal(s.numpy().view(np.uint64), full[a:b]) for a, b, s in owned)
+        ok &= [(a, b) for a, b, _ in owned] == comb.owned_ranges()
+        # every ciphertext is owned by exactly one rank
+        allr = [None] * world
+        dist_.all_gather_object(allr, comb.owned_ranges())
+        cover = sorted(x for r in allr for a, b in r for x in range(a, b))
+        ok &= cover == list(range(K))
+        result_q.put((rank, bool(ok)))
+    finally:
+        dist_.destroy_process_group()
+
+
+def _spawn_world2(target, *args):
+    import multiprocessing as mp
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q_ = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, 2, port) + args + (q_,)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q_.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    return sorted(res)
+
+
+@pytest.mark.parametrize("pieces", [1, 3, 4])
+def test_pipelined_combine_gloo_world2(pieces):
+    """bench.py's N>1 step: per-piece wavg overlapped with async reduce_scatter; the
+    owned shares (after mod q) equal the single-process aggregation, bit-exact, and
+    the ranks' shares tile [0, K)."""
+    pytest.importorskip("torch")
+    assert _spawn_world2(_gloo_pipelined_worker, pieces) == [(0, True), (1, True)]
+
+
 @pytest.mark.parametrize("mode", ["reduce_scatter", "reduce", "all_reduce"])
 def test_distributed_combine_gloo_world2(mode):
     """world_size-2 gloo run of the multi-GPU combine: learner sharding + int64 SUM
