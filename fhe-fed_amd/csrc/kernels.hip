@@ -48,6 +48,47 @@ __device__ __forceinline__ uint64_t red64(uint64_t x, uint64_t q, uint64_t one_s
   uint64_t r = x - hi * q;
   return r >= q ? r - q : r;
 }
+// ---- lazy NTT arithmetic (bit-exact after the final canonicalisation) -----
+// High 64 bits of x*y from three 32x32 partial products (x0*y0 dropped): equals the
+// exact value or one less.
+__device__ __forceinline__ uint64_t umulhi_approx(uint64_t x, uint64_t y) {
+  const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
+  const uint64_t t = (uint64_t)x1 * y0;
+  const uint64_t u = (uint64_t)x0 * y1 + (uint32_t)t;
+  return (uint64_t)x1 * y1 + (t >> 32) + (u >> 32);
+}
+// x * w mod q up to 2 extra q: result in [0, 3q) for any 64-bit x (Shoup, no correction).
+__device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
+  return x * w - umulhi_approx(x, wp) * q;
+}
+// Forward (CT) butterfly keeping values in [0, 8q) (q < 2^60, so 8q < 2^63).
+__device__ __forceinline__ void ct_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
+                                        uint64_t q, uint64_t q3, uint64_t q4) {
+  const uint64_t x = X >= q4 ? X - q4 : X;  // [0, 4q)
+  const uint64_t t = shoup_lazy(Y, W, Wp, q);  // [0, 3q)
+  X = x + t;                                 // [0, 7q)
+  Y = x - t + q3;                            // (0, 7q)
+}
+// Inverse (GS) butterfly keeping values in [0, 4q).
+__device__ __forceinline__ void gs_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
+                                        uint64_t q, uint64_t q4) {
+  const uint64_t s = X + Y;                  // [0, 8q)
+  const uint64_t d = X - Y + q4;             // (0, 8q)
+  X = s >= q4 ? s - q4 : s;                  // [0, 4q)
+  Y = shoup_lazy(d, W, Wp, q);               // [0, 3q)
+}
+// [0, 8q) -> [0, q)
+__device__ __forceinline__ uint64_t canon8(uint64_t x, uint64_t q) {
+  x = x >= 4 * q ? x - 4 * q : x;
+  x = x >= 2 * q ? x - 2 * q : x;
+  return x >= q ? x - q : x;
+}
+// [0, 4q) -> [0, q)
+__device__ __forceinline__ uint64_t canon4(uint64_t x, uint64_t q) {
+  x = x >= 2 * q ? x - 2 * q : x;
+  return x >= q ? x - q : x;
+}
+
 // a * b mod q for arbitrary a, b < q (no precomputed companion).
 __device__ __forceinline__ uint64_t mulmod_generic(uint64_t a, uint64_t b, const TowerConst& c) {
   uint64_t hi = __umul64hi(a, b), lo = a * b;
@@ -208,7 +249,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols(uint64_t* __restrict__ polys
   const uint64_t poly = blockIdx.x / bpp;
   const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
   const uint32_t t = (uint32_t)(poly % L);
-  const uint64_t q = tcs[t].q;
+  const uint64_t q = tcs[t].q, q3 = 3 * q, q4 = 4 * q;
   const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
   const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
   uint64_t* __restrict__ a = polys + poly * N + col;
@@ -224,14 +265,167 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        const uint64_t U = x[r0], V = shoup_mul(x[r1], W, Wp, q);
-        x[r0] = addmod(U, V, q);
-        x[r1] = submod(U, V, q);
+        ct_bfly(x[r0], x[r1], W, Wp, q, q3, q4);
       }
     }
   }
+  // lazy values in [0, 8q): the blocks pass that follows canonicalises
 #pragma unroll
   for (int r = 0; r < R; ++r) a[(uint64_t)r * BLK] = x[r];
+}
+
+// ---- LDS block passes: radix-2^k register chunks -------------------------
+// LDS layout: plain.  An XOR swizzle (i ^ h(i >> 5)) that removes the 8-/4-way bank
+// conflicts of the d = 4 / d = 1 chunks measured SLOWER (30.4 vs 27.5 ms for the
+// ntt_fwd_blocks share of a 11,424-ciphertext encrypt sweep): this pass is bound by
+// VALU issue (64-bit Shoup products), not by LDS.  lds_sw is kept as the one place
+// to change the layout.
+__device__ __forceinline__ uint32_t lds_sw(uint32_t i) { return i; }
+// 16-byte fill/drain: elements (2p, 2p+1) share one aligned 16-byte LDS slot under
+// lds_sw, swapped when the XOR flips bit 0.
+__device__ __forceinline__ void lds_put2(uint64_t* sm, uint32_t p, ulonglong2 v) {
+  const uint32_t i = 2 * p, s = lds_sw(i);
+  if (s & 1) {
+    const uint64_t t = v.x;
+    v.x = v.y;
+    v.y = t;
+  }
+  reinterpret_cast<ulonglong2*>(sm)[s >> 1] = v;
+}
+__device__ __forceinline__ ulonglong2 lds_get2(const uint64_t* sm, uint32_t p) {
+  const uint32_t i = 2 * p, s = lds_sw(i);
+  ulonglong2 v = reinterpret_cast<const ulonglong2*>(sm)[s >> 1];
+  if (s & 1) {
+    const uint64_t t = v.x;
+    v.x = v.y;
+    v.y = t;
+  }
+  return v;
+}
+// A block of blk = 2^blkLog contiguous elements (global block index b) sits in LDS.
+// Its stages are taken KCH = 3 at a time: each thread loads a set of 2^KCH elements
+// that only interact among themselves during those stages, runs them in registers
+// (2^KCH - 1 twiddle pairs), and writes the set back — one barrier per chunk instead
+// of one per stage.  256 threads, blk <= 2048 (so at most 8 elements per thread).
+//
+// Forward (CT, half-size h = blk/2 .. 1): a chunk of k stages starting at half-size
+// h0 works on sets {j0 + d m}, d = h0 / 2^(k-1), j0 = g 2 h0 + off (off < d).
+template <int KC>
+__device__ __forceinline__ void fwd_chunk(uint64_t* sm, uint32_t blk, uint32_t h0Log, uint32_t b,
+                                          uint32_t blkLog, uint32_t logN,
+                                          const uint64_t* __restrict__ w,
+                                          const uint64_t* __restrict__ wp, uint64_t q) {
+  constexpr int M = 1 << KC;
+  const uint32_t dLog = h0Log - (KC - 1), d = 1u << dLog;
+  const uint32_t nsets = blk >> KC;
+  const uint64_t gbase = (uint64_t)b << blkLog;  // global index of the block start
+  for (uint32_t set = threadIdx.x; set < nsets; set += 256) {
+    const uint32_t g = set >> dLog, off = set & (d - 1);
+    const uint32_t j0 = (g << (h0Log + 1)) + off;
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = sm[lds_sw(j0 + (m << dLog))];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int hm = 1 << (KC - 1 - i);          // half-size in units of d
+      const uint32_t hLog = h0Log - i;           // log2 of the half-size
+      const uint32_t s = logN - 1 - hLog;        // global stage: m_stage = 2^s
+#pragma unroll
+      for (int gs = 0; gs < (1 << i); ++gs) {    // 2^i twiddle groups at this stage
+        const uint64_t gi = (gbase + j0 + ((uint64_t)(gs * 2 * hm) << dLog)) >> (hLog + 1);
+        const uint64_t W = w[(1ull << s) + gi], Wp = wp[(1ull << s) + gi];
+#pragma unroll
+        for (int mm = 0; mm < hm; ++mm) {
+          const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
+          ct_bfly(x[m0], x[m1], W, Wp, q, 3 * q, 4 * q);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) sm[lds_sw(j0 + (m << dLog))] = x[m];
+  }
+}
+
+// Runs every stage of the block (local half-sizes blk/2 .. 1), chunked 3 at a time.
+__device__ __forceinline__ void ntt_fwd_block_stages(uint64_t* sm, uint32_t blkLog, uint32_t b,
+                                                     uint32_t logN, const uint64_t* __restrict__ w,
+                                                     const uint64_t* __restrict__ wp, uint64_t q) {
+  const uint32_t blk = 1u << blkLog;
+  uint32_t left = blkLog;  // stages remaining; next half-size = 2^(left-1)
+  while (left > 0) {
+    const uint32_t h0Log = left - 1;
+    if (left >= 3) {
+      fwd_chunk<3>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 3;
+    } else if (left == 2) {
+      fwd_chunk<2>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 2;
+    } else {
+      fwd_chunk<1>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 1;
+    }
+    __syncthreads();
+  }
+}
+
+// Inverse (GS, half-size t = 1 .. blk/2): a chunk of k stages starting at half-size
+// t0 works on sets {j0 + t0 m}, j0 = g t0 2^k + off (off < t0); twiddle for half-size
+// t at global element j: ipsi_rev[N/(2t) + j/(2t)].
+template <int KC>
+__device__ __forceinline__ void inv_chunk(uint64_t* sm, uint32_t blk, uint32_t t0Log, uint32_t b,
+                                          uint32_t blkLog, uint32_t logN,
+                                          const uint64_t* __restrict__ w,
+                                          const uint64_t* __restrict__ wp, uint64_t q) {
+  constexpr int M = 1 << KC;
+  const uint32_t t0 = 1u << t0Log;
+  const uint32_t nsets = blk >> KC;
+  const uint64_t gbase = (uint64_t)b << blkLog;
+  for (uint32_t set = threadIdx.x; set < nsets; set += 256) {
+    const uint32_t g = set >> t0Log, off = set & (t0 - 1);
+    const uint32_t j0 = (g << (t0Log + KC)) + off;
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = sm[lds_sw(j0 + (m << t0Log))];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int hm = 1 << i;                  // half-size in units of t0
+      const uint32_t tLog = t0Log + i;
+      const uint64_t hbase = (uint64_t)1 << (logN - 1 - tLog);  // N / (2t)
+#pragma unroll
+      for (int gs = 0; gs < (M >> (i + 1)); ++gs) {
+        const uint64_t gi = (gbase + j0 + ((uint64_t)(gs * 2 * hm) << t0Log)) >> (tLog + 1);
+        const uint64_t W = w[hbase + gi], Wp = wp[hbase + gi];
+#pragma unroll
+        for (int mm = 0; mm < hm; ++mm) {
+          const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
+          gs_bfly(x[m0], x[m1], W, Wp, q, 4 * q);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) sm[lds_sw(j0 + (m << t0Log))] = x[m];
+  }
+}
+
+__device__ __forceinline__ void ntt_inv_block_stages(uint64_t* sm, uint32_t blkLog, uint32_t b,
+                                                     uint32_t logN, const uint64_t* __restrict__ w,
+                                                     const uint64_t* __restrict__ wp, uint64_t q) {
+  const uint32_t blk = 1u << blkLog;
+  uint32_t t0Log = 0;
+  while (t0Log < blkLog) {
+    const uint32_t left = blkLog - t0Log;
+    if (left >= 3) {
+      inv_chunk<3>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 3;
+    } else if (left == 2) {
+      inv_chunk<2>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 2;
+    } else {
+      inv_chunk<1>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 1;
+    }
+    __syncthreads();
+  }
 }
 
 // Blocks pass, stages s = sstart .. logN-1 on contiguous blocks of 2^(logN-sstart).
@@ -247,31 +441,19 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks(uint64_t* __restrict__ pol
   const uint32_t b = blockIdx.x & (nb - 1);
   const uint32_t t = (uint32_t)(poly % L);
   const uint64_t q = tcs[t].q;
-  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
-  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
   uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
-  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
-    reinterpret_cast<ulonglong2*>(sm)[i] = reinterpret_cast<const ulonglong2*>(a)[i];
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256)
+    lds_put2(sm, p, reinterpret_cast<const ulonglong2*>(a)[p]);
   __syncthreads();
-  for (uint32_t s = sstart; s < logN; ++s) {
-    const uint32_t m = 1u << s, tlog = logN - 1 - s, tt = 1u << tlog;
-    for (uint32_t k = threadIdx.x; k < blk / 2; k += 256) {
-      const uint32_t j = ((k >> tlog) << (tlog + 1)) | (k & (tt - 1));
-      const uint32_t gi = (b << (blkLog - tlog - 1)) + (k >> tlog);
-      const uint64_t W = w[m + gi], Wp = wp[m + gi];
-      const uint64_t U = sm[j], V = shoup_mul(sm[j + tt], W, Wp, q);
-      sm[j] = addmod(U, V, q);
-      sm[j + tt] = submod(U, V, q);
-    }
-    __syncthreads();
+  ntt_fwd_block_stages(sm, blkLog, b, logN, tw + (uint64_t)t * N, twp + (uint64_t)t * N, q);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+    const ulonglong2 v = lds_get2(sm, p);
+    reinterpret_cast<ulonglong2*>(a)[p] = make_ulonglong2(canon8(v.x, q), canon8(v.y, q));
   }
-  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
-    reinterpret_cast<ulonglong2*>(a)[i] = reinterpret_cast<const ulonglong2*>(sm)[i];
 }
 
-// Inverse (Gentleman-Sande, bit-reversed -> natural), stage with half-size tt
-// pairs (j, j+tt), twiddle ipsi_rev[N/(2tt) + j/(2tt)]; small tt first (LDS
-// blocks), then the top LOGR stages on register columns, scaled by N^-1.
+// Inverse blocks pass: small half-sizes first (LDS), then the top LOGR stages on
+// register columns (ntt_inv_cols), scaled by N^-1 in the last pass.
 __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ polys, uint32_t L,
                                                       uint32_t logN, uint32_t blkLog,
                                                       const uint64_t* __restrict__ tw,
@@ -286,31 +468,21 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
   const uint32_t t = (uint32_t)(poly % L);
   const TowerConst& c = tcs[t];
   const uint64_t q = c.q;
-  const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
-  const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
   uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
-  for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
-    reinterpret_cast<ulonglong2*>(sm)[i] = reinterpret_cast<const ulonglong2*>(a)[i];
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256)
+    lds_put2(sm, p, reinterpret_cast<const ulonglong2*>(a)[p]);
   __syncthreads();
-  for (uint32_t u = 0; u < blkLog; ++u) {
-    const uint32_t tt = 1u << u;
-    const uint32_t h = N >> (u + 1);
-    for (uint32_t k = threadIdx.x; k < blk / 2; k += 256) {
-      const uint32_t j = ((k >> u) << (u + 1)) | (k & (tt - 1));
-      const uint32_t gi = (b << (blkLog - u - 1)) + (k >> u);
-      const uint64_t W = w[h + gi], Wp = wp[h + gi];
-      const uint64_t U = sm[j], V = sm[j + tt];
-      sm[j] = addmod(U, V, q);
-      sm[j + tt] = shoup_mul(submod(U, V, q), W, Wp, q);
-    }
-    __syncthreads();
-  }
+  ntt_inv_block_stages(sm, blkLog, b, logN, tw + (uint64_t)t * N, twp + (uint64_t)t * N, q);
   if (scale_ninv) {
     const uint64_t ni = c.ninv, nip = c.ninv_shoup;
-    for (uint32_t i = threadIdx.x; i < blk; i += 256) a[i] = shoup_mul(sm[i], ni, nip, q);
-  } else {
-    for (uint32_t i = threadIdx.x; i < blk / 2; i += 256)
-      reinterpret_cast<ulonglong2*>(a)[i] = reinterpret_cast<const ulonglong2*>(sm)[i];
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const ulonglong2 v = lds_get2(sm, p);
+      reinterpret_cast<ulonglong2*>(a)[p] = make_ulonglong2(canon4(shoup_lazy(v.x, ni, nip, q), q),
+                                                            canon4(shoup_lazy(v.y, ni, nip, q), q));
+    }
+  } else {  // lazy values in [0, 4q): the columns pass canonicalises
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256)
+      reinterpret_cast<ulonglong2*>(a)[p] = lds_get2(sm, p);
   }
 }
 
@@ -343,15 +515,13 @@ __global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        const uint64_t U = x[r0], V = x[r1];
-        x[r0] = addmod(U, V, q);
-        x[r1] = shoup_mul(submod(U, V, q), W, Wp, q);
+        gs_bfly(x[r0], x[r1], W, Wp, q, 4 * q);
       }
     }
   }
   const uint64_t ni = c.ninv, nip = c.ninv_shoup;
 #pragma unroll
-  for (int r = 0; r < R; ++r) a[(uint64_t)r * BLK] = shoup_mul(x[r], ni, nip, q);
+  for (int r = 0; r < R; ++r) a[(uint64_t)r * BLK] = canon4(shoup_lazy(x[r], ni, nip, q), q);
 }
 
 #define NTT_DISPATCH(LOGRV, KERNEL, ...)                                                   \
@@ -603,10 +773,14 @@ __device__ __forceinline__ int64_t gauss_sample(uint64_t r, const uint64_t* __re
 __device__ __forceinline__ int64_t ternary_sample(uint64_t r) { return (int64_t)(r % 3) - 1; }
 
 // -------------------------------------------------------------- encrypt ----
-// One thread = 8 consecutive coefficients of one ciphertext (one ChaCha20 block
-// per sampled polynomial).  m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at
-// j = i*gap (real) and N/2 + i*gap (imag) (CKKSPackedEncoding::Encode layout).
+// One thread = ChaCha20 block bb of each sampled polynomial, which feeds the 8
+// coefficients j = bb + u N/8 (u = 0..7) — so every store below is a coalesced
+// 8-byte-per-lane row.  m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at j = i*gap
+// (real part) and N/2 + i*gap (imaginary part) (CKKSPackedEncoding::Encode layout).
 // Writes [K][3][L][N]: v, m + e0, e1 reduced per tower (COEFFICIENT domain).
+__device__ __forceinline__ uint64_t small_mod(int64_t v, uint64_t q) {  // |v| < q
+  return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v;
+}
 __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
                                                        uint64_t K, uint32_t logN, uint32_t logS,
                                                        uint32_t L, double delta,
@@ -615,23 +789,23 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
                                                        Key8 key, uint64_t g0,
                                                        uint64_t* __restrict__ out,
                                                        uint32_t* __restrict__ flag) {
-  const uint32_t N = 1u << logN, S = 1u << logS;
+  const uint32_t N = 1u << logN, S = 1u << logS, E = N >> 3;
   const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = gid >> (logN - 3);
   if (k >= K) return;
-  const uint32_t j0 = (uint32_t)(gid & ((N >> 3) - 1)) * 8;
+  const uint32_t bb = (uint32_t)(gid & (E - 1));
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   uint64_t rv[8], re0[8], re1[8];
-  chacha20_block(key, j0 >> 3, nonce, rv);
-  chacha20_block(key, (N >> 3) + (j0 >> 3), nonce, re0);
-  chacha20_block(key, 2 * (N >> 3) + (j0 >> 3), nonce, re1);
+  chacha20_block(key, bb, nonce, rv);
+  chacha20_block(key, E + bb, nonce, re0);
+  chacha20_block(key, 2 * E + bb, nonce, re1);
   const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
   const double dS = (double)S;
   const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
   int64_t mv[8], vv[8], e1v[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    const uint32_t j = j0 + u;
+    const uint32_t j = bb + u * E;
     const uint32_t jj = j < half ? j : j - half;
     int64_t m = 0;
     if ((jj & ((1u << gapLog) - 1)) == 0) {
@@ -647,14 +821,14 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
   }
   for (uint32_t t = 0; t < L; ++t) {
     const TowerConst c = tcs[t];
-    ulonglong2* o0 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 0) * L + t) * N + j0);
-    ulonglong2* o1 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 1) * L + t) * N + j0);
-    ulonglong2* o2 = reinterpret_cast<ulonglong2*>(out + ((k * 3 + 2) * L + t) * N + j0);
+    uint64_t* o0 = out + ((k * 3 + 0) * L + t) * N + bb;
+    uint64_t* o1 = out + ((k * 3 + 1) * L + t) * N + bb;
+    uint64_t* o2 = out + ((k * 3 + 2) * L + t) * N + bb;
 #pragma unroll
-    for (int u = 0; u < 8; u += 2) {
-      o0[u / 2] = make_ulonglong2(mod_signed_dev(vv[u], c), mod_signed_dev(vv[u + 1], c));
-      o1[u / 2] = make_ulonglong2(mod_signed_dev(mv[u], c), mod_signed_dev(mv[u + 1], c));
-      o2[u / 2] = make_ulonglong2(mod_signed_dev(e1v[u], c), mod_signed_dev(e1v[u + 1], c));
+    for (int u = 0; u < 8; ++u) {
+      o0[u * E] = small_mod(vv[u], c.q);
+      o1[u * E] = mod_signed_dev(mv[u], c);
+      o2[u * E] = small_mod(e1v[u], c.q);
     }
   }
 }

@@ -687,6 +687,7 @@ int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
 /*   counter64 (words 12,13) | nonce64 (words 14,15).                         */
 /*   key[8] = splitmix64(seed) x4, each split lo/hi.                          */
 /*   Stream (nonce, counter): u64 word w = block(w/8) words (2(w%8), 2(w%8)+1)*/
+/*   (encrypt: coefficient j <- word (j mod N/8)*8 + j div N/8, see below)     */
 /*   ternary: r % 3 - 1;  Gaussian: k = #{i : (r>>1) >= cdt[i]}, sign r&1.    */
 /* ------------------------------------------------------------------------ */
 
@@ -772,8 +773,14 @@ static inline int64_t gauss_from_word(uint64_t r, const uint64_t* cdt, int T) {
 }
 static inline int64_t ternary_from_word(uint64_t r) { return (int64_t)(r % 3) - 1; }
 
-/* Encrypt randomness for global ciphertext index g: nonce = (1<<56)|g,
- * v from counter words [0,N), e0 from [N,2N), e1 from [2N,3N). */
+/* Encrypt randomness for global ciphertext index g: nonce = (1<<56)|g; the v, e0,
+ * e1 polynomials use stream words [0,N), [N,2N), [2N,3N).  Coefficient j of a
+ * polynomial takes word widx(j) = (j mod N/8) * 8 + j div (N/8) of its range, i.e.
+ * ChaCha block b feeds coefficients b, b + N/8, ..., b + 7N/8. */
+static inline uint32_t enc_word_index(uint32_t j, uint32_t N) {
+  const uint32_t e = N / 8;
+  return (j % e) * 8 + j / e;
+}
 void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int64_t* v,
                        int64_t* e0, int64_t* e1) {
   uint32_t key[8];
@@ -783,9 +790,10 @@ void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int6
   uint64_t* w = malloc(sizeof(uint64_t) * 3 * N);
   or_stream_words(key, (1ull << 56) | g, 0, 3ull * N, w);
   for (uint32_t j = 0; j < N; ++j) {
-    v[j] = ternary_from_word(w[j]);
-    e0[j] = gauss_from_word(w[N + j], cdt, T);
-    e1[j] = gauss_from_word(w[2ull * N + j], cdt, T);
+    const uint32_t k = enc_word_index(j, N);
+    v[j] = ternary_from_word(w[k]);
+    e0[j] = gauss_from_word(w[N + k], cdt, T);
+    e1[j] = gauss_from_word(w[2ull * N + k], cdt, T);
   }
   free(w);
 }
