@@ -10,10 +10,11 @@
 //   modq_kernel        fold a collective's uint64 sum of partials back to [0,q)
 //   ntt_*              negacyclic NTT/INTT, 2 passes (register columns + LDS blocks)
 //   fft_*              CKKS special FFT / inverse (encode / decode), 2 passes
-//   enc_prep_kernel    round/scale/reduce the encoded slots + ChaCha20 sampling of
-//                      (v, e0, e1) (ckks.cpp:80-81)
-//   enc_combine_kernel c0 = v*b + (m + e0), c1 = v*a + e1
-//   dec_combine_kernel c0 + c1*s (ckks.cpp:189)
+//   enc_prep_kernel    round/scale the encoded slots + ChaCha20 sampling of (v, e0, e1)
+//                      into a compact 10-byte record per coefficient (ckks.cpp:80-81)
+//   ntt_fwd_cols_enc   expand the record per tower + first NTT stages
+//   ntt_fwd_blocks_enc last NTT stages of v, m+e0, e1 + c0 = v*b + (m+e0), c1 = v*a + e1
+//   ntt_inv_blocks     (decrypt) c0 + c1*s formed in its LDS fill (ckks.cpp:189)
 //   crt_decode_kernel  exact centered CRT -> double / scale, bit-reversed scatter
 //   keygen_*           ternary s, Gaussian e, uniform a; b = e - a*s
 //
@@ -98,6 +99,9 @@ __device__ __forceinline__ uint64_t mod_signed_dev(int64_t v, const TowerConst& 
   if (v >= 0) return red64((uint64_t)v, c.q, c.one_shoup);
   uint64_t r = red64((uint64_t)0 - (uint64_t)v, c.q, c.one_shoup);
   return r ? c.q - r : 0;
+}
+__device__ __forceinline__ uint64_t small_mod(int64_t v, uint64_t q) {  // |v| < q
+  return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v;
 }
 __device__ __forceinline__ uint32_t bitrev_dev(uint32_t x, uint32_t bits) {
   return bits ? (__brev(x) >> (32 - bits)) : 0;
@@ -452,14 +456,92 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks(uint64_t* __restrict__ pol
   }
 }
 
+// Encrypt's last NTT pass fused with the public-key combine: one workgroup owns block
+// b of tower t of ciphertext k, transforms v, m + e0 and e1 (pbuf [K][3][L][N], lazy
+// after the columns pass) one after the other through the same LDS block, and writes
+// c0 = v*b + (m + e0), c1 = v*a + e1 (ckks.cpp:81, PALISADE Encrypt) — the transformed
+// polynomials never return to HBM.
+__global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __restrict__ pbuf,
+                                                          uint32_t L, uint32_t logN, uint32_t sstart,
+                                                          const uint64_t* __restrict__ tw,
+                                                          const uint64_t* __restrict__ twp,
+                                                          const TowerConst* __restrict__ tcs,
+                                                          const uint64_t* __restrict__ pk,
+                                                          const uint64_t* __restrict__ pksh,
+                                                          uint64_t* __restrict__ ct,
+                                                          const int64_t* __restrict__ me0,
+                                                          const int16_t* __restrict__ ve) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  constexpr int PP = 4;  // 16-byte pairs per thread (blk <= 2048)
+  const uint32_t blkLog = logN - sstart, blk = 1u << blkLog;
+  const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
+  const uint64_t rest = blockIdx.x >> sstart;
+  const uint32_t t = (uint32_t)(rest % L);
+  const uint64_t k = rest / L;
+  const uint64_t q = tcs[t].q;
+  const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
+  const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << blkLog);  // within [L][N]
+  const uint64_t LN = (uint64_t)L << logN;
+  ulonglong2 V[PP], M[PP];
+#pragma unroll
+  for (int poly = 0; poly < 3; ++poly) {
+    if (me0) {  // single-pass ring: expand the compact sample record (no columns pass)
+      const TowerConst& cst = tcs[t];
+      const uint64_t base = (k << logN) + ((uint64_t)b << blkLog);
+      for (uint32_t i = threadIdx.x; i < blk; i += 256) {
+        const int32_t sv = ve[base + i];
+        sm[lds_sw(i)] = poly == 1 ? mod_signed_dev(me0[base + i], cst)
+                                  : small_mod(poly == 0 ? (int32_t)(int8_t)(sv & 0xFF) : (sv >> 8), q);
+      }
+    } else {
+      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + poly) * LN + off);
+      for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) lds_put2(sm, p, src[p]);
+    }
+    __syncthreads();
+    ntt_fwd_block_stages(sm, blkLog, b, logN, w, wp, q);
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+      const uint32_t p = threadIdx.x + 256 * i;
+      if (p >= blk / 2) break;
+      ulonglong2 v = lds_get2(sm, p);
+      v = make_ulonglong2(canon8(v.x, q), canon8(v.y, q));
+      const uint64_t e = off + 2 * p;
+      if (poly == 0) {
+        V[i] = v;
+      } else if (poly == 1) {
+        M[i] = v;
+      } else {
+        const ulonglong2 B = *reinterpret_cast<const ulonglong2*>(pk + e);
+        const ulonglong2 Bs = *reinterpret_cast<const ulonglong2*>(pksh + e);
+        const ulonglong2 A = *reinterpret_cast<const ulonglong2*>(pk + LN + e);
+        const ulonglong2 As = *reinterpret_cast<const ulonglong2*>(pksh + LN + e);
+        ulonglong2 c0, c1;
+        c0.x = addmod(shoup_mul(V[i].x, B.x, Bs.x, q), M[i].x, q);
+        c0.y = addmod(shoup_mul(V[i].y, B.y, Bs.y, q), M[i].y, q);
+        c1.x = addmod(shoup_mul(V[i].x, A.x, As.x, q), v.x, q);
+        c1.y = addmod(shoup_mul(V[i].y, A.y, As.y, q), v.y, q);
+        *reinterpret_cast<ulonglong2*>(ct + k * 2 * LN + e) = c0;
+        *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 1) * LN + e) = c1;
+      }
+    }
+    __syncthreads();  // LDS is refilled by the next polynomial
+  }
+}
+
 // Inverse blocks pass: small half-sizes first (LDS), then the top LOGR stages on
 // register columns (ntt_inv_cols), scaled by N^-1 in the last pass.
+// With ct != nullptr the input is decrypt's c0 + c1*s (ckks.cpp:189), formed while
+// filling LDS from the ciphertext batch [K][2][L][N] (poly p = k*L + t).
 __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ polys, uint32_t L,
                                                       uint32_t logN, uint32_t blkLog,
                                                       const uint64_t* __restrict__ tw,
                                                       const uint64_t* __restrict__ twp,
                                                       const TowerConst* __restrict__ tcs,
-                                                      int scale_ninv) {
+                                                      int scale_ninv,
+                                                      const uint64_t* __restrict__ ct,
+                                                      const uint64_t* __restrict__ sk,
+                                                      const uint64_t* __restrict__ sksh) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
   const uint32_t N = 1u << logN, blk = 1u << blkLog;
   const uint32_t sh = logN - blkLog, nb = 1u << sh;
@@ -469,8 +551,21 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
   const TowerConst& c = tcs[t];
   const uint64_t q = c.q;
   uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
-  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256)
-    lds_put2(sm, p, reinterpret_cast<const ulonglong2*>(a)[p]);
+  if (ct) {
+    const uint64_t kk = poly / L, off = ((uint64_t)t << logN) + ((uint64_t)b << blkLog);
+    const ulonglong2* c0 = reinterpret_cast<const ulonglong2*>(ct + (kk * 2 * L << logN) + off);
+    const ulonglong2* c1 = reinterpret_cast<const ulonglong2*>(ct + ((kk * 2 + 1) * L << logN) + off);
+    const ulonglong2* s = reinterpret_cast<const ulonglong2*>(sk + off);
+    const ulonglong2* ss = reinterpret_cast<const ulonglong2*>(sksh + off);
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const ulonglong2 x0 = c0[p], x1 = c1[p], sv = s[p], sw = ss[p];
+      lds_put2(sm, p, make_ulonglong2(addmod(x0.x, shoup_mul(x1.x, sv.x, sw.x, q), q),
+                                      addmod(x0.y, shoup_mul(x1.y, sv.y, sw.y, q), q)));
+    }
+  } else {
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256)
+      lds_put2(sm, p, reinterpret_cast<const ulonglong2*>(a)[p]);
+  }
   __syncthreads();
   ntt_inv_block_stages(sm, blkLog, b, logN, tw + (uint64_t)t * N, twp + (uint64_t)t * N, q);
   if (scale_ninv) {
@@ -556,7 +651,8 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
                        logN, (uint32_t)logR, dt.psi_rev, dt.psi_rev_sh, dt.tc);
   } else {
     hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
-                       logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0);
+                       logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0,
+                       (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr);
     if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
@@ -774,20 +870,18 @@ __device__ __forceinline__ int64_t ternary_sample(uint64_t r) { return (int64_t)
 
 // -------------------------------------------------------------- encrypt ----
 // One thread = ChaCha20 block bb of each sampled polynomial, which feeds the 8
-// coefficients j = bb + u N/8 (u = 0..7) — so every store below is a coalesced
-// 8-byte-per-lane row.  m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at j = i*gap
-// (real part) and N/2 + i*gap (imaginary part) (CKKSPackedEncoding::Encode layout).
-// Writes [K][3][L][N]: v, m + e0, e1 reduced per tower (COEFFICIENT domain).
-__device__ __forceinline__ uint64_t small_mod(int64_t v, uint64_t q) {  // |v| < q
-  return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v;
-}
+// coefficients j = bb + u N/8 (u = 0..7), so every store is a coalesced row.
+// m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at j = i*gap (real part) and
+// N/2 + i*gap (imaginary part) (CKKSPackedEncoding::Encode layout).  Output is the
+// compact per-coefficient record {int64 m + e0, int16 (e1 << 8) | (uint8)v} — 10 bytes
+// instead of the 3 L residues the NTT needs, which ntt_fwd_cols_enc expands per tower.
 __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
                                                        uint64_t K, uint32_t logN, uint32_t logS,
-                                                       uint32_t L, double delta,
-                                                       const TowerConst* __restrict__ tcs,
+                                                       double delta,
                                                        const uint64_t* __restrict__ cdt, int T,
                                                        Key8 key, uint64_t g0,
-                                                       uint64_t* __restrict__ out,
+                                                       int64_t* __restrict__ me0,
+                                                       int16_t* __restrict__ ve,
                                                        uint32_t* __restrict__ flag) {
   const uint32_t N = 1u << logN, S = 1u << logS, E = N >> 3;
   const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -795,78 +889,100 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
   if (k >= K) return;
   const uint32_t bb = (uint32_t)(gid & (E - 1));
   const uint64_t nonce = (1ull << 56) | (g0 + k);
-  uint64_t rv[8], re0[8], re1[8];
-  chacha20_block(key, bb, nonce, rv);
-  chacha20_block(key, E + bb, nonce, re0);
-  chacha20_block(key, 2 * E + bb, nonce, re1);
   const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
   const double dS = (double)S;
   const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
-  int64_t mv[8], vv[8], e1v[8];
+  uint64_t w[8];
+  int32_t vv[8];
+  chacha20_block(key, bb, nonce, w);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) vv[u] = (int32_t)ternary_sample(w[u]);
+  chacha20_block(key, E + bb, nonce, w);
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const uint32_t j = bb + u * E;
     const uint32_t jj = j < half ? j : j - half;
     int64_t m = 0;
     if ((jj & ((1u << gapLog) - 1)) == 0) {
-      const uint32_t i = jj >> gapLog;
-      const double2 cv = fbuf[k * S + bitrev_dev(i, logS)];
+      const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
       const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
       if (fabs(val) > lim) atomicOr(flag, 1u);
       m = round_half_away(val);
     }
-    vv[u] = ternary_sample(rv[u]);
-    mv[u] = m + gauss_sample(re0[u], cdt, T);
-    e1v[u] = gauss_sample(re1[u], cdt, T);
+    me0[(k << logN) + j] = m + gauss_sample(w[u], cdt, T);
   }
-  for (uint32_t t = 0; t < L; ++t) {
-    const TowerConst c = tcs[t];
-    uint64_t* o0 = out + ((k * 3 + 0) * L + t) * N + bb;
-    uint64_t* o1 = out + ((k * 3 + 1) * L + t) * N + bb;
-    uint64_t* o2 = out + ((k * 3 + 2) * L + t) * N + bb;
+  chacha20_block(key, 2 * E + bb, nonce, w);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      o0[u * E] = small_mod(vv[u], c.q);
-      o1[u * E] = mod_signed_dev(mv[u], c);
-      o2[u * E] = small_mod(e1v[u], c.q);
-    }
+  for (int u = 0; u < 8; ++u) {
+    const int32_t e1 = (int32_t)gauss_sample(w[u], cdt, T);
+    ve[(k << logN) + bb + u * E] = (int16_t)((e1 << 8) | (vv[u] & 0xFF));
   }
 }
 
-// c0 = v*b + (m + e0), c1 = v*a + e1 (all EVALUATION).  One thread = 2 residues.
-__global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __restrict__ pbuf,
-                                                          uint64_t K, uint32_t logN, uint32_t L,
-                                                          const uint64_t* __restrict__ pk,
-                                                          const uint64_t* __restrict__ pksh,
-                                                          const TowerConst* __restrict__ tcs,
-                                                          uint64_t* __restrict__ ct) {
-  const uint32_t N = 1u << logN;
-  const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;  // over [K][L][N]
-  const uint64_t LN = (uint64_t)L << logN;
-  const uint64_t k = e / LN;
+// Encrypt's first NTT pass reading the compact sample record (enc_prep_kernel):
+// thread = column c of ciphertext k, coefficients j = c + BLK r.  For every tower the
+// three polynomials v, m + e0, e1 are reduced, run through the first LOGR stages and
+// stored lazily ([0, 8q)) into pbuf [K][3][L][N] for ntt_fwd_blocks_enc.
+template <int LOGR, int POLY>
+__global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restrict__ me0,
+                                                        const int16_t* __restrict__ ve, uint64_t K,
+                                                        uint32_t logN, uint32_t L,
+                                                        const TowerConst* __restrict__ tcs,
+                                                        const uint64_t* __restrict__ tw,
+                                                        const uint64_t* __restrict__ twp,
+                                                        uint64_t* __restrict__ out) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t BLK = (1u << logN) >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t k = blockIdx.x / bpp;
   if (k >= K) return;
-  const uint64_t rem = e - k * LN;  // t*N + j
-  const uint32_t t = (uint32_t)(rem >> logN);
-  const uint64_t q = tcs[t].q;
-  const ulonglong2 V = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 0) * LN + rem);
-  const ulonglong2 M = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 1) * LN + rem);
-  const ulonglong2 E = *reinterpret_cast<const ulonglong2*>(pbuf + (k * 3 + 2) * LN + rem);
-  const ulonglong2 B = *reinterpret_cast<const ulonglong2*>(pk + rem);
-  const ulonglong2 Bs = *reinterpret_cast<const ulonglong2*>(pksh + rem);
-  const ulonglong2 A = *reinterpret_cast<const ulonglong2*>(pk + LN + rem);
-  const ulonglong2 As = *reinterpret_cast<const ulonglong2*>(pksh + LN + rem);
-  ulonglong2 c0, c1;
-  c0.x = addmod(shoup_mul(V.x, B.x, Bs.x, q), M.x, q);
-  c0.y = addmod(shoup_mul(V.y, B.y, Bs.y, q), M.y, q);
-  c1.x = addmod(shoup_mul(V.x, A.x, As.x, q), E.x, q);
-  c1.y = addmod(shoup_mul(V.y, A.y, As.y, q), E.y, q);
-  *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 0) * LN + rem) = c0;
-  *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 1) * LN + rem) = c1;
-  (void)N;
+  const uint32_t c = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t j0 = (k << logN) + c;
+  // POLY: 0 = v, 1 = m + e0, 2 = e1 (one launch each keeps one source array live)
+  int64_t val[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t j = j0 + (uint64_t)BLK * r;
+    if (POLY == 1) {
+      val[r] = me0[j];
+    } else {
+      const int32_t sv = ve[j];
+      val[r] = POLY == 0 ? (int32_t)(int8_t)(sv & 0xFF) : (sv >> 8);
+    }
+  }
+#pragma unroll 1
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst cst = tcs[t];
+    const uint64_t q = cst.q, q3 = 3 * q, q4 = 4 * q;
+    const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
+    const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = POLY == 1 ? mod_signed_dev(val[r], cst) : small_mod(val[r], q);
+#pragma unroll
+    for (int s = 0; s < LOGR; ++s) {
+      const int m = 1 << s, tr = R >> (s + 1);
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        const uint64_t W = w[m + i], Wp = wp[m + i];
+#pragma unroll
+        for (int jj = 0; jj < tr; ++jj) {
+          const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+          ct_bfly(x[r0], x[r1], W, Wp, q, q3, q4);
+        }
+      }
+    }
+    uint64_t* __restrict__ o = out + (k * 3 + POLY) * LN + ((uint64_t)t << logN) + c;
+#pragma unroll
+    for (int r = 0; r < R; ++r) o[(uint64_t)r * BLK] = x[r];
+  }
 }
 
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
-  return K * (uint64_t)p.batch * sizeof(double2) + K * 3ull * p.L * p.N * sizeof(uint64_t);
+  // FFT buffer | pbuf [K][3][L][N] | me0 [K][N] int64 | ve [K][N] int16
+  return K * (uint64_t)p.batch * sizeof(double2) + K * 3ull * p.L * p.N * sizeof(uint64_t) +
+         K * (uint64_t)p.N * (sizeof(int64_t) + sizeof(int16_t)) + 64;
 }
 
 void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
@@ -891,47 +1007,50 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        blkLog, 1, dt.fft_inv);
   }
   SHELFI_HIP(hipGetLastError());
-  // 2. scale/round/reduce + sample
+  // 2. encode (scale/round) + sampling -> compact record
   Key8 k8;
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
+  int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
+  int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
   const uint64_t threads = K * (p.N / 8);
-  hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
-                     fbuf, K, p.logN, logS, p.L, p.delta, dt.tc, dt.cdt, dt.cdt_len, k8, g0, pbuf,
-                     flag);
+  hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, fbuf,
+                     K, p.logN, logS, p.delta, dt.cdt, dt.cdt_len, k8, g0, me0, ve, flag);
   SHELFI_HIP(hipGetLastError());
-  // 3. NTT of the 3 L polynomials per ciphertext
-  launch_ntt(pbuf, K * 3 * p.L, p.L, p.logN, false, dt, s);
-  // 4. combine with the public key
-  const uint64_t pairs = K * (uint64_t)p.L * p.N / 2;
-  hipLaunchKernelGGL(enc_combine_kernel, dim3((uint32_t)((pairs + 255) / 256)), dim3(256), 0, s,
-                     pbuf, K, p.logN, p.L, dk.pk, dk.pk_sh, dt.tc, ct);
+  // 3. NTT of v, m + e0, e1 per tower (columns pass expands the record), then the
+  // blocks pass fused with the public-key combine writes the ciphertexts
+  const uint32_t nblkLog = p.logN < (uint32_t)kNttBlockLog ? p.logN : (uint32_t)kNttBlockLog;
+  const int nlogR = (int)(p.logN - nblkLog);
+  if (nlogR > 0) {
+    const uint64_t nb = K * ((p.N >> nlogR) / 256);
+#define COLS_ENC(LR)                                                                          \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 0>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                       \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 1>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                       \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 2>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);
+    switch (nlogR) {
+      case 1: COLS_ENC(1) break;
+      case 2: COLS_ENC(2) break;
+      case 3: COLS_ENC(3) break;
+      case 4: COLS_ENC(4) break;
+      case 5: COLS_ENC(5) break;
+      case 6: COLS_ENC(6) break;
+      default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};
+    }
+#undef COLS_ENC
+    SHELFI_HIP(hipGetLastError());
+  }
+  const uint64_t nbb = K * p.L << nlogR;
+  if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
+  hipLaunchKernelGGL(ntt_fwd_blocks_enc, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
+                     pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
+                     dk.pk_sh, ct, nlogR > 0 ? (const int64_t*)nullptr : me0,
+                     nlogR > 0 ? (const int16_t*)nullptr : ve);
   SHELFI_HIP(hipGetLastError());
 }
 
 // -------------------------------------------------------------- decrypt ----
-__global__ __launch_bounds__(256) void dec_combine_kernel(const uint64_t* __restrict__ ct,
-                                                          uint64_t K, uint32_t logN, uint32_t L,
-                                                          const uint64_t* __restrict__ sk,
-                                                          const uint64_t* __restrict__ sksh,
-                                                          const TowerConst* __restrict__ tcs,
-                                                          uint64_t* __restrict__ dbuf) {
-  const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;  // over [K][L][N]
-  const uint64_t LN = (uint64_t)L << logN;
-  const uint64_t k = e / LN;
-  if (k >= K) return;
-  const uint64_t rem = e - k * LN;
-  const uint32_t t = (uint32_t)(rem >> logN);
-  const uint64_t q = tcs[t].q;
-  const ulonglong2 c0 = *reinterpret_cast<const ulonglong2*>(ct + (k * 2 + 0) * LN + rem);
-  const ulonglong2 c1 = *reinterpret_cast<const ulonglong2*>(ct + (k * 2 + 1) * LN + rem);
-  const ulonglong2 s = *reinterpret_cast<const ulonglong2*>(sk + rem);
-  const ulonglong2 ss = *reinterpret_cast<const ulonglong2*>(sksh + rem);
-  ulonglong2 d;
-  d.x = addmod(c0.x, shoup_mul(c1.x, s.x, ss.x, q), q);
-  d.y = addmod(c0.y, shoup_mul(c1.y, s.y, ss.y, q), q);
-  *reinterpret_cast<ulonglong2*>(dbuf + e) = d;
-}
-
 // Exact centered CRT: y_t = b_t (Q/q_t)^-1 mod q_t; X = sum y_t (Q/q_t) - k Q with
 // k = round(sum y_t / q_t) (exact while |X| << Q/2), evaluated mod 2^128 and read
 // as a signed 128-bit integer; then (double)X * (1/scale) (PALISADE Decode:
@@ -995,11 +1114,21 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
-  const uint64_t pairs = K * (uint64_t)p.L * p.N / 2;
-  hipLaunchKernelGGL(dec_combine_kernel, dim3((uint32_t)((pairs + 255) / 256)), dim3(256), 0, s,
-                     ct, K, p.logN, p.L, dk.sk, dk.sk_sh, dt.tc, dbuf);
-  SHELFI_HIP(hipGetLastError());
-  launch_ntt(dbuf, K * p.L, p.L, p.logN, true, dt, s);
+  // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts)
+  {
+    const uint32_t blkLog = p.logN < (uint32_t)kNttBlockLog ? p.logN : (uint32_t)kNttBlockLog;
+    const int logR = (int)(p.logN - blkLog);
+    const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
+    if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
+    hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
+                       s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
+                       logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh);
+    if (logR > 0) {
+      NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, dbuf, p.L, p.logN,
+                   dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
+    }
+    SHELFI_HIP(hipGetLastError());
+  }
   const uint64_t slots = K * (uint64_t)p.batch;
   hipLaunchKernelGGL(crt_decode_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, s,
                      dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
