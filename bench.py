@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--api-cts", type=int, default=64,
+                    help="ciphertexts per learner for the bytes-API (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
                     help="PMC-derived HBM bytes per wavg launch (from tools/pmc_traffic.py)")
@@ -218,6 +220,29 @@ def main():
     assert torch.isfinite(dec).all().item()
     del dec
 
+    # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`
+    api = None
+    if args.api_cts > 0 and rank == 0:
+        Ka = min(K, args.api_cts)
+        if args.layout == "arena":
+            src = [out[:Ka].clone() for _ in range(Cl)]  # any valid ciphertexts of this key
+        else:
+            src = [c[:Ka] for c in cts]
+        blobs = [m.blob_pack(ck, s.cpu().numpy().view(np.uint64)) for s in src]
+        del src
+        ck.computeWeightedAverage(blobs, weights)  # warm (allocates staging)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            res_blob = ck.computeWeightedAverage(blobs, weights)
+        dt_api = (time.perf_counter() - t0) / reps
+        api = {"value": round(Cl * Ka / dt_api, 1), "unit": "client-ciphertexts/s",
+               "sample": "%d learners x %d cts, bytes in -> bytes out through "
+                         "SHELFI_FHE.CKKS.computeWeightedAverage (H2D + wavg + D2H)" % (Cl, Ka),
+               "ms_per_call": round(dt_api * 1e3, 2),
+               "input_GB_per_s": round(Cl * Ka * 2 * L * N * 8 / dt_api / 1e9, 2)}
+        del blobs, res_blob
+
     # roofline of the dominant kernel: algorithmic bytes = (C + 1) * K * 2 * L * N * 8
     bytes_per_launch = (Cl + 1) * K * 2 * L * N * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
@@ -252,6 +277,8 @@ def main():
         "encode_encrypt_ms_per_ct": round(1e3 * sorted(enc_times)[len(enc_times) // 2] / K, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),
     }
+    if api:
+        res["api_bytes_path"] = api
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, L, q, delta, Cl, args.cpu_seconds)
     if rank == 0:

@@ -27,6 +27,24 @@ __version__ = "0.1.0"
 __all__ = ["Scheme", "CKKS", "ShelfiError", "__version__"]
 
 
+_PyBytes_FromStringAndSize = C.pythonapi.PyBytes_FromStringAndSize
+_PyBytes_FromStringAndSize.restype = C.py_object
+_PyBytes_FromStringAndSize.argtypes = [C.c_void_p, C.c_ssize_t]
+_PyBytes_AsString = C.pythonapi.PyBytes_AsString
+_PyBytes_AsString.restype = C.c_void_p
+_PyBytes_AsString.argtypes = [C.py_object]
+
+
+def _new_bytes(n: int) -> bytes:
+    """An uninitialised bytes object of length n, filled in place by the library before
+    it is ever exposed (CPython's PyBytes_FromStringAndSize(NULL, n) contract)."""
+    return _PyBytes_FromStringAndSize(None, n)
+
+
+def _bytes_ptr(b: bytes) -> int:
+    return _PyBytes_AsString(b)
+
+
 class Scheme:
     """binding.cpp:16 ``py::class_<Scheme>`` — opaque base of the scheme plugins
     (include/scheme.h:15-32)."""
@@ -180,12 +198,16 @@ class CKKS(Scheme):
         for i, b in enumerate(blobs):
             arr[i] = C.cast(C.c_char_p(b), _lib.u8p)
             lens[i] = len(b)
-        out = _lib.u8p()
         n_out = C.c_size_t()
-        check(self._lib.shelfi_weighted_average(self._ctx, arr, lens, w.ctypes.data_as(_lib.f32p),
-                                                C_, C.byref(out), C.byref(n_out)),
+        wp = w.ctypes.data_as(_lib.f32p)
+        check(self._lib.shelfi_weighted_average_into(self._ctx, arr, lens, wp, C_, None, 0,
+                                                     C.byref(n_out)), "computeWeightedAverage")
+        # the result is written straight into a new bytes object's buffer (no extra copy)
+        res = _new_bytes(n_out.value)
+        check(self._lib.shelfi_weighted_average_into(self._ctx, arr, lens, wp, C_, _bytes_ptr(res),
+                                                     n_out.value, C.byref(n_out)),
               "computeWeightedAverage")
-        return self._take(out, n_out.value)
+        return res
 
     def decrypt(self, learner_data, data_dimensions: int) -> np.ndarray:
         """ckks.cpp:170-213 -> float64[data_dimensions]."""

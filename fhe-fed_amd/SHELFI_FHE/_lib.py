@@ -66,6 +66,8 @@ SIGNATURES = {
     "shelfi_encrypt": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "shelfi_weighted_average": (C.c_int, [C.c_void_p, C.POINTER(u8p), C.POINTER(C.c_size_t), f32p,
                                           C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_weighted_average_into": (C.c_int, [C.c_void_p, C.POINTER(u8p), C.POINTER(C.c_size_t), f32p,
+                                               C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "shelfi_decrypt": (C.c_int, [C.c_void_p, u8p, C.c_size_t, C.c_size_t, f64p]),
     "shelfi_blob_info": (C.c_int, [u8p, C.c_size_t, u64p, C.POINTER(C.c_uint32), f64p, u64p]),
     "shelfi_blob_pack": (C.c_int, [C.c_void_p, u64p, C.c_uint64, C.c_uint32, C.c_double,

@@ -461,6 +461,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
     uint64_t q[kMaxTowers], psi[kMaxTowers];
     generate_chain(N, num_towers, scale_bits, first_mod_bits, q, psi);
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     SHELFI_HIP(hipMalloc(&ctx->dev_flag, 16));
     set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
   });
@@ -479,12 +480,14 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     free_keys(ctx);
     free_tables(ctx);
     dfree(ctx->scratch);
     dfree(ctx->io);
     dfree_t(ctx->dev_flag);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (prev >= 0) (void)hipSetDevice(prev);
   }
   delete ctx;
@@ -724,6 +727,90 @@ int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, si
   });
 }
 
+// Validates the learners' blobs (same params, key, K, depth, scale) and returns the
+// header of the result (depth + 1, scale * Delta: EvalMult by a constant, no rescale).
+static BlobHeader wavg_check(const shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                             size_t C) {
+  if (C == 0) throw Error{SHELFI_ERR_ARG, "computeWeightedAverage: no learners"};
+  BlobHeader h0 = parse_blob(blobs[0], lens[0], ctx);
+  for (size_t c = 1; c < C; ++c) {
+    BlobHeader h = parse_blob(blobs[c], lens[c], ctx);
+    if (h.K != h0.K)
+      throw Error{SHELFI_ERR_FORMAT, "learners hold different numbers of ciphertexts"};
+    if (h.key_id != h0.key_id)
+      throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts were encrypted under different keys"};
+    if (h.depth != h0.depth || h.scale != h0.scale)
+      throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts have different depth/scale"};
+  }
+  BlobHeader ho = h0;
+  ho.depth = h0.depth + 1;
+  ho.scale = h0.scale * ctx->p.delta;
+  return ho;
+}
+
+// Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
+// chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
+// (stream B), with two device buffer sets.  Writes the payload of the result.
+static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, const float* weights,
+                                size_t C, uint64_t K, uint8_t* out_payload) {
+  const Params& p = ctx->p;
+  const size_t ct_bytes = 2ull * p.L * p.N * 8;
+  // chunk: ~32 MiB of input per learner-group buffer, at least 1 ciphertext
+  const size_t group = std::min<size_t>(C, kWavgMaxLearners);
+  uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / (ct_bytes * group));
+  kc = std::min<uint64_t>(kc, K);
+  const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
+  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (in_chunk + out_chunk));
+  uint8_t* inb[2] = {io, io + in_chunk};
+  uint8_t* outb[2] = {io + 2 * in_chunk, io + 2 * in_chunk + out_chunk};
+  hipStream_t sA = ctx->stream, sB = ctx->stream2;
+  hipEvent_t copied[2], done[2];
+  for (int i = 0; i < 2; ++i) {
+    SHELFI_HIP(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming));
+    SHELFI_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  }
+  struct Ev {
+    hipEvent_t* e;
+    ~Ev() {
+      for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
+    }
+  };
+  hipEvent_t all[4] = {copied[0], copied[1], done[0], done[1]};
+  Ev guard{all};
+  const uint64_t nchunks = (K + kc - 1) / kc;
+  for (uint64_t ci = 0; ci < nchunks; ++ci) {
+    const int b = (int)(ci & 1);
+    const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+    for (size_t c0 = 0; c0 < C; c0 += group) {
+      const size_t gc = std::min(group, C - c0);
+      if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(sA, done[b], 0));  // buffer free
+      for (size_t c = 0; c < gc; ++c)
+        SHELFI_HIP(hipMemcpyAsync(inb[b] + c * kn * ct_bytes,
+                                  blobs[c0 + c] + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes,
+                                  hipMemcpyHostToDevice, sA));
+      SHELFI_HIP(hipEventRecord(copied[b], sA));
+      SHELFI_HIP(hipStreamWaitEvent(sB, copied[b], 0));
+      WavgArgs a;
+      std::memset(&a, 0, sizeof(a));
+      for (size_t c = 0; c < gc; ++c) a.ptrs[c] = (const uint64_t*)(inb[b] + c * kn * ct_bytes);
+      fill_weights(a, p, weights + c0, gc);
+      a.out = (uint64_t*)outb[b];
+      a.rows = kn * 2 * p.L;
+      a.C = (uint32_t)gc;
+      a.L = p.L;
+      a.logN = p.logN;
+      a.accumulate = c0 ? 1 : 0;
+      launch_wavg(a, ctx->dt.tc, sB);
+      if (c0 + gc >= C)
+        SHELFI_HIP(hipMemcpyAsync(out_payload + k0 * ct_bytes, outb[b], kn * ct_bytes,
+                                  hipMemcpyDeviceToHost, sB));
+      SHELFI_HIP(hipEventRecord(done[b], sB));
+    }
+  }
+  SHELFI_HIP(hipStreamSynchronize(sB));
+  SHELFI_HIP(hipStreamSynchronize(sA));
+}
+
 int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
                             const float* weights, size_t C, uint8_t** out, size_t* out_len) {
   if (!ctx || !out || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
@@ -732,62 +819,36 @@ int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const 
   *out_len = 0;
   return guarded([&] {
     DeviceGuard g(ctx->device);
-    const Params& p = ctx->p;
-    if (C == 0) throw Error{SHELFI_ERR_ARG, "computeWeightedAverage: no learners"};
-    BlobHeader h0 = parse_blob(blobs[0], lens[0], ctx);
-    for (size_t c = 1; c < C; ++c) {
-      BlobHeader h = parse_blob(blobs[c], lens[c], ctx);
-      if (h.K != h0.K)
-        throw Error{SHELFI_ERR_FORMAT, "learners hold different numbers of ciphertexts"};
-      if (h.key_id != h0.key_id)
-        throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts were encrypted under different keys"};
-      if (h.depth != h0.depth || h.scale != h0.scale)
-        throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts have different depth/scale"};
-    }
-    const uint64_t K = h0.K;
-    const size_t ct_bytes = 2ull * p.L * p.N * 8, payload = K * ct_bytes;
-    BlobHeader ho = h0;
-    ho.depth = h0.depth + 1;     // EvalMult by a constant: depth + 1, no rescale
-    ho.scale = h0.scale * p.delta;  // scalingFactor * scFactor(level 0)
-    const size_t total = sizeof(BlobHeader) + payload;
+    const BlobHeader ho = wavg_check(ctx, blobs, lens, C);
+    const size_t total = sizeof(BlobHeader) + ho.K * 2ull * ctx->p.L * ctx->p.N * 8;
     uint8_t* blob = (uint8_t*)std::malloc(total);
     if (!blob) throw std::bad_alloc();
     std::memcpy(blob, &ho, sizeof(ho));
     try {
-      if (K) {
-        // learners in groups of 16 (one launch each, accumulating)
-        const size_t group = std::min<size_t>(C, kWavgMaxLearners);
-        uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, (group + 1) * payload);
-        uint64_t* dout = (uint64_t*)(io + group * payload);
-        for (size_t c0 = 0; c0 < C; c0 += group) {
-          const size_t gc = std::min(group, C - c0);
-          WavgArgs a;
-          std::memset(&a, 0, sizeof(a));
-          for (size_t c = 0; c < gc; ++c) {
-            SHELFI_HIP(hipMemcpyAsync(io + c * payload, blobs[c0 + c] + sizeof(BlobHeader),
-                                      payload, hipMemcpyHostToDevice, ctx->stream));
-            a.ptrs[c] = (const uint64_t*)(io + c * payload);
-          }
-          fill_weights(a, p, weights + c0, gc);
-          a.out = dout;
-          a.rows = K * 2 * p.L;
-          a.C = (uint32_t)gc;
-          a.L = p.L;
-          a.logN = p.logN;
-          a.accumulate = c0 ? 1 : 0;
-          launch_wavg(a, ctx->dt.tc, ctx->stream);
-          SHELFI_HIP(hipStreamSynchronize(ctx->stream));
-        }
-        SHELFI_HIP(hipMemcpyAsync(blob + sizeof(BlobHeader), dout, payload, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-        SHELFI_HIP(hipStreamSynchronize(ctx->stream));
-      }
+      if (ho.K) wavg_bytes_pipeline(ctx, blobs, weights, C, ho.K, blob + sizeof(BlobHeader));
     } catch (...) {
       std::free(blob);
       throw;
     }
     *out = blob;
     *out_len = total;
+  });
+}
+
+int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                                 const float* weights, size_t C, uint8_t* out, size_t out_cap,
+                                 size_t* out_len) {
+  if (!ctx || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    const BlobHeader ho = wavg_check(ctx, blobs, lens, C);
+    const size_t total = sizeof(BlobHeader) + ho.K * 2ull * ctx->p.L * ctx->p.N * 8;
+    *out_len = total;
+    if (!out) return;  // size query
+    if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
+    std::memcpy(out, &ho, sizeof(ho));
+    if (ho.K) wavg_bytes_pipeline(ctx, blobs, weights, C, ho.K, out + sizeof(BlobHeader));
   });
 }
 

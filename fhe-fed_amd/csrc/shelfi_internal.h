@@ -93,7 +93,8 @@ struct DeviceKeys {
 struct shelfi_ctx {
   shelfi::Params p;
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // copy / default work stream
+  hipStream_t stream2 = nullptr;  // compute stream of the pipelined bytes API
   shelfi::DeviceTables dt;
   shelfi::DeviceKeys dk;
   std::vector<uint64_t> pk_host, sk_host;

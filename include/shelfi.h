@@ -99,6 +99,11 @@ int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, si
 int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
                             const float* weights, size_t num_learners, uint8_t** out,
                             size_t* out_len);
+/* Same, writing into a caller-owned buffer (out = NULL: only *out_len = result size).
+ * Copies, aggregation and the copy-out are pipelined over ciphertext chunks. */
+int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                                 const float* weights, size_t num_learners, uint8_t* out,
+                                 size_t out_cap, size_t* out_len);
 /* ckks.cpp:170-213 decrypt: blob -> n doubles (caller-owned out[n]). */
 int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out);
 
