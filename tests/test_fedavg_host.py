@@ -1,0 +1,52 @@
+"""CPU tests of the FedAvg harness host logic (SHELFI_FHE.fedavg): model shapes,
+selection rules of benchmark_selection*.py / masking.py, flatten/unflatten."""
+import numpy as np
+import pytest
+
+from SHELFI_FHE import fedavg as F
+
+
+def test_model_param_counts():
+    assert sum(int(np.prod(s)) for s in F.resnet_shapes(18).values()) == 11_689_512
+    assert sum(int(np.prod(s)) for s in F.resnet_shapes(50).values()) == 25_557_032
+    assert sum(int(np.prod(s)) for s in F.lenet5_shapes().values()) == 61_706
+
+
+def test_layer_index_rule():
+    # benchmark_selection.py:152: re.sub("[^0-9]", "", key)
+    assert F.layer_index("layer1.0.conv1.weight") == 101
+    assert F.layer_index("fc.weight") is None
+    assert F.layer_index("conv2.bias") == 2
+
+
+def test_selection_modes():
+    s = F.Selection("layers", layers=[2])
+    assert s.encrypted_index("conv2.weight", 10) == slice(0, 10)
+    assert s.encrypted_index("conv1.weight", 10) is None
+    r = F.Selection("rate", rate=0.1)
+    assert r.encrypted_index("x", 1000) == slice(0, 100)  # round(len * sel_rate)
+    assert r.encrypted_index("x", 4) is None
+    m = F.Selection("mask", masks={"a": np.array([True, False, True])})
+    assert m.encrypted_index("a", 3).tolist() == [True, False, True]
+    assert m.encrypted_index("b", 3) is None
+
+
+def test_top_k_mask():
+    sens = np.array([0.1, 5.0, 0.3, 4.0, 0.2])
+    assert F.top_k_mask(sens, 0.4).tolist() == [False, True, False, True, False]
+
+
+def test_flatten_roundtrip():
+    torch = pytest.importorskip("torch")
+    st = {"w": torch.randn(3, 4), "b": torch.randn(4)}
+    flat = F.flatten_state(st)
+    assert flat["w"].dtype == np.float64 and flat["w"].shape == (12,)
+    back = F.unflatten_state(flat, F.state_shapes(st), like=st)
+    assert torch.equal(back["w"], st["w"]) and back["w"].dtype == torch.float32
+
+
+def test_plain_fedavg():
+    sts = F.synthetic_states(F.lenet5_shapes(), 3, seed=1)
+    w = [0.2, 0.3, 0.5]
+    got = F.plain_fedavg(sts, w, "fc1.weight")
+    assert np.allclose(got, sum(wi * s["fc1.weight"] for wi, s in zip(w, sts)))
