@@ -174,11 +174,13 @@ class CKKS(Scheme):
     def encrypt(self, data_array) -> bytes:
         """ckks.cpp:61-104 (py::array_t<double> forcecast: float32 is widened)."""
         x = np.ascontiguousarray(np.asarray(data_array, dtype=np.float64).reshape(-1))
-        out = _lib.u8p()
+        xp = x.ctypes.data_as(_lib.f64p)
         n_out = C.c_size_t()
-        check(self._lib.shelfi_encrypt(self._ctx, x.ctypes.data_as(_lib.f64p), x.size,
-                                       C.byref(out), C.byref(n_out)), "encrypt")
-        return self._take(out, n_out.value)
+        check(self._lib.shelfi_encrypt_into(self._ctx, xp, x.size, None, 0, C.byref(n_out)), "encrypt")
+        res = _new_bytes(n_out.value)
+        check(self._lib.shelfi_encrypt_into(self._ctx, xp, x.size, _bytes_ptr(res), n_out.value,
+                                            C.byref(n_out)), "encrypt")
+        return res
 
     def computeWeightedAverage(self, learner_data, scaling_factors) -> bytes:
         """ckks.cpp:264-320.  Length mismatch prints and returns b"" (:265-268);

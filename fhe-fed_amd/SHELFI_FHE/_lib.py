@@ -64,6 +64,8 @@ SIGNATURES = {
     "shelfi_set_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_get_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_encrypt": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_encrypt_into": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]),
     "shelfi_weighted_average": (C.c_int, [C.c_void_p, C.POINTER(u8p), C.POINTER(C.c_size_t), f32p,
                                           C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "shelfi_weighted_average_into": (C.c_int, [C.c_void_p, C.POINTER(u8p), C.POINTER(C.c_size_t), f32p,

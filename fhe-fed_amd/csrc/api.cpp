@@ -462,6 +462,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
     generate_chain(N, num_towers, scale_bits, first_mod_bits, q, psi);
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
     SHELFI_HIP(hipMalloc(&ctx->dev_flag, 16));
     set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
   });
@@ -481,6 +482,7 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
     free_keys(ctx);
     free_tables(ctx);
     dfree(ctx->scratch);
@@ -488,6 +490,7 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     dfree_t(ctx->dev_flag);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
     if (prev >= 0) (void)hipSetDevice(prev);
   }
   delete ctx;
@@ -657,74 +660,137 @@ int shelfi_load(shelfi_ctx* ctx, const char* cryptodir) {
 }
 
 // ------------------------------------------------------------- bytes API ----
-int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, size_t* out_len) {
-  if (!ctx || !out || !out_len || (n && !x)) return SHELFI_ERR_ARG;
+static BlobHeader make_header(const shelfi_ctx* ctx, uint64_t K, uint32_t depth, double scale) {
+  const Params& p = ctx->p;
+  BlobHeader h;
+  std::memset(&h, 0, sizeof(h));
+  std::memcpy(h.magic, "SHCT", 4);
+  h.version = 1;
+  h.header_bytes = 64;
+  h.logN = p.logN;
+  h.L = p.L;
+  h.K = K;
+  h.depth = depth;
+  h.level = 0;
+  h.scale = scale;
+  h.params_id = ctx->params_id;
+  h.key_id = ctx->key_id;
+  h.batch = p.batch;
+  h.encoding = 4;
+  return h;
+}
+
+// Three-stage pipeline over chunks: H2D on stream A, kernels on stream B (scratch is
+// reused chunk after chunk on B), D2H on stream C, two staging buffer sets.
+struct Pipe {
+  hipStream_t a, b, c;
+  hipEvent_t in_ready[2], computed[2], out_free[2];
+  explicit Pipe(shelfi_ctx* ctx) : a(ctx->stream), b(ctx->stream2), c(ctx->stream3) {
+    for (int i = 0; i < 2; ++i) {
+      in_ready[i] = computed[i] = out_free[i] = nullptr;
+    }
+    for (int i = 0; i < 2; ++i) {
+      SHELFI_HIP(hipEventCreateWithFlags(&in_ready[i], hipEventDisableTiming));
+      SHELFI_HIP(hipEventCreateWithFlags(&computed[i], hipEventDisableTiming));
+      SHELFI_HIP(hipEventCreateWithFlags(&out_free[i], hipEventDisableTiming));
+    }
+  }
+  ~Pipe() {
+    for (int i = 0; i < 2; ++i) {
+      if (in_ready[i]) (void)hipEventDestroy(in_ready[i]);
+      if (computed[i]) (void)hipEventDestroy(computed[i]);
+      if (out_free[i]) (void)hipEventDestroy(out_free[i]);
+    }
+  }
+  void sync() {
+    SHELFI_HIP(hipStreamSynchronize(c));
+    SHELFI_HIP(hipStreamSynchronize(b));
+    SHELFI_HIP(hipStreamSynchronize(a));
+  }
+};
+
+// encode + encrypt n doubles (host) -> K ciphertext payloads written to out_payload.
+static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, uint64_t K,
+                                   uint8_t* out_payload) {
+  const Params& p = ctx->p;
+  const size_t ct_bytes = 2ull * p.L * p.N * 8;
+  uint32_t key[8];
+  uint64_t g0;
+  draw_key(ctx, K, key, &g0);
+  uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
+  kc = std::min<uint64_t>(kc, K);
+  const size_t xin = kc * p.batch * 8, cto = kc * ct_bytes;
+  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (xin + cto));
+  uint8_t* xb[2] = {io, io + xin};
+  uint8_t* cb[2] = {io + 2 * xin, io + 2 * xin + cto};
+  void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc));
+  Pipe pp(ctx);
+  SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, pp.b));
+  const uint64_t nchunks = (K + kc - 1) / kc;
+  for (uint64_t ci = 0; ci < nchunks; ++ci) {
+    const int b = (int)(ci & 1);
+    const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+    const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kn * p.batch);
+    if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // x buffer consumed
+    SHELFI_HIP(hipMemcpyAsync(xb[b], x + xs, xn * 8, hipMemcpyHostToDevice, pp.a));
+    SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
+    SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+    if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));  // ct buffer drained
+    launch_encrypt(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
+                   g0 + k0, ctx->dev_flag, pp.b);
+    SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+    SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
+    SHELFI_HIP(hipMemcpyAsync(out_payload + k0 * ct_bytes, cb[b], kn * ct_bytes,
+                              hipMemcpyDeviceToHost, pp.c));
+    SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+  }
+  pp.sync();
+  std::memset(key, 0, sizeof(key));
+  uint32_t flag = 0;
+  SHELFI_HIP(hipMemcpy(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost));
+  if (flag)
+    throw Error{SHELFI_ERR_RANGE,
+                "encrypt: non-finite input or |value * scale| > 2^61 (PALISADE approxFactor range)"};
+}
+
+int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out, size_t out_cap,
+                        size_t* out_len) {
+  if (!ctx || !out_len || (n && !x)) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
-  *out = nullptr;
-  *out_len = 0;
   return guarded([&] {
     require_keys(ctx);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
-    for (size_t i = 0; i < n; ++i)
-      if (!std::isfinite(x[i])) throw Error{SHELFI_ERR_RANGE, "encrypt: input contains NaN/inf"};
-    // ckks.cpp:65 cipherSize = ceil(size / batchSize)
-    const uint64_t K = (n + p.batch - 1) / p.batch;
-    const size_t ct_bytes = 2ull * p.L * p.N * 8;
-    const size_t total = sizeof(BlobHeader) + K * ct_bytes;
-    uint8_t* blob = (uint8_t*)std::malloc(total);
-    if (!blob) throw std::bad_alloc();
-    BlobHeader h;
-    std::memset(&h, 0, sizeof(h));
-    std::memcpy(h.magic, "SHCT", 4);
-    h.version = 1;
-    h.header_bytes = 64;
-    h.logN = p.logN;
-    h.L = p.L;
-    h.K = K;
-    h.depth = 1;
-    h.level = 0;
-    h.scale = p.delta;
-    h.params_id = ctx->params_id;
-    h.key_id = ctx->key_id;
-    h.batch = p.batch;
-    h.encoding = 4;
-    std::memcpy(blob, &h, sizeof(h));
-    try {
-      if (K) {
-        uint32_t key[8];
-        uint64_t g0;
-        draw_key(ctx, K, key, &g0);
-        const uint64_t chunk = std::max<uint64_t>(1, (512ull << 20) / encrypt_scratch_bytes(p, 1));
-        const uint64_t kc_max = std::min<uint64_t>(chunk, K);
-        const size_t xin = kc_max * p.batch * 8, cto = kc_max * ct_bytes;
-        uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, xin + cto);
-        void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
-        SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, ctx->stream));
-        for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
-          const uint64_t kc = std::min(kc_max, K - k0);
-          const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kc * p.batch);
-          SHELFI_HIP(hipMemcpyAsync(io, x + xs, xn * 8, hipMemcpyHostToDevice, ctx->stream));
-          launch_encrypt(p, ctx->dt, ctx->dk, (const double*)io, xn, kc, (uint64_t*)(io + xin),
-                         scratch, key, g0 + k0, ctx->dev_flag, ctx->stream);
-          SHELFI_HIP(hipMemcpyAsync(blob + sizeof(h) + k0 * ct_bytes, io + xin, kc * ct_bytes,
-                                    hipMemcpyDeviceToHost, ctx->stream));
-          SHELFI_HIP(hipStreamSynchronize(ctx->stream));
-        }
-        std::memset(key, 0, sizeof(key));
-        uint32_t flag = 0;
-        SHELFI_HIP(hipMemcpy(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost));
-        if (flag)
-          throw Error{SHELFI_ERR_RANGE,
-                      "encrypt: |value * scale| exceeds 2^61 (PALISADE approxFactor range)"};
-      }
-    } catch (...) {
-      std::free(blob);
-      throw;
-    }
-    *out = blob;
+    const uint64_t K = (n + p.batch - 1) / p.batch;  // ckks.cpp:65
+    const size_t total = sizeof(BlobHeader) + K * 2ull * p.L * p.N * 8;
     *out_len = total;
+    if (!out) return;
+    if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
+    const BlobHeader h = make_header(ctx, K, 1, p.delta);
+    std::memcpy(out, &h, sizeof(h));
+    if (K) encrypt_bytes_pipeline(ctx, x, n, K, out + sizeof(BlobHeader));
   });
+}
+
+int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, size_t* out_len) {
+  if (!ctx || !out || !out_len || (n && !x)) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  size_t total = 0;
+  int rc = shelfi_encrypt_into(ctx, x, n, nullptr, 0, &total);
+  if (rc) return rc;
+  uint8_t* blob = (uint8_t*)std::malloc(total ? total : 1);
+  if (!blob) {
+    set_error("host out of memory");
+    return SHELFI_ERR_DEVICE;
+  }
+  rc = shelfi_encrypt_into(ctx, x, n, blob, total, &total);
+  if (rc) {
+    std::free(blob);
+    return rc;
+  }
+  *out = blob;
+  *out_len = total;
+  return SHELFI_OK;
 }
 
 // Validates the learners' blobs (same params, key, K, depth, scale) and returns the
@@ -868,21 +934,33 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
     const uint64_t K = (n + p.batch - 1) / p.batch;
     const size_t ct_bytes = 2ull * p.L * p.N * 8;
-    const uint64_t chunk = std::max<uint64_t>(1, (512ull << 20) / decrypt_scratch_bytes(p, 1));
-    const uint64_t kc_max = std::min<uint64_t>(chunk, K);
-    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, kc_max * ct_bytes + kc_max * p.batch * 8);
-    double* dout = (double*)(io + kc_max * ct_bytes);
-    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
-    for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
-      const uint64_t kc = std::min(kc_max, K - k0);
-      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
-      SHELFI_HIP(hipMemcpyAsync(io, blob + sizeof(BlobHeader) + k0 * ct_bytes, kc * ct_bytes,
-                                hipMemcpyHostToDevice, ctx->stream));
-      launch_decrypt(p, ctx->dt, ctx->dk, (const uint64_t*)io, kc, h.scale, on, dout, scratch,
-                     ctx->stream);
-      SHELFI_HIP(hipMemcpyAsync(out + o0, dout, on * 8, hipMemcpyDeviceToHost, ctx->stream));
-      SHELFI_HIP(hipStreamSynchronize(ctx->stream));
+    uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
+    kc = std::min<uint64_t>(kc, K);
+    const size_t cin = kc * ct_bytes, dout = kc * p.batch * 8;
+    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout));
+    uint8_t* cb[2] = {io, io + cin};
+    uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc));
+    Pipe pp(ctx);
+    const uint64_t nchunks = (K + kc - 1) / kc;
+    for (uint64_t ci = 0; ci < nchunks; ++ci) {
+      const int b = (int)(ci & 1);
+      const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
+      if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
+      SHELFI_HIP(hipMemcpyAsync(cb[b], blob + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes,
+                                hipMemcpyHostToDevice, pp.a));
+      SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
+      SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+      if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
+      launch_decrypt(p, ctx->dt, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
+                     scratch, pp.b);
+      SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+      SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
+      SHELFI_HIP(hipMemcpyAsync(out + o0, ob[b], on * 8, hipMemcpyDeviceToHost, pp.c));
+      SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
     }
+    pp.sync();
   });
 }
 
@@ -905,20 +983,7 @@ int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t K
   return guarded([&] {
     const Params& p = ctx->p;
     const size_t payload = K * 2ull * p.L * p.N * 8;
-    BlobHeader h;
-    std::memset(&h, 0, sizeof(h));
-    std::memcpy(h.magic, "SHCT", 4);
-    h.version = 1;
-    h.header_bytes = 64;
-    h.logN = p.logN;
-    h.L = p.L;
-    h.K = K;
-    h.depth = depth;
-    h.scale = scale;
-    h.params_id = ctx->params_id;
-    h.key_id = ctx->key_id;
-    h.batch = p.batch;
-    h.encoding = 4;
+    const BlobHeader h = make_header(ctx, K, depth, scale);
     uint8_t* blob = (uint8_t*)std::malloc(sizeof(h) + payload);
     if (!blob) throw std::bad_alloc();
     std::memcpy(blob, &h, sizeof(h));

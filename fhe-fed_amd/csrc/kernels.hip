@@ -906,7 +906,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
     if ((jj & ((1u << gapLog) - 1)) == 0) {
       const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
       const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
-      if (fabs(val) > lim) atomicOr(flag, 1u);
+      if (!(fabs(val) <= lim)) atomicOr(flag, 1u);  // also catches NaN / inf
       m = round_half_away(val);
     }
     me0[(k << logN) + j] = m + gauss_sample(w[u], cdt, T);

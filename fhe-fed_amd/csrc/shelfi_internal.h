@@ -95,6 +95,7 @@ struct shelfi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;   // copy / default work stream
   hipStream_t stream2 = nullptr;  // compute stream of the pipelined bytes API
+  hipStream_t stream3 = nullptr;  // copy-out stream of the pipelined bytes API
   shelfi::DeviceTables dt;
   shelfi::DeviceKeys dk;
   std::vector<uint64_t> pk_host, sk_host;

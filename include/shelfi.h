@@ -95,6 +95,10 @@ int shelfi_get_keys(const shelfi_ctx* ctx, uint64_t* pk, uint64_t* sk);
 /* ---- bytes API (binding.cpp:26-31) ---------------------------------------- */
 /* ckks.cpp:61-104 encrypt: n doubles -> blob of ceil(n/batch) ciphertexts. */
 int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, size_t* out_len);
+/* Same into a caller-owned buffer (out = NULL: only *out_len); H2D, kernels and D2H
+ * are pipelined over ciphertext chunks. */
+int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out, size_t out_cap,
+                        size_t* out_len);
 /* ckks.cpp:264-320 computeWeightedAverage: C blobs, float32 weights (ckks.cpp:287). */
 int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
                             const float* weights, size_t num_learners, uint8_t** out,

@@ -203,6 +203,28 @@ def test_encrypt_bitexact(cfg, n, request):
     assert np.abs(dec - x).max() < 1e-7
 
 
+def test_pipelined_bytes_api_multichunk(cfg2):
+    """encrypt/decrypt stream 64 MiB chunks of ciphertexts through two staging buffers
+    (H2D, kernels, D2H on three streams): 70 ciphertexts = 3 chunks at N=2^15, L=4,
+    residues and decode bit-exact vs the oracle, ragged last chunk."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    n = 69 * S + 123
+    seed = 4242
+    cfg2.set_seed(seed)
+    x = np.random.default_rng(3).uniform(-0.1, 0.1, n).astype(np.float32).astype(np.float64)
+    blob = cfg2.encrypt(x)
+    got = m.blob_residues(blob, N, len(q))
+    pk, sk = cfg2.get_keys()
+    ref = O.encrypt_vector(x, pk, q, psi, N, S, delta, seed=seed, g0=0)
+    assert got.shape[0] == 70 and np.array_equal(got, ref)
+    dec = cfg2.decrypt(blob, n)
+    assert np.array_equal(dec, O.decrypt_vector(ref, sk, q, psi, S, delta, n))
+    assert np.abs(dec - x).max() < 1e-8
+    # a decrypt of fewer values than the blob holds stops inside the second chunk
+    n2 = 40 * S + 7
+    assert np.array_equal(cfg2.decrypt(blob, n2), dec[:n2])
+
+
 @pytest.mark.parametrize("cfg", CFGS)
 def test_e2e_weighted_average(cfg, request):
     """pythonApi/ckks_example.py:8-111 flow (3 learners, weights [0.5, 0.2, 0.3]),
@@ -277,6 +299,9 @@ def test_api_behaviour(cfg1, cfg2, capsys):
     # out-of-range values are rejected rather than silently wrapped
     with pytest.raises(ValueError):
         cfg1.encrypt(np.array([1e9]))
+    for bad in (np.nan, np.inf, -np.inf):
+        with pytest.raises(ValueError):
+            cfg1.encrypt(np.array([0.5, bad]))
     # no keys
     ck = m.CKKS("ckks", 4096, 52, "/nonexistent/")
     ck.loadCryptoParams()
