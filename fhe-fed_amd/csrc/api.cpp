@@ -19,6 +19,7 @@
 #include <mutex>
 #include <new>
 
+#include "host_stage.h"
 #include "palisade_io.h"
 #include "shelfi_internal.h"
 
@@ -485,6 +486,8 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
     free_keys(ctx);
     free_tables(ctx);
+    delete ctx->stage;
+    ctx->stage = nullptr;
     dfree(ctx->scratch);
     dfree(ctx->io);
     dfree_t(ctx->dev_flag);
@@ -696,6 +699,9 @@ struct Pipe {
     }
   }
   ~Pipe() {
+    (void)hipStreamSynchronize(c);  // no-ops on success; on an error, nothing stays in flight
+    (void)hipStreamSynchronize(b);
+    (void)hipStreamSynchronize(a);
     for (int i = 0; i < 2; ++i) {
       if (in_ready[i]) (void)hipEventDestroy(in_ready[i]);
       if (computed[i]) (void)hipEventDestroy(computed[i]);
@@ -706,6 +712,27 @@ struct Pipe {
     SHELFI_HIP(hipStreamSynchronize(c));
     SHELFI_HIP(hipStreamSynchronize(b));
     SHELFI_HIP(hipStreamSynchronize(a));
+  }
+};
+
+// The ctx's pinned staging rings (8 x 8 MiB each way), created on first use.
+static Stager& stager(shelfi_ctx* ctx) {
+  if (!ctx->stage) ctx->stage = new Stager(8u << 20, 8, 8, default_copy_threads());
+  return *ctx->stage;
+}
+
+// Drops the staged outputs of a pipeline that threw (declared after its Pipe, so the
+// slots are abandoned before the streams are drained).
+struct StageRun {
+  Stager& s;
+  bool done = false;
+  explicit StageRun(Stager& st) : s(st) {}
+  void finish() {
+    s.finish();
+    done = true;
+  }
+  ~StageRun() {
+    if (!done) s.abort();
   }
 };
 
@@ -725,6 +752,7 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
   uint8_t* cb[2] = {io + 2 * xin, io + 2 * xin + cto};
   void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc));
   Pipe pp(ctx);
+  StageRun sr(stager(ctx));
   SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, pp.b));
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
@@ -732,7 +760,7 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
     const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kn * p.batch);
     if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // x buffer consumed
-    SHELFI_HIP(hipMemcpyAsync(xb[b], x + xs, xn * 8, hipMemcpyHostToDevice, pp.a));
+    sr.s.h2d(xb[b], x + xs, xn * 8, pp.a);
     SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
     SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
     if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));  // ct buffer drained
@@ -740,10 +768,11 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
                    g0 + k0, ctx->dev_flag, pp.b);
     SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
     SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
-    SHELFI_HIP(hipMemcpyAsync(out_payload + k0 * ct_bytes, cb[b], kn * ct_bytes,
-                              hipMemcpyDeviceToHost, pp.c));
+    sr.s.d2h(out_payload + k0 * ct_bytes, cb[b], kn * ct_bytes, pp.c);
     SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+    sr.s.poll();
   }
+  sr.finish();
   pp.sync();
   std::memset(key, 0, sizeof(key));
   uint32_t flag = 0;
@@ -767,6 +796,7 @@ int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out
     if (!out) return;
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     const BlobHeader h = make_header(ctx, K, 1, p.delta);
+    advise_huge(out, total);
     std::memcpy(out, &h, sizeof(h));
     if (K) encrypt_bytes_pipeline(ctx, x, n, K, out + sizeof(BlobHeader));
   });
@@ -821,7 +851,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
                                 size_t C, uint64_t K, uint8_t* out_payload) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
-  // chunk: ~32 MiB of input per learner-group buffer, at least 1 ciphertext
+  // chunk: ~64 MiB of input per learner-group buffer, at least 1 ciphertext
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
@@ -829,33 +859,22 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
   uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (in_chunk + out_chunk));
   uint8_t* inb[2] = {io, io + in_chunk};
   uint8_t* outb[2] = {io + 2 * in_chunk, io + 2 * in_chunk + out_chunk};
-  hipStream_t sA = ctx->stream, sB = ctx->stream2;
-  hipEvent_t copied[2], done[2];
-  for (int i = 0; i < 2; ++i) {
-    SHELFI_HIP(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming));
-    SHELFI_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
-  }
-  struct Ev {
-    hipEvent_t* e;
-    ~Ev() {
-      for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
-    }
-  };
-  hipEvent_t all[4] = {copied[0], copied[1], done[0], done[1]};
-  Ev guard{all};
+  // A: staged H2D of the learners' slices; B: wavg; C: staged D2H of the sum
+  Pipe pp(ctx);
+  StageRun sr(stager(ctx));
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
     for (size_t c0 = 0; c0 < C; c0 += group) {
       const size_t gc = std::min(group, C - c0);
-      if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(sA, done[b], 0));  // buffer free
+      if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
       for (size_t c = 0; c < gc; ++c)
-        SHELFI_HIP(hipMemcpyAsync(inb[b] + c * kn * ct_bytes,
-                                  blobs[c0 + c] + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes,
-                                  hipMemcpyHostToDevice, sA));
-      SHELFI_HIP(hipEventRecord(copied[b], sA));
-      SHELFI_HIP(hipStreamWaitEvent(sB, copied[b], 0));
+        sr.s.h2d(inb[b] + c * kn * ct_bytes, blobs[c0 + c] + sizeof(BlobHeader) + k0 * ct_bytes,
+                 kn * ct_bytes, pp.a);
+      SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
+      SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+      if (ci >= 2 && c0 == 0) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       WavgArgs a;
       std::memset(&a, 0, sizeof(a));
       for (size_t c = 0; c < gc; ++c) a.ptrs[c] = (const uint64_t*)(inb[b] + c * kn * ct_bytes);
@@ -866,15 +885,18 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
       a.L = p.L;
       a.logN = p.logN;
       a.accumulate = c0 ? 1 : 0;
-      launch_wavg(a, ctx->dt.tc, sB);
-      if (c0 + gc >= C)
-        SHELFI_HIP(hipMemcpyAsync(out_payload + k0 * ct_bytes, outb[b], kn * ct_bytes,
-                                  hipMemcpyDeviceToHost, sB));
-      SHELFI_HIP(hipEventRecord(done[b], sB));
+      launch_wavg(a, ctx->dt.tc, pp.b);
+      SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+      if (c0 + gc >= C) {
+        SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
+        sr.s.d2h(out_payload + k0 * ct_bytes, outb[b], kn * ct_bytes, pp.c);
+        SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+      }
+      sr.s.poll();
     }
   }
-  SHELFI_HIP(hipStreamSynchronize(sB));
-  SHELFI_HIP(hipStreamSynchronize(sA));
+  sr.finish();
+  pp.sync();
 }
 
 int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
@@ -913,6 +935,7 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     *out_len = total;
     if (!out) return;  // size query
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
+    advise_huge(out, total);
     std::memcpy(out, &ho, sizeof(ho));
     if (ho.K) wavg_bytes_pipeline(ctx, blobs, weights, C, ho.K, out + sizeof(BlobHeader));
   });
@@ -942,14 +965,15 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc));
     Pipe pp(ctx);
+    StageRun sr(stager(ctx));
+    advise_huge(out, n * 8);
     const uint64_t nchunks = (K + kc - 1) / kc;
     for (uint64_t ci = 0; ci < nchunks; ++ci) {
       const int b = (int)(ci & 1);
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
-      SHELFI_HIP(hipMemcpyAsync(cb[b], blob + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes,
-                                hipMemcpyHostToDevice, pp.a));
+      sr.s.h2d(cb[b], blob + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes, pp.a);
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
@@ -957,9 +981,11 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
                      scratch, pp.b);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
-      SHELFI_HIP(hipMemcpyAsync(out + o0, ob[b], on * 8, hipMemcpyDeviceToHost, pp.c));
+      sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
       SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+      sr.s.poll();
     }
+    sr.finish();
     pp.sync();
   });
 }

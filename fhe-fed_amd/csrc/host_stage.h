@@ -1,0 +1,100 @@
+// Host <-> HBM staging for the bytes API.
+//
+// The bytes API hands over pageable Python buffers.  A DMA from pageable memory makes
+// the HIP runtime copy through its own staging buffer on the calling thread, so
+// hipMemcpyAsync blocks the host and the H2D / compute / D2H pipeline serializes;
+// and a freshly allocated output (a new bytes object) first-touch faults on the copy
+// thread at ~16 GB/s.  The Stager instead owns rings of pinned slots: pageable data
+// is memcpy'd into a slot by a pool of threads (faults spread over the cores) and the
+// slot is DMA'd asynchronously; outputs are DMA'd into pinned slots and drained into
+// the destination by the same pool while later DMAs run.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace shelfi {
+
+// Persistent workers splitting one memcpy at a time (the caller takes a share too).
+class CopyPool {
+ public:
+  explicit CopyPool(int threads);
+  ~CopyPool();
+  CopyPool(const CopyPool&) = delete;
+  CopyPool& operator=(const CopyPool&) = delete;
+  void copy(void* dst, const void* src, size_t n);
+  int threads() const { return parts_; }
+
+ private:
+  void run(int id);
+  int parts_ = 1;  // set before the workers start
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_go_, cv_done_;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t n_ = 0;
+};
+
+class Stager {
+ public:
+  // slot_bytes: DMA granule; n_in / n_out: pinned slots per direction.
+  Stager(size_t slot_bytes, int n_in, int n_out, int threads);
+  ~Stager();
+  Stager(const Stager&) = delete;
+  Stager& operator=(const Stager&) = delete;
+
+  // Enqueue host -> device of n bytes on `s`.  Returns once the data has been copied
+  // into pinned slots (the source may then be reused); the DMAs run asynchronously.
+  void h2d(void* dev, const void* host, size_t n, hipStream_t s);
+  // Enqueue device -> host of n bytes on `s`.  `host` is written later, by poll() /
+  // finish() (or when its slot is needed again); it must stay valid until finish().
+  void d2h(void* host, const void* dev, size_t n, hipStream_t s);
+  // Drain every output slot whose DMA has completed (non-blocking).
+  void poll();
+  // Drain all outputs and wait for all inputs.  Must be called before the host
+  // buffers are touched or released; rethrows the first error.
+  void finish();
+  // Abandon in-flight work after an error: wait for the DMAs, drop pending outputs.
+  void abort() noexcept;
+
+  size_t slot_bytes() const { return slot_bytes_; }
+  int threads() const { return pool_.threads(); }
+
+ private:
+  struct Slot {
+    uint8_t* host = nullptr;
+    hipEvent_t ev = nullptr;
+    bool used = false;      // an event has been recorded
+    uint8_t* dst = nullptr;  // pending output destination (d2h slots)
+    size_t len = 0;
+  };
+  bool drain_front(bool block);
+  void wait_in_slot(Slot& sl);
+
+  size_t slot_bytes_;
+  std::vector<Slot> in_, out_;
+  size_t in_next_ = 0, out_next_ = 0;
+  std::deque<size_t> pending_;  // out slot indices in enqueue order
+  CopyPool pool_;
+};
+
+// Ask for transparent huge pages on the 2 MiB-aligned interior of a large output
+// buffer that has not been touched yet (a new bytes object: 512x fewer first-touch
+// faults and a cheaper munmap later).  numpy does the same for its large arrays.
+void advise_huge(void* p, size_t n);
+
+// Worker threads for a Stager: SHELFI_COPY_THREADS, else min(8, CPUs this process may use).
+int default_copy_threads();
+
+}  // namespace shelfi

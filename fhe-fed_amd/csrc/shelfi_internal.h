@@ -90,12 +90,17 @@ struct DeviceKeys {
 
 }  // namespace shelfi
 
+namespace shelfi {
+class Stager;
+}
+
 struct shelfi_ctx {
   shelfi::Params p;
   int device = 0;
   hipStream_t stream = nullptr;   // copy / default work stream
   hipStream_t stream2 = nullptr;  // compute stream of the pipelined bytes API
   hipStream_t stream3 = nullptr;  // copy-out stream of the pipelined bytes API
+  shelfi::Stager* stage = nullptr;  // pinned staging rings (host_stage.h), lazily created
   shelfi::DeviceTables dt;
   shelfi::DeviceKeys dk;
   std::vector<uint64_t> pk_host, sk_host;
