@@ -9,13 +9,20 @@ combined by one RCCL reduce_scatter over xGMI + the modq kernel (SHELFI_FHE/dist
 
 Workload (default): BASELINE config 3's per-GPU shard — 16 learners x ResNet-18
 (11,689,512 params -> 714 ciphertexts of 16384 slots), ring 2^15, L = 4 towers;
-at --gpus 8 this is config 3 (128 learners).  --workload cfg2 runs config 2
-(16 learners x LeNet-5, 4 ciphertexts) instead.
+at --gpus 8 this is config 3 (128 learners).  Other BASELINE configs as parity /
+secondary workloads: --workload cfg2 (16 x LeNet-5, 4 cts), cfg4 (16 learners,
+ring 2^16, L = 6, 2^20 params -> 32 cts), cfg5 (selective encryption: 10% of
+ResNet-50's 25,557,032 params -> 156 cts, 8 learners per GPU = 64 at --gpus 8).
+
+Inputs follow SURVEY §8(d): learner i's vector is
+np.random.default_rng(1000 + i).uniform(-1, 1, n) through float32 (learner i lives on
+rank i mod G), encrypted on device; weights 1/C.
 
 Prints ONE JSON line (rank 0).  Also measured on the same inputs: device-resident
-encode+encrypt and decrypt+decode ms per ciphertext; a rocprof-comparable per-launch
-wavg duration from HIP events (roofline); and the CPU baseline (oracle/ Shoup port,
-1 thread, bounded sample) on this host.
+encode+encrypt and decrypt+decode ms per ciphertext (with their HBM fractions); a
+rocprof-comparable per-launch wavg duration from HIP events (roofline); the bytes
+API sample (PCIe-inclusive); and the CPU baseline (oracle/ port, 1 thread and all
+cores, plus its encrypt/decrypt ms per ciphertext) on this host.
 """
 from __future__ import annotations
 
@@ -29,8 +36,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fhe-fed_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-RESNET18_PARAMS = 11_689_512
-LENET5_PARAMS = 61_706
+# name -> (slots, multDepth, params per learner, learners per GPU, description)
+WORKLOADS = {
+    "cfg2": (16384, 3, 61_706, 16, "LeNet-5"),
+    "cfg3": (16384, 3, 11_689_512, 16, "ResNet-18"),
+    "cfg4": (32768, 5, 1 << 20, 16, "2^20-parameter vector"),
+    "cfg5": (16384, 3, 2_555_703, 8, "10% of ResNet-50 (selective encryption)"),
+}
 METRIC = "ciphertexts aggregated/sec (+ encode+enc / dec+decode ms), N clients, ring 2^15 L=4"
 
 
@@ -39,8 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["cfg3", "cfg2"], default="cfg3")
-    ap.add_argument("--learners-per-gpu", type=int, default=16)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
+    ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--pieces", type=int, default=4,
                     help="N>1: ciphertext pieces whose RCCL reduce_scatter overlaps the next piece's wavg")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
@@ -54,9 +66,40 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(N, L, q, delta, C, seconds):
-    """Oracle Shoup-constant port (oracle/ckks_oracle.c or_wavg_fast), 1 thread, a
-    bounded sample of the same workload: C learners x 4 ciphertexts, repeated."""
+def _median_rate(fn, units, seconds, parts=5):
+    """Warm once, then `parts` timed chunks of ~seconds/parts each; median rate."""
+    fn()
+    rates = []
+    for _ in range(parts):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / parts:
+                break
+        rates.append(reps * units / el)
+    rates.sort()
+    return rates[len(rates) // 2]
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(N, L, q, psi, delta, slots, C, seconds):
+    """The oracle port (oracle/ckks_oracle.c) on this host, bounded samples of the same
+    workload: aggregation = or_wavg_fast (Shoup constant modmul, as
+    PALISADE's NativeVector ModMul by a scalar) over C learners x 4 ciphertexts, median
+    of 5 at 1 thread (the reported value) and at all usable cores; encode+encrypt and
+    decrypt+decode ms per ciphertext (1 thread, oracle encrypt/decrypt)."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -72,19 +115,37 @@ def cpu_baseline(N, L, q, delta, C, seconds):
         cts.append(a)
     w = [1.0 / C] * C
     out = np.zeros_like(cts[0])
-    O.wavg_fast(cts, w, q, delta, nthreads=1, out=out)  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        O.wavg_fast(cts, w, q, delta, nthreads=1, out=out)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    rate = reps * C * Ks / el
-    return {"value": rate, "unit": "client-ciphertexts/s", "cores": 1, "kind": "port",
-            "sample": "%d learners x %d ciphertexts (N=%d, L=%d), %d repetitions in %.1f s; "
-                      "oracle/ckks_oracle.c or_wavg_fast (Shoup constant modmul, as PALISADE's "
-                      "NativeVector ModMul by a scalar), 1 thread" % (C, Ks, N, L, reps, el)}
+    # this process's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box
+    # does; its affinity mask shows the whole machine), else the affinity mask
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    one = _median_rate(lambda: O.wavg_fast(cts, w, q, delta, nthreads=1, out=out), C * Ks, seconds)
+    allc = _median_rate(lambda: O.wavg_fast(cts, w, q, delta, nthreads=cores, out=out), C * Ks,
+                        max(2.0, seconds / 4))
+    # encode+encrypt / decrypt+decode: synthetic keys of this context (timing only)
+    s = rng.integers(-1, 2, N).astype(np.int64)
+    sk = np.empty((L, N), np.uint64)
+    for t in range(L):
+        sk[t] = O.ntt_fwd((s % int(q[t])).astype(np.uint64), q[t], psi[t])
+    pk = np.empty((2, L, N), np.uint64)
+    for t in range(L):
+        pk[:, t, :] = rng.integers(0, int(q[t]), (2, N), dtype=np.uint64)
+    x = rng.uniform(-1, 1, 2 * slots).astype(np.float32).astype(np.float64)
+    t0 = time.perf_counter()
+    enc = O.encrypt_vector(x, pk, q, psi, N, slots, delta, seed=5)
+    enc_ms = (time.perf_counter() - t0) * 1e3 / enc.shape[0]
+    t0 = time.perf_counter()
+    for k in range(enc.shape[0]):
+        try:
+            O.decrypt(enc[k], sk, q, psi, slots, delta, slots)
+        except ValueError:  # random pk: the value is garbage, the work is the same
+            pass
+    dec_ms = (time.perf_counter() - t0) * 1e3 / enc.shape[0]
+    return {"value": round(one, 1), "unit": "client-ciphertexts/s", "cores": 1, "kind": "port",
+            "sample": "%d learners x %d ciphertexts (N=%d, L=%d), median of 5 chunks over %.0f s; "
+                      "oracle/ckks_oracle.c or_wavg_fast, 1 thread" % (C, Ks, N, L, seconds),
+            "all_cores": {"value": round(allc, 1), "cores": cores},
+            "encode_encrypt_ms_per_ct": round(enc_ms, 3), "decrypt_decode_ms_per_ct": round(dec_ms, 3),
+            "host": {"cpu_model": _cpu_model(), "usable_cores": cores}}
 
 
 def main():
@@ -108,28 +169,30 @@ def main():
     from SHELFI_FHE import device as D
     from SHELFI_FHE import dist as SD
 
-    batch = 16384
-    params = RESNET18_PARAMS if args.workload == "cfg3" else LENET5_PARAMS
+    batch, depth, params, Cl_default, model = WORKLOADS[args.workload]
     K = -(-params // batch)
-    Cl = args.learners_per_gpu
+    Cl = args.learners_per_gpu or Cl_default
     # one key pair shared by every rank (seeded keygen, no key files written), then a
     # per-rank encryption stream
-    ck = m.CKKS("ckks", batch, 52, "", multDepth=3, device=local, seed=7)
+    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, device=local, seed=7)
     if ck.genCryptoContextAndKeyGen() != 1:
         raise SystemExit("keygen failed")
     ck.set_seed(1000 + rank)
     inf = ck.info()
     N, L = inf["ring_dim"], inf["num_towers"]
     q = np.array(inf["moduli"], np.uint64)
+    psi = np.array(inf["roots"], np.uint64)
     delta = inf["delta"]
     dev = torch.device("cuda", local)
 
-    # synthetic learners: float32 model weights U(-0.1, 0.1), encrypted on device
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
+    # synthetic learners: global learner i = rank + world * j gets
+    # default_rng(1000 + i).uniform(-1, 1, n) through float32, encrypted on device
     cts, enc_times = [], []
-    for i in range(Cl):
-        x = (torch.rand(params, generator=g, device=dev, dtype=torch.float32) * 0.2 - 0.1).double()
+    for j in range(Cl):
+        i = rank + world * j
+        xh = np.random.default_rng(1000 + i).uniform(-1, 1, params).astype(np.float32)
+        x = torch.from_numpy(xh).to(dev).double()
+        del xh
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         cts.append(D.encrypt(ck, x))
@@ -258,29 +321,41 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "wavg_kernel", "bytes_per_launch": bytes_per_launch,
                 "launch_ms_avg": round(kern_avg_ms, 4), "launch_ms_min": round(kern_ms[0], 4)}
+    # encrypt / decrypt per ciphertext: SURVEY §8(d) algorithmic bytes (f64 slots + ct,
+    # keys amortized) over the measured time; these are VALU-bound (NTT), the HBM
+    # fraction says how far from the memory bound they run
+    enc_ms = 1e3 * sorted(enc_times)[len(enc_times) // 2] / K
+    ct_bytes = 16 * L * N
+    enc_bytes = 8 * batch + ct_bytes + ct_bytes / K
+    dec_bytes = ct_bytes + 8 * L * N / K + 8 * batch
+
+    def frac(bytes_, ms):
+        return round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     res = {
         "metric": METRIC, "value": round(value, 1), "unit": "client-ciphertexts/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-        "data": "synthetic: real CKKS encryptions (device encoder + ChaCha20 sampler) of U(-0.1,0.1) "
-                "float32 weights; inputs resident in HBM before the timed region",
-        "config": {"workload": "%s: %d learners/GPU x %s (%d params -> %d cts of %d slots), ring 2^15, "
-                               "L=4 towers%s" % (args.workload, Cl,
-                                                 "ResNet-18" if args.workload == "cfg3" else "LeNet-5",
-                                                 params, K, batch,
-                                                 "" if world == 1 else
-                                                 ", RCCL reduce_scatter overlapped in %d pieces" % args.pieces),
+        "data": "synthetic: real CKKS encryptions (device encoder + ChaCha20 sampler) of "
+                "default_rng(1000+i).uniform(-1,1) float32 vectors; inputs resident in HBM before "
+                "the timed region",
+        "config": {"workload": "%s: %d learners/GPU x %s (%d params -> %d cts of %d slots), ring 2^%d, "
+                               "L=%d towers%s" % (args.workload, Cl, model, params, K, batch,
+                                                  N.bit_length() - 1, L,
+                                                  "" if world == 1 else
+                                                  ", RCCL reduce_scatter overlapped in %d pieces" % args.pieces),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
                    "parallelism": "learner-sharded dp%d" % world, "layout": args.layout},
         "roofline": roofline,
-        "encode_encrypt_ms_per_ct": round(1e3 * sorted(enc_times)[len(enc_times) // 2] / K, 5),
+        "encode_encrypt_ms_per_ct": round(enc_ms, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),
+        "encrypt_hbm_frac": frac(enc_bytes, enc_ms),
+        "decrypt_hbm_frac": frac(dec_bytes, dec_ms_per_ct),
     }
     if api:
         res["api_bytes_path"] = api
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(N, L, q, delta, Cl, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(N, L, q, psi, delta, batch, Cl, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
