@@ -127,6 +127,22 @@ class CKKS(Scheme):
     def set_seed(self, seed: int) -> None:
         check(self._lib.shelfi_set_seed(self._ctx, int(seed)))
 
+    def set_decode_noise(self, enabled: bool = True, m_factor: float = 1.0) -> None:
+        """PALISADE 1.11's decode noise flooding (CKKSPackedEncoding::Decode): Gaussian
+        noise of stddev sqrt(m_factor + 1) * max(sigma, sqrt(N)/8) at scale 2^p, where
+        sigma is estimated from the decryption's anti-symmetric part, and a RuntimeError
+        when log2 sigma > scaleFactorBits - 5.  Off by default: decrypt is then exact
+        and deterministic (the noise-free value PALISADE floods)."""
+        check(self._lib.shelfi_set_decode_noise(self._ctx, 1 if enabled else 0, float(m_factor)),
+              "set_decode_noise")
+
+    def last_log_precision(self):
+        """PALISADE Plaintext::GetLogPrecision of the last flooded decrypt (worst
+        ciphertext): scaleFactorBits - logError; None if none was flooded."""
+        le = C.c_int()
+        check(self._lib.shelfi_decode_log_error(self._ctx, C.byref(le)), "decode_log_error")
+        return None if le.value < 0 else self.info()["scale_bits"] - le.value
+
     # ---------------------------------------------------------- keys (a2/a3) --
     def loadCryptoParams(self) -> None:
         """ckks.cpp:11-23: failures are printed, never raised."""
@@ -217,7 +233,7 @@ class CKKS(Scheme):
             learner_data = learner_data.encode("latin-1")
         b = bytes(learner_data)
         n = int(data_dimensions)
-        out = np.zeros(n, np.float64)
+        out = np.empty(n, np.float64)
         check(self._lib.shelfi_decrypt(self._ctx, C.cast(C.c_char_p(b), _lib.u8p), len(b), n,
                                        out.ctypes.data_as(_lib.f64p)), "decrypt")
         return out

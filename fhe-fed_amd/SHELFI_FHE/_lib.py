@@ -19,6 +19,7 @@ SHELFI_ERR_IO = -3
 SHELFI_ERR_FORMAT = -4
 SHELFI_ERR_STATE = -5
 SHELFI_ERR_RANGE = -6
+SHELFI_ERR_PRECISION = -7
 
 MAX_TOWERS = 16
 
@@ -64,6 +65,8 @@ SIGNATURES = {
     "shelfi_set_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_get_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_encrypt": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_set_decode_noise": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "shelfi_decode_log_error": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "shelfi_encrypt_into": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]),
     "shelfi_weighted_average": (C.c_int, [C.c_void_p, C.POINTER(u8p), C.POINTER(C.c_size_t), f32p,

@@ -941,6 +941,49 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
   });
 }
 
+// Noise-flooding setup for one decrypt of K ciphertexts (enabled by
+// shelfi_set_decode_noise); its randomness comes from the ctx stream like encrypt's.
+static DecodeNoise decode_noise_begin(shelfi_ctx* ctx, uint64_t K, hipStream_t s) {
+  DecodeNoise dn;
+  if (!ctx->decode_noise) return dn;
+  dn.enabled = 1;
+  dn.m_factor = ctx->decode_m_factor;
+  dn.p_bits = ctx->p.scale_bits;
+  draw_key(ctx, K, dn.key, &dn.g0);
+  dn.flags = ctx->dev_flag;
+  SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 1, 0, 8, s));
+  return dn;
+}
+
+// After the decrypt's stream work has completed: record logError, raise PALISADE's
+// precision failure (Decode throws math_error when log2 sigma > p - 5).
+static void decode_noise_end(shelfi_ctx* ctx, DecodeNoise& dn) {
+  if (!dn.enabled) return;
+  std::memset(dn.key, 0, sizeof(dn.key));
+  uint32_t f[2] = {0, 0};
+  SHELFI_HIP(hipMemcpy(f, ctx->dev_flag + 1, 8, hipMemcpyDeviceToHost));
+  ctx->last_log_error = (int)f[1];
+  if (f[0])
+    throw Error{SHELFI_ERR_PRECISION,
+                "The decryption failed because the approximation error is too high. Check the "
+                "parameters."};
+}
+
+int shelfi_set_decode_noise(shelfi_ctx* ctx, int enabled, double m_factor) {
+  if (!ctx || !(m_factor >= 0.0) || !std::isfinite(m_factor)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  ctx->decode_noise = enabled ? 1 : 0;
+  ctx->decode_m_factor = m_factor;
+  return SHELFI_OK;
+}
+
+int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
+  if (!ctx || !log_error) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  *log_error = ctx->last_log_error;
+  return SHELFI_OK;
+}
+
 int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out) {
   if (!ctx || (n && !out)) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
@@ -967,6 +1010,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     Pipe pp(ctx);
     StageRun sr(stager(ctx));
     advise_huge(out, n * 8);
+    DecodeNoise dn = decode_noise_begin(ctx, K, pp.b);
     const uint64_t nchunks = (K + kc - 1) / kc;
     for (uint64_t ci = 0; ci < nchunks; ++ci) {
       const int b = (int)(ci & 1);
@@ -977,8 +1021,9 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
+      dn.g0 += (ci ? kc : 0);
       launch_decrypt(p, ctx->dt, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
-                     scratch, pp.b);
+                     scratch, pp.b, &dn);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
       sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
@@ -987,6 +1032,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     }
     sr.finish();
     pp.sync();
+    decode_noise_end(ctx, dn);
   });
 }
 
@@ -1150,13 +1196,17 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
     const uint64_t kc_max = std::min<uint64_t>(chunk, Kn);
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
     const size_t ct_words = 2ull * p.L * p.N;
+    DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
+    const uint64_t g0 = dn.g0;
     for (uint64_t k0 = 0; k0 < Kn; k0 += kc_max) {
       const uint64_t kc = std::min(kc_max, Kn - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
+      dn.g0 = g0 + k0;
       launch_decrypt(p, ctx->dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0,
-                     scratch, s);
+                     scratch, s, &dn);
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
+    decode_noise_end(ctx, dn);
   });
 }
 

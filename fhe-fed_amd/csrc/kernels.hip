@@ -1103,13 +1103,134 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
   fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
 }
 
+// ------------------------------------------------- decode noise flooding ----
+// PALISADE 1.11 CKKSPackedEncoding::Decode, on the coefficient
+// pairs v_i = (c[i gap], c[N/2 + i gap]) / scale that crt_decode_kernel wrote at
+// bitrev(i).  m(X^-1) in this packing is conj_0 = (re_0, -im_0),
+// conj_i = (-im_{S-i}, -re_{S-i}); the anti-symmetric part u = v - conj has S
+// independent components (i = 0: 2 im_0; 0 < i < S/2: both; i = S/2: one), whose
+// sample stddev / 2 estimates the decryption error sigma.  In 2^p units (p = scale
+// bits, PALISADE's plaintext modulus): fail if log2 sigma > p - 5; sigma >= sqrt(N)/8;
+// stddev = sqrt(M+1) sigma; each output becomes (v + conj)/2 + 2^-p N(0, stddev);
+// logError = round(log2(stddev sqrt(2 S))).  One block per ciphertext.
+__device__ __forceinline__ double block_sum_1024(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x < 64) {
+    s = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (threadIdx.x == 0) red[16] = s;
+  }
+  __syncthreads();
+  s = red[16];
+  __syncthreads();
+  return s;
+}
+
+// Box-Muller pair from two 64-bit words: u1 in (0, 1], u2 in [0, 1).
+__device__ __forceinline__ void box_muller(uint64_t a, uint64_t b, double& z0, double& z1) {
+  const double u1 = (double)((a >> 11) + 1) * 0x1.0p-53;
+  const double u2 = (double)(b >> 11) * 0x1.0p-53;
+  const double r = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);
+  z0 = r * cs;
+  z1 = r * sn;
+}
+
+__global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict__ fbuf, uint32_t logS,
+                                                            uint32_t logN, double two_p,
+                                                            double p_bits, double m_factor,
+                                                            Key8 key, uint64_t g0,
+                                                            uint32_t* __restrict__ flags) {
+  __shared__ double red[17];
+  const uint32_t S = 1u << logS, half = S >> 1;
+  double2* __restrict__ f = fbuf + (uint64_t)blockIdx.x * S;
+  // u components of pair index i in [0, S/2]
+  auto comps = [&](uint32_t i, double& a, double& b) -> int {
+    const double2 x = f[bitrev_dev(i, logS)];
+    if (i == 0) {
+      a = 2.0 * x.y;
+      return 1;
+    }
+    if (i == half) {
+      a = x.x + x.y;
+      return 1;
+    }
+    const double2 y = f[bitrev_dev(S - i, logS)];
+    a = x.x + y.y;
+    b = x.y + y.x;
+    return 2;
+  };
+  double sigma;
+  if (S == 1) {
+    sigma = fabs(f[0].y);  // PALISADE StdDev: vec[0].imag() for one slot
+  } else {
+    double s1 = 0.0;
+    for (uint32_t i = threadIdx.x; i <= half; i += blockDim.x) {
+      double a = 0.0, b = 0.0;
+      const int c = comps(i, a, b);
+      s1 += a + (c == 2 ? b : 0.0);
+    }
+    const double mean = block_sum_1024(s1, red) / (double)S;
+    double s2 = 0.0;
+    for (uint32_t i = threadIdx.x; i <= half; i += blockDim.x) {
+      double a = 0.0, b = 0.0;
+      const int c = comps(i, a, b);
+      s2 += (a - mean) * (a - mean) + (c == 2 ? (b - mean) * (b - mean) : 0.0);
+    }
+    const double var = block_sum_1024(s2, red) / (double)(S - 1);
+    sigma = 0.5 * sqrt(var);
+  }
+  double sigma_p = sigma * two_p;  // PALISADE works at scale 2^p
+  const double logstd = log2(sigma_p);
+  if (!(logstd <= p_bits - 5.0)) {
+    if (threadIdx.x == 0) atomicOr(&flags[1], 1u);  // decode precision failure
+  }
+  const double floor_sd = 0.125 * sqrt((double)(1u << logN));
+  if (sigma_p < floor_sd) sigma_p = floor_sd;
+  const double stddev_p = sqrt(m_factor + 1.0) * sigma_p;
+  if (threadIdx.x == 0) {
+    const double le = rint(log2(stddev_p * sqrt(2.0 * (double)S)));
+    atomicMax((int*)&flags[2], (int)le);
+  }
+  const double nsd = stddev_p / two_p;  // noise stddev in output units
+  const uint64_t nonce = (3ull << 56) | (g0 + blockIdx.x);
+  __syncthreads();  // every thread has read its pairs before any is overwritten
+  for (uint32_t i = threadIdx.x; i <= half; i += blockDim.x) {
+    uint64_t w[8];
+    chacha20_block(key, i, nonce, w);
+    double z[4];
+    box_muller(w[0], w[1], z[0], z[1]);
+    box_muller(w[2], w[3], z[2], z[3]);
+    const uint32_t pi = bitrev_dev(i, logS);
+    const double2 x = f[pi];
+    if (i == 0) {
+      f[pi] = make_double2(x.x + nsd * z[0], nsd * z[1]);
+      if (S == 1) continue;
+    } else if (i == half) {
+      f[pi] = make_double2(0.5 * (x.x - x.y) + nsd * z[0], 0.5 * (x.y - x.x) + nsd * z[1]);
+    } else {
+      const uint32_t pj = bitrev_dev(S - i, logS);
+      const double2 y = f[pj];
+      f[pi] = make_double2(0.5 * (x.x - y.y) + nsd * z[0], 0.5 * (x.y - y.x) + nsd * z[1]);
+      f[pj] = make_double2(0.5 * (y.x - x.y) + nsd * z[2], 0.5 * (y.y - x.x) + nsd * z[3]);
+    }
+  }
+}
+
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
   return K * (uint64_t)p.L * p.N * sizeof(uint64_t) + K * (uint64_t)p.batch * sizeof(double2);
 }
 
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s) {
+                    void* scratch, hipStream_t s, const DecodeNoise* dn) {
   if (!K) return;
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
@@ -1134,6 +1255,14 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                      dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
                      fbuf);
   SHELFI_HIP(hipGetLastError());
+  if (dn && dn->enabled) {
+    Key8 k8;
+    for (int i = 0; i < 8; ++i) k8.k[i] = dn->key[i];
+    hipLaunchKernelGGL(decode_flood_kernel, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, logS, p.logN,
+                       ldexp(1.0, (int)dn->p_bits), (double)dn->p_bits, dn->m_factor, k8, dn->g0,
+                       dn->flags);
+    SHELFI_HIP(hipGetLastError());
+  }
   const uint32_t blkLog = logS < (uint32_t)kFftBlockLog ? logS : (uint32_t)kFftBlockLog;
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;

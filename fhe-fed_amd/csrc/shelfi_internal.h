@@ -110,7 +110,11 @@ struct shelfi_ctx {
   uint64_t params_id = 0;
   uint64_t seed = 0;          // 0 -> OS entropy per call
   uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
-  uint32_t* dev_flag = nullptr;  // device error flag (encode range)
+  uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
+                                 // [2] max decode logError (noise flooding)
+  int decode_noise = 0;          // shelfi_set_decode_noise
+  double decode_m_factor = 1.0;
+  int last_log_error = -1;       // of the last flooded decrypt, -1 if none
   // scratch arena (grown on demand, never shrunk)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -141,9 +145,18 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                     const double* x, uint64_t n, uint64_t K, uint64_t* ct, void* scratch,
                     const uint32_t key[8], uint64_t g0, uint32_t* flag, hipStream_t s);
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K);
+// Decode noise flooding (PALISADE 1.11 Decode); off = exact decode.
+struct DecodeNoise {
+  int enabled = 0;
+  double m_factor = 1.0;   // CKKS_M_FACTOR
+  uint32_t p_bits = 52;    // PALISADE plaintext modulus of CKKS = scale bits
+  uint32_t key[8] = {};    // ChaCha20 key, nonce (3 << 56) | (g0 + ciphertext)
+  uint64_t g0 = 0;
+  uint32_t* flags = nullptr;  // device: [1] |= precision failure, [2] = max logError
+};
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s);
+                    void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr);
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
 void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
                    uint64_t* pk, void* scratch, hipStream_t s);

@@ -33,6 +33,7 @@ extern "C" {
 #define SHELFI_ERR_FORMAT -4   /* malformed / mismatched ciphertext or key blob */
 #define SHELFI_ERR_STATE -5    /* keys not loaded, etc. */
 #define SHELFI_ERR_RANGE -6    /* value outside the CKKS encoding/decoding range */
+#define SHELFI_ERR_PRECISION -7 /* decode: approximation error too high (PALISADE math_error) */
 
 typedef struct shelfi_ctx shelfi_ctx;
 
@@ -110,6 +111,17 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
                                  size_t out_cap, size_t* out_len);
 /* ckks.cpp:170-213 decrypt: blob -> n doubles (caller-owned out[n]). */
 int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out);
+
+/* Decode noise flooding, PALISADE 1.11 CKKSPackedEncoding::Decode:
+ * symmetrize, estimate sigma from the anti-symmetric part, add Gaussian noise of
+ * stddev sqrt(m_factor + 1) * max(sigma, sqrt(N)/8) (m_factor = CKKS_M_FACTOR, 1 in
+ * PALISADE), fail with SHELFI_ERR_PRECISION when log2 sigma > scale_bits - 5.  Off by
+ * default (exact, deterministic decode); applies to shelfi_decrypt and
+ * shelfi_dev_decrypt.  Randomness: the ctx's seeded / OS-random ChaCha20 stream. */
+int shelfi_set_decode_noise(shelfi_ctx* ctx, int enabled, double m_factor);
+/* logError of the last flooded decrypt (max over its ciphertexts; PALISADE
+ * Plaintext::GetLogError), -1 if none.  Precision = scale_bits - logError. */
+int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error);
 
 /* Blob inspection: number of ciphertexts, depth, scale, key id. */
 int shelfi_blob_info(const uint8_t* blob, size_t len, uint64_t* num_cts, uint32_t* depth,

@@ -639,10 +639,12 @@ int or_crt_centered(const uint64_t* r, uint32_t L, const uint64_t* q, int64_t* h
 
 /* decrypt one ciphertext ct[2][L][N] with sk[L][N] (EVAL).  Writes the first
  * `n` real slot values to out.  Returns 0 / negative on error. */
-int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
-               const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
-               size_t n, double* out) {
-  if (n > slots) return -1;
+/* b = c0 + c1*s -> INTT -> centered CRT -> / scale, as coefficient pairs
+ * (re_i, im_i) = (c[i*gap], c[N/2 + i*gap]) / scale (PALISADE Decode's curValues
+ * before the 2^p normalisation). */
+int or_decrypt_coeffs(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
+                      const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
+                      double* re, double* im) {
   uint64_t* b = malloc(sizeof(uint64_t) * L * N);
   for (uint32_t t = 0; t < L; ++t) {
     const uint64_t* c0 = ct + (size_t)t * N;
@@ -654,8 +656,6 @@ int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
   }
   double inv_scale = 1.0 / scale;
   uint32_t gap = N / (2 * slots);
-  double* re = malloc(sizeof(double) * slots);
-  double* im = malloc(sizeof(double) * slots);
   uint64_t r[16];
   int rc = 0;
   for (uint32_t i = 0; i < slots && !rc; ++i) {
@@ -669,14 +669,90 @@ int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
       if (part) im[i] = v; else re[i] = v;
     }
   }
+  free(b);
+  return rc;
+}
+
+int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
+               const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
+               size_t n, double* out) {
+  if (n > slots) return -1;
+  double* re = malloc(sizeof(double) * slots);
+  double* im = malloc(sizeof(double) * slots);
+  int rc = or_decrypt_coeffs(ct, sk, N, L, q, psi, slots, scale, re, im);
   if (!rc) {
     or_fft_special(re, im, slots);
     for (size_t i = 0; i < n; ++i) out[i] = re[i];
   }
   free(re);
   free(im);
-  free(b);
   return rc;
+}
+
+/* PALISADE 1.11 CKKSPackedEncoding::Decode noise flooding [PALISADE-1.11, SURVEY
+ * App. B.6], restated on the coefficient pairs above (output units; PALISADE's
+ * 2^p-scaled values are these times 2^p, an exact power-of-two rescaling):
+ *   conj_0 = (re_0, -im_0), conj_i = (-im_{S-i}, -re_{S-i})        (m(X^-1))
+ *   u = v - conj over its S independent components (i = 0: im; 0 < i < S/2: re, im;
+ *   i = S/2: re);  sigma = 0.5 * sqrt(sum (u - mean)^2 / (S - 1))  (S = 1: |im_0|)
+ *   sigma_p = sigma 2^p;  fail if log2 sigma_p > p - 5;  sigma_p >= sqrt(N)/8;
+ *   stddev_p = sqrt(M + 1) sigma_p;  logError = round(log2(stddev_p sqrt(2S))).
+ * The normalisation constants are restated, not pinned (PALISADE absent). */
+void or_decode_stats(const double* re, const double* im, uint32_t S, uint32_t N, uint32_t p_bits,
+                     double m_factor, double* stddev_p, int* log_error, int* fail) {
+  double sigma;
+  uint32_t half = S / 2;
+  if (S == 1) {
+    sigma = fabs(im[0]);
+  } else {
+    double s1 = 0.0;
+    for (uint32_t i = 0; i <= half; ++i) {
+      if (i == 0) s1 += 2.0 * im[0];
+      else if (i == half) s1 += re[i] + im[i];
+      else s1 += (re[i] + im[S - i]) + (im[i] + re[S - i]);
+    }
+    double mean = s1 / (double)S, s2 = 0.0;
+    for (uint32_t i = 0; i <= half; ++i) {
+      double a, b;
+      if (i == 0) { a = 2.0 * im[0]; s2 += (a - mean) * (a - mean); }
+      else if (i == half) { a = re[i] + im[i]; s2 += (a - mean) * (a - mean); }
+      else {
+        a = re[i] + im[S - i];
+        b = im[i] + re[S - i];
+        s2 += (a - mean) * (a - mean) + (b - mean) * (b - mean);
+      }
+    }
+    sigma = 0.5 * sqrt(s2 / (double)(S - 1));
+  }
+  double two_p = ldexp(1.0, (int)p_bits);
+  double sp = sigma * two_p;
+  *fail = !(log2(sp) <= (double)p_bits - 5.0);
+  double fl = 0.125 * sqrt((double)N);
+  if (sp < fl) sp = fl;
+  *stddev_p = sqrt(m_factor + 1.0) * sp;
+  *log_error = (int)rint(log2(*stddev_p * sqrt(2.0 * (double)S)));
+}
+
+/* (v + conj)/2 + nsd * z in place; z[2i], z[2i+1] = the (re, im) normals of slot i. */
+void or_decode_symmetrize(double* re, double* im, uint32_t S, const double* z, double nsd) {
+  uint32_t half = S / 2;
+  for (uint32_t i = 0; i <= half; ++i) {
+    if (i == 0) {
+      re[0] = re[0] + nsd * z[0];
+      im[0] = nsd * z[1];
+      if (S == 1) break;
+    } else if (i == half) {
+      double a = re[i], b = im[i];
+      re[i] = 0.5 * (a - b) + nsd * z[2 * i];
+      im[i] = 0.5 * (b - a) + nsd * z[2 * i + 1];
+    } else {
+      double xr = re[i], xi = im[i], yr = re[S - i], yi = im[S - i];
+      re[i] = 0.5 * (xr - yi) + nsd * z[2 * i];
+      im[i] = 0.5 * (xi - yr) + nsd * z[2 * i + 1];
+      re[S - i] = 0.5 * (yr - xi) + nsd * z[2 * (S - i)];
+      im[S - i] = 0.5 * (yi - xr) + nsd * z[2 * (S - i) + 1];
+    }
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -822,4 +898,59 @@ void or_sample_keygen(uint64_t seed, uint32_t N, uint32_t L, const uint64_t* q, 
     for (uint32_t j = 0; j < N; ++j) a_eval[(size_t)t * N + j] = uniform_mod(w[2 * j], w[2 * j + 1], q[t]);
   }
   free(w);
+}
+
+/* Decode-flooding normals of ciphertext g (product spec): pair index i in [0, S/2]
+ * draws ChaCha20 block (counter i, nonce (3 << 56) | g); words w0..w3 give two
+ * Box-Muller pairs (u1 = ((w >> 11) + 1) 2^-53, u2 = (w' >> 11) 2^-53,
+ * r = sqrt(-2 ln u1), (r cos 2 pi u2, r sin 2 pi u2)): slot i takes the first pair,
+ * slot S - i (0 < i < S/2) the second.  z[2i], z[2i+1] = (re, im) of slot i. */
+void or_flood_normals(uint64_t seed, uint64_t g, uint32_t S, double* z) {
+  uint32_t key[8], blk[16];
+  or_seed_to_key(seed, key);
+  uint32_t half = S / 2;
+  for (uint32_t i = 0; i <= half; ++i) {
+    or_chacha20_block(key, i, (3ull << 56) | g, blk);
+    double zz[4];
+    for (int pr = 0; pr < 2; ++pr) {
+      uint64_t a = (uint64_t)blk[4 * pr] | ((uint64_t)blk[4 * pr + 1] << 32);
+      uint64_t b = (uint64_t)blk[4 * pr + 2] | ((uint64_t)blk[4 * pr + 3] << 32);
+      double u1 = (double)((a >> 11) + 1) * 0x1.0p-53;
+      double u2 = (double)(b >> 11) * 0x1.0p-53;
+      double r = sqrt(-2.0 * log(u1));
+      zz[2 * pr] = r * cos(2.0 * M_PI * u2);
+      zz[2 * pr + 1] = r * sin(2.0 * M_PI * u2);
+    }
+    z[2 * i] = zz[0];
+    z[2 * i + 1] = zz[1];
+    if (i > 0 && i < half) {
+      z[2 * (S - i)] = zz[2];
+      z[2 * (S - i) + 1] = zz[3];
+    }
+    if (S == 1) break;
+  }
+}
+
+/* decrypt + flooded decode of one ciphertext (seeded stream, ciphertext index g). */
+int or_decrypt_flood(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
+                     const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
+                     uint32_t p_bits, double m_factor, uint64_t seed, uint64_t g, size_t n,
+                     double* out, int* log_error, int* fail) {
+  if (n > slots) return -1;
+  double* re = malloc(sizeof(double) * slots);
+  double* im = malloc(sizeof(double) * slots);
+  double* z = malloc(sizeof(double) * 2 * slots);
+  int rc = or_decrypt_coeffs(ct, sk, N, L, q, psi, slots, scale, re, im);
+  if (!rc) {
+    double sd;
+    or_decode_stats(re, im, slots, N, p_bits, m_factor, &sd, log_error, fail);
+    or_flood_normals(seed, g, slots, z);
+    or_decode_symmetrize(re, im, slots, z, sd / ldexp(1.0, (int)p_bits));
+    or_fft_special(re, im, slots);
+    for (size_t i = 0; i < n; ++i) out[i] = re[i];
+  }
+  free(z);
+  free(re);
+  free(im);
+  return rc;
 }

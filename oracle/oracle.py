@@ -47,6 +47,14 @@ def _load():
         "or_min_root": (C.c_uint64, [C.c_uint64, C.c_uint64]),
         "or_params_generate": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p]),
         "or_ntt_fwd": (None, [u64p, C.c_uint32, C.c_uint64, C.c_uint64]),
+        "or_decrypt_coeffs": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
+                                        C.c_double, f64p, f64p]),
+        "or_decode_stats": (None, [f64p, f64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, f64p,
+                                   C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "or_flood_normals": (None, [C.c_uint64, C.c_uint64, C.c_uint32, f64p]),
+        "or_decrypt_flood": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
+                                       C.c_double, C.c_uint32, C.c_double, C.c_uint64, C.c_uint64,
+                                       C.c_size_t, f64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "or_ntt_inv": (None, [u64p, C.c_uint32, C.c_uint64, C.c_uint64]),
         "or_fft_twiddles": (None, [C.c_uint32, f64p, f64p, f64p, f64p]),
         "or_fft_special_inv": (None, [f64p, f64p, C.c_uint32]),
@@ -329,3 +337,41 @@ def decrypt_vector(cts, sk, q, psi, slots: int, scale: float, n: int):
             break
         out[k * slots:k * slots + ln] = decrypt(cts[k], sk, q, psi, slots, scale, ln)
     return out
+
+
+# ------------------------------------------------- decode noise flooding ----
+def decrypt_coeffs(ct, sk, q, psi, slots: int, scale: float):
+    """Coefficient pairs (re_i, im_i) = (c[i gap], c[N/2 + i gap]) / scale of c0 + c1 s."""
+    ct, sk, q, psi = u64(ct), u64(sk), u64(q), u64(psi)
+    L, N = sk.shape
+    re, im = np.zeros(slots), np.zeros(slots)
+    rc = lib.or_decrypt_coeffs(_p(ct, u64p), _p(sk, u64p), N, L, _p(q, u64p), _p(psi, u64p), slots,
+                               float(scale), _p(re, f64p), _p(im, f64p))
+    if rc:
+        raise ValueError("decrypt failed rc=%d" % rc)
+    return re, im
+
+
+def decode_stats(re, im, N: int, p_bits: int = 52, m_factor: float = 1.0):
+    """PALISADE Decode's sigma estimate -> (stddev at scale 2^p, logError, fail)."""
+    re, im = (np.ascontiguousarray(a, dtype=np.float64) for a in (re, im))
+    sd, le, fail = C.c_double(), C.c_int(), C.c_int()
+    lib.or_decode_stats(_p(re, f64p), _p(im, f64p), len(re), N, p_bits, float(m_factor), C.byref(sd),
+                        C.byref(le), C.byref(fail))
+    return sd.value, le.value, bool(fail.value)
+
+
+def decrypt_flood(ct, sk, q, psi, slots: int, scale: float, n: int, seed: int, g: int,
+                  p_bits: int = 52, m_factor: float = 1.0):
+    """Flooded decrypt of one ciphertext with the product's seeded noise stream
+    -> (values, logError, fail)."""
+    ct, sk, q, psi = u64(ct), u64(sk), u64(q), u64(psi)
+    L, N = sk.shape
+    out = np.zeros(n)
+    le, fail = C.c_int(), C.c_int()
+    rc = lib.or_decrypt_flood(_p(ct, u64p), _p(sk, u64p), N, L, _p(q, u64p), _p(psi, u64p), slots,
+                              float(scale), p_bits, float(m_factor), seed, g, n, _p(out, f64p),
+                              C.byref(le), C.byref(fail))
+    if rc:
+        raise ValueError("decrypt failed rc=%d" % rc)
+    return out, le.value, bool(fail.value)

@@ -1,0 +1,77 @@
+"""§8(f3): PALISADE 1.11 decode noise flooding, restated in the oracle
+(or_decode_stats / or_decode_symmetrize / or_decrypt_flood).  The estimator and the
+thresholds are checked on synthetic coefficient pairs with a known error; the
+flooded decrypt of a real ciphertext under the reference keys stays within the
+added noise of the exact decode.  Normalisation constants of PALISADE's StdDev are
+restated, not pinned (PALISADE absent): parity with PALISADE is tolerance-level."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+P_BITS = 52
+
+
+def _pairs(S, N, sigma_p, rng, sym_scale=0.5):
+    """Coefficient pairs = a symmetric message part + an error with per-coefficient
+    stddev sigma_p (at scale 2^p), expressed in output units."""
+    # symmetric part: m(X) = m(X^-1) <=> re_i = -im_{S-i}, im_0 = 0, re_h = -im_h
+    re = rng.uniform(-sym_scale, sym_scale, S)
+    im = np.empty(S)
+    im[0] = 0.0
+    im[1:] = -re[1:][::-1]
+    h = S // 2
+    im[h] = -re[h]
+    e = rng.normal(0, sigma_p, (2, S)) / 2.0 ** P_BITS
+    return re + e[0], im + e[1]
+
+
+@pytest.mark.parametrize("S,N", [(4096, 8192), (16384, 32768), (1024, 8192)])
+def test_sigma_estimate_recovers_known_error(S, N):
+    rng = np.random.default_rng(S)
+    for sigma_p in (40.0, 3000.0, 2.0 ** 30):
+        re, im = _pairs(S, N, sigma_p, rng)
+        sd, le, fail = O.decode_stats(re, im, N, P_BITS, 1.0)
+        # u = v - conj has stddev sqrt(2) sigma_p; 0.5 sqrt(var) = sigma_p / sqrt(2)
+        est = sd / np.sqrt(2.0)
+        assert abs(est - sigma_p / np.sqrt(2.0)) / (sigma_p / np.sqrt(2.0)) < 0.05, (sigma_p, est)
+        assert not fail
+        assert le == int(np.rint(np.log2(sd * np.sqrt(2 * S))))
+
+
+def test_sigma_floor_and_precision_failure():
+    rng = np.random.default_rng(1)
+    S, N = 4096, 8192
+    re, im = _pairs(S, N, 0.0, rng)  # exact symmetric message: floor sqrt(N)/8
+    sd, le, fail = O.decode_stats(re, im, N, P_BITS, 1.0)
+    assert sd == pytest.approx(np.sqrt(2.0) * 0.125 * np.sqrt(N)) and not fail
+    re, im = _pairs(S, N, 2.0 ** 48, rng)  # ~4 bits of precision left -> PALISADE throws
+    assert O.decode_stats(re, im, N, P_BITS, 1.0)[2]
+    sd3, _, _ = O.decode_stats(*_pairs(S, N, 1000.0, rng), N, P_BITS, 3.0)
+    sd1, _, _ = O.decode_stats(*_pairs(S, N, 1000.0, np.random.default_rng(1)), N, P_BITS, 1.0)
+    assert sd3 / sd1 == pytest.approx(np.sqrt(4.0 / 2.0), rel=0.1)  # sqrt(M + 1)
+
+
+def test_flooded_decrypt_of_a_real_ciphertext(palisade_keys):
+    ctx, pk, sk = palisade_keys
+    q = np.array(ctx["q"], np.uint64)
+    psi = np.array(ctx["psi"], np.uint64)
+    N, S = ctx["N"], 4096
+    delta = float(int(q[-1]))
+    x = np.random.default_rng(2).uniform(-1, 1, S).astype(np.float32).astype(np.float64)
+    ct = O.encrypt_vector(x, pk, q, psi, N, S, delta, seed=11)[0]
+    exact = O.decrypt(ct, sk, q, psi, S, delta, S)
+    fl, le, fail = O.decrypt_flood(ct, sk, q, psi, S, delta, S, seed=11, g=5)
+    assert not fail
+    re, im = O.decrypt_coeffs(ct, sk, q, psi, S, delta)
+    sd, le2, _ = O.decode_stats(re, im, N, P_BITS, 1.0)
+    assert le == le2
+    # slot noise: real part of an S-term sum of iid N(0, nsd^2) pairs -> nsd sqrt(S)
+    nsd = sd / 2.0 ** P_BITS
+    d = fl - exact
+    assert np.std(d) == pytest.approx(nsd * np.sqrt(S), rel=0.1)
+    assert np.abs(d).max() < 8 * nsd * np.sqrt(S)
+    assert np.abs(fl - x).max() < 1e-9
+    # the seeded stream is reproducible, another ciphertext index draws other noise
+    assert np.array_equal(O.decrypt_flood(ct, sk, q, psi, S, delta, S, seed=11, g=5)[0], fl)
+    assert not np.array_equal(O.decrypt_flood(ct, sk, q, psi, S, delta, S, seed=11, g=6)[0], fl)
