@@ -58,12 +58,44 @@ def parse():
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the end-to-end check (decrypt of owned aggregate cts vs plain FedAvg)")
     ap.add_argument("--api-cts", type=int, default=64,
                     help="ciphertexts per learner for the bytes-API (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
                     help="PMC-derived HBM bytes per wavg launch (from tools/pmc_traffic.py)")
     return ap.parse_args()
+
+
+def check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8):
+    """Decrypt up to max_cts of the ciphertexts this rank owns and compare with plain
+    FedAvg of ALL learners (every rank regenerates any learner's slice from its seed:
+    PCG64 draws one 64-bit word per uniform double, so advance() skips to the slice)."""
+    import numpy as np
+
+    total = Cl * world
+    w32 = float(np.float32(1.0 / total))
+    err, n_checked = 0.0, 0
+    for a, b, share in owned:
+        b = min(b, a + max_cts - n_checked)
+        if b <= a:
+            break
+        lo, hi = a * batch, min(b * batch, params)
+        if hi <= lo:
+            continue
+        exp = np.zeros(hi - lo)
+        for i in range(total):
+            g = np.random.default_rng(1000 + i)
+            g.bit_generator.advance(lo)
+            exp += w32 * g.uniform(-1, 1, hi - lo).astype(np.float32).astype(np.float64)
+        dec = D.decrypt(ck, share[:b - a], hi - lo, delta * delta).cpu().numpy()
+        err = max(err, float(np.abs(dec - exp).max()))
+        n_checked += b - a
+    return {"max_abs_err": err, "cts_checked_per_rank": n_checked,
+            "what": "decrypt(aggregate) vs plain FedAvg of all %d learners" % total}
 
 
 def _median_rate(fn, units, seconds, parts=5):
@@ -161,8 +193,12 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
-    if world > 1:
+    distributed = world > 1 or args.force_dist
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import SHELFI_FHE as m
@@ -210,7 +246,7 @@ def main():
         del cts
         cts = None
     out = torch.empty((K, 2, L, N), dtype=torch.int64, device=dev)
-    comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev) if world > 1 else None
+    comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev) if distributed else None
 
     def piece(k0, k1, view):
         if args.layout == "arena":
@@ -225,15 +261,15 @@ def main():
             D.wavg(ck, cts, weights, out=out)
 
     def full_step():
-        if world == 1:
+        if not distributed:
             local_wavg()
-            return out
+            return [(0, K, out)]
         return comb.run(piece, lambda s: D.modq(ck, s))
 
     for _ in range(args.warmup):
         full_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -243,18 +279,18 @@ def main():
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if world == 1:
+        if not distributed:
             ev[i][0].record(stream)
             local_wavg()
             ev[i][1].record(stream)
         else:
             full_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:  # time the local kernel alone (same launches, outside the timed region)
+    if distributed:  # time the local kernel alone (same launches, outside the timed region)
         torch.cuda.synchronize()
         for i in range(args.steps):
             ev[i][0].record(stream)
@@ -264,7 +300,7 @@ def main():
     kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
@@ -272,7 +308,20 @@ def main():
     units = Cl * world * K  # client ciphertexts folded per step, whole job
     value = units / (elapsed / args.steps)
 
-    # correctness spot check of this rank's aggregate (decrypt one ciphertext) and
+    # end-to-end check of the job's result: this rank's owned aggregate ciphertexts
+    # (after the collective + modq at N>1) decrypt to plain FedAvg of every learner
+    check = None
+    if not args.no_check:
+        owned = full_step()
+        torch.cuda.synchronize()
+        check = check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8)
+        if distributed:
+            ce = torch.tensor([check["max_abs_err"]], dtype=torch.float64, device=dev)
+            dist.all_reduce(ce, op=dist.ReduceOp.MAX)
+            check["max_abs_err"] = ce.item()
+        if not check["max_abs_err"] < 1e-6:
+            raise SystemExit("end-to-end check failed: %r" % check)
+
     # device-resident decrypt+decode timing over the K aggregated ciphertexts
     local_wavg()
     torch.cuda.synchronize()
@@ -342,7 +391,7 @@ def main():
         "config": {"workload": "%s: %d learners/GPU x %s (%d params -> %d cts of %d slots), ring 2^%d, "
                                "L=%d towers%s" % (args.workload, Cl, model, params, K, batch,
                                                   N.bit_length() - 1, L,
-                                                  "" if world == 1 else
+                                                  "" if not distributed else
                                                   ", RCCL reduce_scatter overlapped in %d pieces" % args.pieces),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
                    "parallelism": "learner-sharded dp%d" % world, "layout": args.layout},
@@ -352,13 +401,15 @@ def main():
         "encrypt_hbm_frac": frac(enc_bytes, enc_ms),
         "decrypt_hbm_frac": frac(dec_bytes, dec_ms_per_ct),
     }
+    if check:
+        res["check"] = check
     if api:
         res["api_bytes_path"] = api
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, L, q, psi, delta, batch, Cl, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1,0 +1,50 @@
+"""bench.py end to end on the GPU (small cfg2 workload): the local N=1 step and the
+N>1 code path (NCCL process group, pipelined reduce_scatter, modq) run through
+torch.distributed.run with one rank; both must pass bench's own end-to-end check
+(decrypt of the owned aggregate ciphertexts vs plain FedAvg of every learner)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(args, timeout=300):
+    env = dict(os.environ)
+    p = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line)
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+COMMON = ["--workload", "cfg2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--api-cts", "4"]
+
+
+def test_bench_single_gpu_line():
+    r = _run([sys.executable, "bench.py"] + COMMON)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["steps"] == 3 and r["value"] > 0
+    assert r["roofline"]["bound"] == "hbm" and 0 < r["roofline"]["frac"] < 1
+    assert r["check"]["max_abs_err"] < 1e-8
+
+
+def test_bench_distributed_path_one_rank():
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
+              "--force-dist", "--pieces", "3"] + COMMON)
+    assert "reduce_scatter" in r["config"]["workload"]
+    assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
