@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
     ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
-    ap.add_argument("--pieces", type=int, default=4,
+    ap.add_argument("--pieces", type=int, default=8,
                     help="N>1: ciphertext pieces whose RCCL reduce_scatter overlaps the next piece's wavg")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
