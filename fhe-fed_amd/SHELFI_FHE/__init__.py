@@ -127,6 +127,16 @@ class CKKS(Scheme):
     def set_seed(self, seed: int) -> None:
         check(self._lib.shelfi_set_seed(self._ctx, int(seed)))
 
+    def set_wire_format(self, fmt: str = "palisade") -> None:
+        """Bytes format of encrypt's output: "palisade" = the reference's own cereal
+        archive of vector<Ciphertext<DCRTPoly>> (ckks.cpp:98-100; needs keys loaded from
+        the reference's PALISADE files), "shelfi" = this library's blob (default).
+        computeWeightedAverage and decrypt accept both and computeWeightedAverage
+        answers in its inputs' format."""
+        if fmt not in ("palisade", "shelfi"):
+            raise ValueError("wire format must be 'palisade' or 'shelfi'")
+        check(self._lib.shelfi_set_wire_format(self._ctx, 1 if fmt == "palisade" else 0), "set_wire_format")
+
     def set_decode_noise(self, enabled: bool = True, m_factor: float = 1.0) -> None:
         """PALISADE 1.11's decode noise flooding (CKKSPackedEncoding::Decode): Gaussian
         noise of stddev sqrt(m_factor + 1) * max(sigma, sqrt(N)/8) at scale 2^p, where
@@ -290,3 +300,66 @@ def blob_residues(blob: bytes, ring_dim: int, num_towers: int) -> np.ndarray:
     hdr = _lib.load().shelfi_blob_header_bytes()
     arr = np.frombuffer(blob, dtype="<u8", offset=hdr)
     return arr.reshape(-1, 2, num_towers, ring_dim)
+
+
+# ------------------------------------------------ PALISADE wire format (f1) --
+def palisade_parse(archive: bytes, residues: bool = True):
+    """Parse a PALISADE 1.11 archive of vector<Ciphertext<DCRTPoly>> (or a single
+    Ciphertext).  Returns (info dict, residues [K][2][L][N] uint64 or None)."""
+    lib = _lib.load()
+    b = bytes(archive)
+    inf = _lib.PalisadeInfo()
+    check(lib.shelfi_palisade_parse(b, len(b), C.byref(inf), None), "palisade_parse")
+    d = {"ring_dim": inf.ring_dim, "num_towers": inf.num_towers, "num_cts": inf.num_cts,
+         "moduli": [int(inf.moduli[t]) for t in range(inf.num_towers)], "depth": inf.depth,
+         "level": inf.level, "scale": inf.scale, "encoding": inf.encoding,
+         "vector_archive": bool(inf.vector_archive), "ctx_offset": inf.ctx_offset,
+         "ctx_length": inf.ctx_length, "keytag": inf.keytag.decode()}
+    if not residues:
+        return d, None
+    r = np.empty((inf.num_cts, 2, inf.num_towers, inf.ring_dim), np.uint64)
+    check(lib.shelfi_palisade_parse(b, len(b), C.byref(inf), r.ctypes.data_as(_lib.u64p)),
+          "palisade_parse")
+    return d, r
+
+
+def _take_lib_bytes(lib, out, n) -> bytes:
+    try:
+        return C.string_at(out, n)
+    finally:
+        lib.shelfi_free(out)
+
+
+def palisade_write(ctx_obj: bytes, keytag: str, moduli, residues: np.ndarray, depth: int = 1,
+                   level: int = 0, scale: float = 0.0, vector_archive: bool = True) -> bytes:
+    """Write residues [K][2][L][N] as a PALISADE archive around an embedded context
+    object (palisade_key_context) and key tag."""
+    lib = _lib.load()
+    r = np.ascontiguousarray(residues, dtype=np.uint64)
+    K, two, L, N = r.shape
+    q = np.ascontiguousarray(moduli, dtype=np.uint64)
+    out, n = _lib.u8p(), C.c_size_t()
+    ob = bytes(ctx_obj)
+    check(lib.shelfi_palisade_write(ob, len(ob), keytag.encode(), N, L, q.ctypes.data_as(_lib.u64p), K,
+                                    r.ctypes.data_as(_lib.u64p), int(depth), int(level), float(scale),
+                                    1 if vector_archive else 0, C.byref(out), C.byref(n)), "palisade_write")
+    return _take_lib_bytes(lib, out, n.value)
+
+
+def palisade_key_context(key_public: bytes):
+    """(embedded context object, key tag) of a PALISADE key-public.txt."""
+    lib = _lib.load()
+    b = bytes(key_public)
+    out, n = _lib.u8p(), C.c_size_t()
+    tag = C.create_string_buffer(257)
+    check(lib.shelfi_palisade_key_context(b, len(b), C.byref(out), C.byref(n), tag), "palisade_key_context")
+    return _take_lib_bytes(lib, out, n.value), tag.value.decode()
+
+
+def palisade_embed_context(ctxfile: bytes) -> bytes:
+    """A cryptocontext.txt's context object as key/ciphertext archives embed it."""
+    lib = _lib.load()
+    b = bytes(ctxfile)
+    out, n = _lib.u8p(), C.c_size_t()
+    check(lib.shelfi_palisade_embed_context(b, len(b), C.byref(out), C.byref(n)), "palisade_embed_context")
+    return _take_lib_bytes(lib, out, n.value)

@@ -46,6 +46,23 @@ class Info(C.Structure):
     ]
 
 
+class PalisadeInfo(C.Structure):
+    _fields_ = [
+        ("ring_dim", C.c_uint32),
+        ("num_towers", C.c_uint32),
+        ("num_cts", C.c_uint64),
+        ("moduli", C.c_uint64 * MAX_TOWERS),
+        ("depth", C.c_uint64),
+        ("level", C.c_uint64),
+        ("scale", C.c_double),
+        ("encoding", C.c_uint32),
+        ("vector_archive", C.c_int32),
+        ("ctx_offset", C.c_uint64),
+        ("ctx_length", C.c_uint64),
+        ("keytag", C.c_char * 257),
+    ]
+
+
 # name -> (restype, argtypes); every symbol declared in include/shelfi.h
 SIGNATURES = {
     "shelfi_abi_version": (C.c_int, []),
@@ -65,6 +82,15 @@ SIGNATURES = {
     "shelfi_set_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_get_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_encrypt": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_set_wire_format": (C.c_int, [C.c_void_p, C.c_int]),
+    "shelfi_palisade_parse": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(PalisadeInfo), u64p]),
+    "shelfi_palisade_write": (C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_uint32, C.c_uint32, u64p,
+                                        C.c_uint64, u64p, C.c_uint64, C.c_uint64, C.c_double, C.c_int,
+                                        C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_palisade_key_context": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                              C.c_char_p]),
+    "shelfi_palisade_embed_context": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(u8p),
+                                                C.POINTER(C.c_size_t)]),
     "shelfi_set_decode_noise": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
     "shelfi_decode_log_error": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "shelfi_encrypt_into": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.c_void_p, C.c_size_t,

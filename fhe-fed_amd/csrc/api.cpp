@@ -20,6 +20,7 @@
 #include <new>
 
 #include "host_stage.h"
+#include "palisade_codec.h"
 #include "palisade_io.h"
 #include "shelfi_internal.h"
 
@@ -338,6 +339,11 @@ static void install_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk
   ctx->key_id = fnv1a(pk, sizeof(uint64_t) * 2 * LN, ctx->params_id);
   ctx->keys_loaded = true;
   ctx->palisade_keys = palisade;
+  if (!palisade) {  // PALISADE wire format needs the PALISADE context + key tag
+    ctx->pal_ctx_obj.clear();
+    ctx->pal_keytag.clear();
+    ctx->wire = 0;
+  }
 }
 
 static void require_keys(const shelfi_ctx* ctx) {
@@ -655,11 +661,101 @@ int shelfi_load(shelfi_ctx* ctx, const char* cryptodir) {
       set_params(ctx, N, L, ctx->p.scale_bits, ctx->p.first_mod_bits, batch, pc.q.data(),
                  pc.psi.data());
       std::vector<uint64_t> pk, sk;
-      palisade_read_keys(read_file(dir + "key-public.txt"), read_file(dir + "key-private.txt"),
-                         N, pc.q, pk, sk);
+      const std::string pub = read_file(dir + "key-public.txt");
+      palisade_read_keys(pub, read_file(dir + "key-private.txt"), N, pc.q, pk, sk);
+      std::string ctx_obj, keytag;
+      palisade_key_context(pub, ctx_obj, keytag);  // for PALISADE-format output (§8 f1)
       install_keys(ctx, pk.data(), sk.data(), true);
+      ctx->pal_ctx_obj = std::move(ctx_obj);
+      ctx->pal_keytag = std::move(keytag);
     }
   });
+}
+
+static BlobHeader make_header(const shelfi_ctx* ctx, uint64_t K, uint32_t depth, double scale);
+
+// Where the residues of a bytes-API ciphertext batch live in host memory: a library
+// blob (one contiguous payload) or a PALISADE archive (2*L tower runs per ciphertext,
+// palisade_codec.h).  Both map onto the device layout [K][2][L][N].
+struct CtLayout {
+  uint8_t* base = nullptr;
+  bool pal = false;
+  uint64_t K = 0;
+  uint32_t depth = 0;
+  uint64_t level = 0;
+  double scale = 0.0;
+  std::vector<size_t> off;  // PALISADE tower offsets [K][2][L]
+  void pieces(uint64_t k0, uint64_t kn, const Params& p, std::vector<HostPiece>& out) const {
+    out.clear();
+    const size_t ct_bytes = 2ull * p.L * p.N * 8;
+    if (!pal) {
+      out.push_back(HostPiece{base + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes});
+      return;
+    }
+    for (uint64_t i = k0 * 2 * p.L; i < (k0 + kn) * 2 * p.L; ++i)
+      out.push_back(HostPiece{base + off[i], (size_t)p.N * 8});
+  }
+};
+
+// A caller's ciphertext batch, validated against the context (params and key).
+static CtLayout open_cts(const shelfi_ctx* ctx, const uint8_t* b, size_t len) {
+  CtLayout v;
+  v.base = const_cast<uint8_t*>(b);
+  if (b && palisade_looks_like_archive(b, len)) {
+    PalisadeArchive A = palisade_parse_archive(b, len);
+    v.pal = true;
+    v.K = A.K;
+    if (A.K) {
+      const Params& p = ctx->p;
+      bool same = A.N == p.N && A.L == p.L;
+      for (uint32_t t = 0; same && t < p.L; ++t) same = A.q[t] == p.q[t];
+      if (!same)
+        throw Error{SHELFI_ERR_FORMAT, "PALISADE ciphertexts were produced under different crypto parameters"};
+      if (ctx->pal_keytag.empty() || A.keytag != ctx->pal_keytag)
+        throw Error{SHELFI_ERR_FORMAT, "PALISADE ciphertexts were encrypted under a different key (keyTag)"};
+      if (A.encoding != 4) throw Error{SHELFI_ERR_FORMAT, "PALISADE ciphertexts are not CKKS-packed"};
+    }
+    v.depth = (uint32_t)A.depth;
+    v.level = A.level;
+    v.scale = A.scale;
+    v.off = std::move(A.tower_off);
+    return v;
+  }
+  BlobHeader h = parse_blob(b, len, ctx);
+  v.K = h.K;
+  v.depth = h.depth;
+  v.level = h.level;
+  v.scale = h.scale;
+  if (v.K && h.key_id != ctx->key_id)
+    throw Error{SHELFI_ERR_FORMAT, "ciphertext was encrypted under a different key"};
+  return v;
+}
+
+// Size of (and, with buf, the header / framing of) an output batch in the ctx's
+// format; returns its layout.
+static CtLayout make_output(const shelfi_ctx* ctx, bool pal, uint64_t K, uint32_t depth,
+                            uint64_t level, double scale, uint8_t* buf, size_t* total) {
+  CtLayout v;
+  v.base = buf;
+  v.pal = pal;
+  v.K = K;
+  v.depth = depth;
+  v.level = level;
+  v.scale = scale;
+  const Params& p = ctx->p;
+  if (pal) {
+    if (ctx->pal_ctx_obj.empty())
+      throw Error{SHELFI_ERR_STATE, "PALISADE wire format needs keys loaded from PALISADE files"};
+    v.off = palisade_layout(ctx->pal_ctx_obj, ctx->pal_keytag, p.N, p.L, p.q, K, depth, level, scale,
+                            4, true, buf, total);
+    return v;
+  }
+  *total = sizeof(BlobHeader) + K * 2ull * p.L * p.N * 8;
+  if (buf) {
+    const BlobHeader h = make_header(ctx, K, depth, scale);
+    std::memcpy(buf, &h, sizeof(h));
+  }
+  return v;
 }
 
 // ------------------------------------------------------------- bytes API ----
@@ -738,7 +834,7 @@ struct StageRun {
 
 // encode + encrypt n doubles (host) -> K ciphertext payloads written to out_payload.
 static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, uint64_t K,
-                                   uint8_t* out_payload) {
+                                   const CtLayout& dst) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   uint32_t key[8];
@@ -753,6 +849,7 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
   void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc));
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
+  std::vector<HostPiece> pcs;
   SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, pp.b));
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
@@ -768,7 +865,8 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
                    g0 + k0, ctx->dev_flag, pp.b);
     SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
     SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
-    sr.s.d2h(out_payload + k0 * ct_bytes, cb[b], kn * ct_bytes, pp.c);
+    dst.pieces(k0, kn, p, pcs);
+    sr.s.d2hv(pcs.data(), pcs.size(), cb[b], pp.c);
     SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
     sr.s.poll();
   }
@@ -791,14 +889,14 @@ int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     const uint64_t K = (n + p.batch - 1) / p.batch;  // ckks.cpp:65
-    const size_t total = sizeof(BlobHeader) + K * 2ull * p.L * p.N * 8;
+    size_t total = 0;
+    make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, nullptr, &total);
     *out_len = total;
     if (!out) return;
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
-    const BlobHeader h = make_header(ctx, K, 1, p.delta);
     advise_huge(out, total);
-    std::memcpy(out, &h, sizeof(h));
-    if (K) encrypt_bytes_pipeline(ctx, x, n, K, out + sizeof(BlobHeader));
+    const CtLayout dst = make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, out, &total);
+    if (K) encrypt_bytes_pipeline(ctx, x, n, K, dst);
   });
 }
 
@@ -825,30 +923,31 @@ int shelfi_encrypt(shelfi_ctx* ctx, const double* x, size_t n, uint8_t** out, si
 
 // Validates the learners' blobs (same params, key, K, depth, scale) and returns the
 // header of the result (depth + 1, scale * Delta: EvalMult by a constant, no rescale).
-static BlobHeader wavg_check(const shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
-                             size_t C) {
+// Validates the learners' batches (same format, params, key, K, depth, scale).
+static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* const* blobs,
+                                         const size_t* lens, size_t C) {
   if (C == 0) throw Error{SHELFI_ERR_ARG, "computeWeightedAverage: no learners"};
-  BlobHeader h0 = parse_blob(blobs[0], lens[0], ctx);
-  for (size_t c = 1; c < C; ++c) {
-    BlobHeader h = parse_blob(blobs[c], lens[c], ctx);
+  std::vector<CtLayout> in;
+  in.reserve(C);
+  for (size_t c = 0; c < C; ++c) {
+    in.push_back(open_cts(ctx, blobs[c], lens[c]));
+    const CtLayout& h = in.back();
+    const CtLayout& h0 = in.front();
+    if (h.pal != h0.pal)
+      throw Error{SHELFI_ERR_FORMAT, "learners mix PALISADE archives and library blobs"};
     if (h.K != h0.K)
       throw Error{SHELFI_ERR_FORMAT, "learners hold different numbers of ciphertexts"};
-    if (h.key_id != h0.key_id)
-      throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts were encrypted under different keys"};
-    if (h.depth != h0.depth || h.scale != h0.scale)
+    if (h.depth != h0.depth || h.scale != h0.scale || h.level != h0.level)
       throw Error{SHELFI_ERR_FORMAT, "learners' ciphertexts have different depth/scale"};
   }
-  BlobHeader ho = h0;
-  ho.depth = h0.depth + 1;
-  ho.scale = h0.scale * ctx->p.delta;
-  return ho;
+  return in;
 }
 
 // Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
 // chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
 // (stream B), with two device buffer sets.  Writes the payload of the result.
-static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, const float* weights,
-                                size_t C, uint64_t K, uint8_t* out_payload) {
+static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in,
+                                const float* weights, size_t C, uint64_t K, const CtLayout& dst) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   // chunk: ~64 MiB of input per learner-group buffer, at least 1 ciphertext
@@ -862,6 +961,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
   // A: staged H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
+  std::vector<HostPiece> pcs;
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
@@ -869,9 +969,10 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
     for (size_t c0 = 0; c0 < C; c0 += group) {
       const size_t gc = std::min(group, C - c0);
       if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
-      for (size_t c = 0; c < gc; ++c)
-        sr.s.h2d(inb[b] + c * kn * ct_bytes, blobs[c0 + c] + sizeof(BlobHeader) + k0 * ct_bytes,
-                 kn * ct_bytes, pp.a);
+      for (size_t c = 0; c < gc; ++c) {
+        in[c0 + c].pieces(k0, kn, p, pcs);
+        sr.s.h2dv(inb[b] + c * kn * ct_bytes, pcs.data(), pcs.size(), pp.a);
+      }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2 && c0 == 0) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
@@ -889,7 +990,8 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       if (c0 + gc >= C) {
         SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
-        sr.s.d2h(out_payload + k0 * ct_bytes, outb[b], kn * ct_bytes, pp.c);
+        dst.pieces(k0, kn, p, pcs);
+        sr.s.d2hv(pcs.data(), pcs.size(), outb[b], pp.c);
         SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
       }
       sr.s.poll();
@@ -899,30 +1001,6 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const uint8_t* const* blobs, co
   pp.sync();
 }
 
-int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
-                            const float* weights, size_t C, uint8_t** out, size_t* out_len) {
-  if (!ctx || !out || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
-  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
-  *out = nullptr;
-  *out_len = 0;
-  return guarded([&] {
-    DeviceGuard g(ctx->device);
-    const BlobHeader ho = wavg_check(ctx, blobs, lens, C);
-    const size_t total = sizeof(BlobHeader) + ho.K * 2ull * ctx->p.L * ctx->p.N * 8;
-    uint8_t* blob = (uint8_t*)std::malloc(total);
-    if (!blob) throw std::bad_alloc();
-    std::memcpy(blob, &ho, sizeof(ho));
-    try {
-      if (ho.K) wavg_bytes_pipeline(ctx, blobs, weights, C, ho.K, blob + sizeof(BlobHeader));
-    } catch (...) {
-      std::free(blob);
-      throw;
-    }
-    *out = blob;
-    *out_len = total;
-  });
-}
-
 int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
                                  const float* weights, size_t C, uint8_t* out, size_t out_cap,
                                  size_t* out_len) {
@@ -930,15 +1008,43 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     DeviceGuard g(ctx->device);
-    const BlobHeader ho = wavg_check(ctx, blobs, lens, C);
-    const size_t total = sizeof(BlobHeader) + ho.K * 2ull * ctx->p.L * ctx->p.N * 8;
+    const std::vector<CtLayout> in = wavg_inputs(ctx, blobs, lens, C);
+    const CtLayout& h0 = in.front();
+    // EvalMult by a constant (ckks.cpp:288): depth + 1, scale * Delta, same level
+    const uint32_t depth = h0.depth + 1;
+    const double scale = h0.scale * ctx->p.delta;
+    size_t total = 0;
+    make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, nullptr, &total);
     *out_len = total;
     if (!out) return;  // size query
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     advise_huge(out, total);
-    std::memcpy(out, &ho, sizeof(ho));
-    if (ho.K) wavg_bytes_pipeline(ctx, blobs, weights, C, ho.K, out + sizeof(BlobHeader));
+    const CtLayout dst = make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, out, &total);
+    if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst);
   });
+}
+
+int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,
+                            const float* weights, size_t C, uint8_t** out, size_t* out_len) {
+  if (!ctx || !out || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  *out_len = 0;
+  size_t total = 0;
+  int rc = shelfi_weighted_average_into(ctx, blobs, lens, weights, C, nullptr, 0, &total);
+  if (rc) return rc;
+  uint8_t* buf = (uint8_t*)std::malloc(total ? total : 1);
+  if (!buf) {
+    set_error("host out of memory");
+    return SHELFI_ERR_DEVICE;
+  }
+  rc = shelfi_weighted_average_into(ctx, blobs, lens, weights, C, buf, total, &total);
+  if (rc) {
+    std::free(buf);
+    return rc;
+  }
+  *out = buf;
+  *out_len = total;
+  return SHELFI_OK;
 }
 
 // Noise-flooding setup for one decrypt of K ciphertexts (enabled by
@@ -991,9 +1097,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     require_keys(ctx);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
-    BlobHeader h = parse_blob(blob, len, ctx);
-    if (h.key_id != ctx->key_id)
-      throw Error{SHELFI_ERR_FORMAT, "ciphertext was encrypted under a different key"};
+    const CtLayout h = open_cts(ctx, blob, len);
     if (n > h.K * (uint64_t)p.batch)
       throw Error{SHELFI_ERR_ARG, "decrypt: data_dimensions exceeds the slots in the ciphertexts"};
     if (!n) return;
@@ -1011,13 +1115,15 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     StageRun sr(stager(ctx));
     advise_huge(out, n * 8);
     DecodeNoise dn = decode_noise_begin(ctx, K, pp.b);
+    std::vector<HostPiece> pcs;
     const uint64_t nchunks = (K + kc - 1) / kc;
     for (uint64_t ci = 0; ci < nchunks; ++ci) {
       const int b = (int)(ci & 1);
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
-      sr.s.h2d(cb[b], blob + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes, pp.a);
+      h.pieces(k0, kn, p, pcs);
+      sr.s.h2dv(cb[b], pcs.data(), pcs.size(), pp.a);
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
@@ -1231,3 +1337,95 @@ int shelfi_gauss_cdt(double sigma, uint64_t* cdt, int max_entries) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------- PALISADE wire format ----
+int shelfi_set_wire_format(shelfi_ctx* ctx, int format) {
+  if (!ctx || (format != 0 && format != 1)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    if (format == 1 && ctx->pal_ctx_obj.empty())
+      throw Error{SHELFI_ERR_STATE, "PALISADE wire format needs keys loaded from PALISADE files"};
+    ctx->wire = format;
+  });
+}
+
+int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
+                          uint64_t* residues) {
+  if (!archive || !info) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    const PalisadeArchive A = palisade_parse_archive(archive, len);
+    std::memset(info, 0, sizeof(*info));
+    info->ring_dim = A.N;
+    info->num_towers = A.L;
+    info->num_cts = A.K;
+    for (uint32_t t = 0; t < A.L; ++t) info->moduli[t] = A.q[t];
+    info->depth = A.depth;
+    info->level = A.level;
+    info->scale = A.scale;
+    info->encoding = A.encoding;
+    info->vector_archive = A.vector_archive ? 1 : 0;
+    info->ctx_offset = A.ctx_off;
+    info->ctx_length = A.ctx_len;
+    std::memcpy(info->keytag, A.keytag.data(), std::min<size_t>(A.keytag.size(), 256));
+    if (residues)
+      for (size_t i = 0; i < A.tower_off.size(); ++i)
+        std::memcpy(residues + i * (size_t)A.N, archive + A.tower_off[i], (size_t)A.N * 8);
+  });
+}
+
+int shelfi_palisade_write(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
+                          uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
+                          uint64_t num_cts, const uint64_t* residues, uint64_t depth, uint64_t level,
+                          double scale, int vector_archive, uint8_t** out, size_t* out_len) {
+  if (!ctx_obj || !keytag || !moduli || !out || !out_len || (num_cts && !residues) ||
+      num_towers < 1 || num_towers > (uint32_t)kMaxTowers)
+    return SHELFI_ERR_ARG;
+  *out = nullptr;
+  *out_len = 0;
+  return guarded([&] {
+    const std::string obj((const char*)ctx_obj, ctx_len), tag(keytag);
+    size_t total = 0;
+    palisade_layout(obj, tag, ring_dim, num_towers, moduli, num_cts, depth, level, scale, 4,
+                    vector_archive != 0, nullptr, &total);
+    uint8_t* buf = (uint8_t*)std::malloc(total);
+    if (!buf) throw std::bad_alloc();
+    const std::vector<size_t> off = palisade_layout(obj, tag, ring_dim, num_towers, moduli, num_cts,
+                                                    depth, level, scale, 4, vector_archive != 0,
+                                                    buf, &total);
+    for (size_t i = 0; i < off.size(); ++i)
+      std::memcpy(buf + off[i], residues + i * (size_t)ring_dim, (size_t)ring_dim * 8);
+    *out = buf;
+    *out_len = total;
+  });
+}
+
+int shelfi_palisade_key_context(const uint8_t* pub, size_t len, uint8_t** ctx_obj, size_t* ctx_len,
+                                char* keytag) {
+  if (!pub || !ctx_obj || !ctx_len || !keytag) return SHELFI_ERR_ARG;
+  *ctx_obj = nullptr;
+  return guarded([&] {
+    std::string obj, tag;
+    palisade_key_context(std::string((const char*)pub, len), obj, tag);
+    uint8_t* buf = (uint8_t*)std::malloc(obj.size());
+    if (!buf) throw std::bad_alloc();
+    std::memcpy(buf, obj.data(), obj.size());
+    *ctx_obj = buf;
+    *ctx_len = obj.size();
+    std::memset(keytag, 0, 257);
+    std::memcpy(keytag, tag.data(), std::min<size_t>(tag.size(), 256));
+  });
+}
+
+int shelfi_palisade_embed_context(const uint8_t* ctxfile, size_t len, uint8_t** out,
+                                  size_t* out_len) {
+  if (!ctxfile || !out || !out_len) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    const std::string obj = palisade_embed_context(std::string((const char*)ctxfile, len));
+    uint8_t* buf = (uint8_t*)std::malloc(obj.size());
+    if (!buf) throw std::bad_alloc();
+    std::memcpy(buf, obj.data(), obj.size());
+    *out = buf;
+    *out_len = obj.size();
+  });
+}

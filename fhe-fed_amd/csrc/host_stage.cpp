@@ -46,30 +46,31 @@ CopyPool::~CopyPool() {
   for (auto& t : workers_) t.join();
 }
 
-// Share `id` of the current job: page-aligned pieces so first-touch faults of a fresh
-// destination land on different threads.
-static void piece(uint8_t* dst, const uint8_t* src, size_t n, int id, int parts) {
-  const size_t per = ((n / parts) + 4095) & ~size_t(4095);
-  const size_t a = std::min(n, per * (size_t)id), b = std::min(n, per * (size_t)(id + 1));
-  if (b > a) std::memcpy(dst + a, src + a, b - a);
+// Share `id` of the current list: bytes [id T/P, (id+1) T/P) of the concatenated
+// jobs, page-aligned so first-touch faults of a fresh destination land on different
+// threads.
+void CopyPool::share(int id) {
+  const size_t per = ((total_ / parts_) + 4095) & ~size_t(4095);
+  const size_t a = std::min(total_, per * (size_t)id), b = std::min(total_, per * (size_t)(id + 1));
+  size_t base = 0;
+  for (size_t j = 0; j < njobs_ && base < b; ++j) {
+    const CopyJob& J = jobs_[j];
+    const size_t lo = std::max(a, base), hi = std::min(b, base + J.n);
+    if (hi > lo) std::memcpy(J.dst + (lo - base), J.src + (lo - base), hi - lo);
+    base += J.n;
+  }
 }
 
 void CopyPool::run(int id) {
   uint64_t seen = 0;
   for (;;) {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_go_.wait(lk, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
       seen = gen_;
-      dst = dst_;
-      src = src_;
-      n = n_;
     }
-    piece(dst, src, n, id, threads());
+    share(id);
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (--pending_ == 0) cv_done_.notify_one();
@@ -77,24 +78,31 @@ void CopyPool::run(int id) {
   }
 }
 
-void CopyPool::copy(void* dst, const void* src, size_t n) {
-  if (n == 0) return;
-  if (workers_.empty() || n < (512u << 10)) {
-    std::memcpy(dst, src, n);
+void CopyPool::copy_many(const CopyJob* jobs, size_t njobs) {
+  size_t total = 0;
+  for (size_t j = 0; j < njobs; ++j) total += jobs[j].n;
+  if (total == 0) return;
+  if (workers_.empty() || total < (512u << 10)) {
+    for (size_t j = 0; j < njobs; ++j) std::memcpy(jobs[j].dst, jobs[j].src, jobs[j].n);
     return;
   }
   {
     std::lock_guard<std::mutex> lk(mu_);
-    dst_ = (uint8_t*)dst;
-    src_ = (const uint8_t*)src;
-    n_ = n;
+    jobs_ = jobs;
+    njobs_ = njobs;
+    total_ = total;
     pending_ = (int)workers_.size();
     ++gen_;
   }
   cv_go_.notify_all();
-  piece((uint8_t*)dst, (const uint8_t*)src, n, 0, threads());
+  share(0);
   std::unique_lock<std::mutex> lk(mu_);
   cv_done_.wait(lk, [&] { return pending_ == 0; });
+}
+
+void CopyPool::copy(void* dst, const void* src, size_t n) {
+  const CopyJob j{(uint8_t*)dst, (const uint8_t*)src, n};
+  copy_many(&j, 1);
 }
 
 // --------------------------------------------------------------- Stager ----
@@ -137,8 +145,9 @@ bool Stager::drain_front(bool block) {
     if (e != hipSuccess)
       throw Error{SHELFI_ERR_DEVICE, std::string("staged copy: ") + hipGetErrorString(e)};
   }
-  pool_.copy(s.dst, s.host, s.len);
-  s.dst = nullptr;
+  pool_.copy_many(s.out_jobs.data(), s.out_jobs.size());
+  s.out_jobs.clear();
+  s.pending = false;
   pending_.pop_front();
   return true;
 }
@@ -160,41 +169,71 @@ void Stager::wait_in_slot(Slot& sl) {
   }
 }
 
-void Stager::h2d(void* dev, const void* host, size_t n, hipStream_t s) {
-  const uint8_t* src = (const uint8_t*)host;
+void Stager::h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s) {
   uint8_t* dst = (uint8_t*)dev;
-  while (n) {
-    const size_t len = std::min(n, slot_bytes_);
+  size_t pi = 0, po = 0;  // current piece, offset inside it
+  std::vector<CopyJob> jobs;
+  while (pi < np) {
     Slot& sl = in_[in_next_++ % in_.size()];
     wait_in_slot(sl);
-    pool_.copy(sl.host, src, len);
-    SHELFI_HIP(hipMemcpyAsync(dst, sl.host, len, hipMemcpyHostToDevice, s));
+    size_t fill = 0;
+    jobs.clear();
+    while (pi < np && fill < slot_bytes_) {
+      const size_t take = std::min(pieces[pi].n - po, slot_bytes_ - fill);
+      if (take) jobs.push_back(CopyJob{sl.host + fill, pieces[pi].p + po, take});
+      fill += take;
+      po += take;
+      if (po == pieces[pi].n) {
+        ++pi;
+        po = 0;
+      }
+    }
+    if (!fill) break;
+    pool_.copy_many(jobs.data(), jobs.size());
+    SHELFI_HIP(hipMemcpyAsync(dst, sl.host, fill, hipMemcpyHostToDevice, s));
     SHELFI_HIP(hipEventRecord(sl.ev, s));
     sl.used = true;
-    src += len;
-    dst += len;
-    n -= len;
+    dst += fill;
+  }
+}
+
+void Stager::h2d(void* dev, const void* host, size_t n, hipStream_t s) {
+  const HostPiece p{(uint8_t*)host, n};
+  h2dv(dev, &p, 1, s);
+}
+
+void Stager::d2hv(const HostPiece* pieces, size_t np, const void* dev, hipStream_t s) {
+  const uint8_t* src = (const uint8_t*)dev;
+  size_t pi = 0, po = 0;
+  while (pi < np) {
+    const size_t idx = out_next_++ % out_.size();
+    Slot& sl = out_[idx];
+    while (sl.pending) drain_front(true);  // FIFO: the oldest pending is drained first
+    size_t fill = 0;
+    sl.out_jobs.clear();
+    while (pi < np && fill < slot_bytes_) {
+      const size_t take = std::min(pieces[pi].n - po, slot_bytes_ - fill);
+      if (take) sl.out_jobs.push_back(CopyJob{pieces[pi].p + po, sl.host + fill, take});
+      fill += take;
+      po += take;
+      if (po == pieces[pi].n) {
+        ++pi;
+        po = 0;
+      }
+    }
+    if (!fill) break;
+    SHELFI_HIP(hipMemcpyAsync(sl.host, src, fill, hipMemcpyDeviceToHost, s));
+    SHELFI_HIP(hipEventRecord(sl.ev, s));
+    sl.used = true;
+    sl.pending = true;
+    pending_.push_back(idx);
+    src += fill;
   }
 }
 
 void Stager::d2h(void* host, const void* dev, size_t n, hipStream_t s) {
-  uint8_t* dst = (uint8_t*)host;
-  const uint8_t* src = (const uint8_t*)dev;
-  while (n) {
-    const size_t len = std::min(n, slot_bytes_);
-    const size_t idx = out_next_++ % out_.size();
-    Slot& sl = out_[idx];
-    while (sl.dst) drain_front(true);  // FIFO: the oldest pending is drained first
-    SHELFI_HIP(hipMemcpyAsync(sl.host, src, len, hipMemcpyDeviceToHost, s));
-    SHELFI_HIP(hipEventRecord(sl.ev, s));
-    sl.used = true;
-    sl.dst = dst;
-    sl.len = len;
-    pending_.push_back(idx);
-    dst += len;
-    src += len;
-    n -= len;
-  }
+  const HostPiece p{(uint8_t*)host, n};
+  d2hv(&p, 1, dev, s);
 }
 
 void Stager::finish() {
@@ -208,7 +247,8 @@ void Stager::abort() noexcept {
   for (auto* ring : {&in_, &out_})
     for (Slot& sl : *ring) {
       if (sl.used) (void)hipEventSynchronize(sl.ev);
-      sl.dst = nullptr;
+      sl.pending = false;
+      sl.out_jobs.clear();
     }
   pending_.clear();
 }

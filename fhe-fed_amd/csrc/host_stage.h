@@ -22,7 +22,15 @@
 
 namespace shelfi {
 
-// Persistent workers splitting one memcpy at a time (the caller takes a share too).
+// One memcpy of a scatter/gather list.
+struct CopyJob {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t n;
+};
+
+// Persistent workers splitting one copy list at a time (the caller takes a share
+// too): the list is treated as one byte stream cut into page-aligned shares.
 class CopyPool {
  public:
   explicit CopyPool(int threads);
@@ -30,10 +38,12 @@ class CopyPool {
   CopyPool(const CopyPool&) = delete;
   CopyPool& operator=(const CopyPool&) = delete;
   void copy(void* dst, const void* src, size_t n);
+  void copy_many(const CopyJob* jobs, size_t njobs);
   int threads() const { return parts_; }
 
  private:
   void run(int id);
+  void share(int id);
   int parts_ = 1;  // set before the workers start
   std::vector<std::thread> workers_;
   std::mutex mu_;
@@ -41,9 +51,14 @@ class CopyPool {
   uint64_t gen_ = 0;
   int pending_ = 0;
   bool stop_ = false;
-  uint8_t* dst_ = nullptr;
-  const uint8_t* src_ = nullptr;
-  size_t n_ = 0;
+  const CopyJob* jobs_ = nullptr;
+  size_t njobs_ = 0, total_ = 0;
+};
+
+// A host range of a scatter/gather transfer.
+struct HostPiece {
+  uint8_t* p;
+  size_t n;
 };
 
 class Stager {
@@ -60,6 +75,11 @@ class Stager {
   // Enqueue device -> host of n bytes on `s`.  `host` is written later, by poll() /
   // finish() (or when its slot is needed again); it must stay valid until finish().
   void d2h(void* host, const void* dev, size_t n, hipStream_t s);
+  // Gather: the pieces, in order, land contiguously at `dev`.
+  void h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s);
+  // Scatter: contiguous device bytes at `dev` go to the pieces, in order (written
+  // later, like d2h).
+  void d2hv(const HostPiece* pieces, size_t np, const void* dev, hipStream_t s);
   // Drain every output slot whose DMA has completed (non-blocking).
   void poll();
   // Drain all outputs and wait for all inputs.  Must be called before the host
@@ -75,9 +95,9 @@ class Stager {
   struct Slot {
     uint8_t* host = nullptr;
     hipEvent_t ev = nullptr;
-    bool used = false;      // an event has been recorded
-    uint8_t* dst = nullptr;  // pending output destination (d2h slots)
-    size_t len = 0;
+    bool used = false;             // an event has been recorded
+    bool pending = false;          // output waiting to be drained (d2h slots)
+    std::vector<CopyJob> out_jobs;  // where a pending output goes
   };
   bool drain_front(bool block);
   void wait_in_slot(Slot& sl);

@@ -115,6 +115,9 @@ struct shelfi_ctx {
   int decode_noise = 0;          // shelfi_set_decode_noise
   double decode_m_factor = 1.0;
   int last_log_error = -1;       // of the last flooded decrypt, -1 if none
+  std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)
+  std::string pal_keytag;        // PALISADE keys: key tag
+  int wire = 0;                  // encrypt output: 0 blob, 1 PALISADE archive
   // scratch arena (grown on demand, never shrunk)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;

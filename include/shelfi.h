@@ -132,6 +132,42 @@ int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t n
 /* Offset of the residue payload inside a blob (64-byte header). */
 size_t shelfi_blob_header_bytes(void);
 
+/* ---- PALISADE 1.11 wire format -------------- */
+/* The reference's bytes are cereal PortableBinary archives of
+ * vector<Ciphertext<DCRTPoly>> (ckks.cpp:98-100, :281, :308-310).  With keys loaded from
+ * the reference's PALISADE files, shelfi_set_wire_format(ctx, 1) makes encrypt produce
+ * such archives; computeWeightedAverage and decrypt accept archives and blobs alike,
+ * and computeWeightedAverage answers in its inputs' format. */
+typedef struct {
+  uint32_t ring_dim, num_towers;
+  uint64_t num_cts;
+  uint64_t moduli[16];
+  uint64_t depth, level;
+  double scale;
+  uint32_t encoding;      /* 4 = CKKSPacked */
+  int32_t vector_archive; /* 0: a single Ciphertext (e.g. mkhe's CT1.txt) */
+  uint64_t ctx_offset, ctx_length; /* the embedded context object inside the archive */
+  char keytag[257];
+} shelfi_palisade_info;
+int shelfi_set_wire_format(shelfi_ctx* ctx, int format); /* 0 blob (default), 1 PALISADE */
+/* Host-only: parse an archive; residues [K][2][L][N] copied out when non-NULL. */
+int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
+                          uint64_t* residues);
+/* Host-only: write an archive (free with shelfi_free) from residues [K][2][L][N] and an
+ * embedded context object (shared-pointer ids from 3: shelfi_palisade_key_context). */
+int shelfi_palisade_write(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
+                          uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
+                          uint64_t num_cts, const uint64_t* residues, uint64_t depth, uint64_t level,
+                          double scale, int vector_archive, uint8_t** out, size_t* out_len);
+/* Host-only: the embedded context object (free with shelfi_free) and key tag of a
+ * PALISADE key-public.txt (ckks.cpp:48). */
+int shelfi_palisade_key_context(const uint8_t* pub, size_t len, uint8_t** ctx_obj, size_t* ctx_len,
+                                char keytag[257]);
+/* Host-only: a cryptocontext.txt's context object re-embedded one shared-pointer id
+ * later (what key and ciphertext archives hold). */
+int shelfi_palisade_embed_context(const uint8_t* ctxfile, size_t len, uint8_t** out,
+                                  size_t* out_len);
+
 /* ---- device-resident batch API (HBM in, HBM out; `stream` = hipStream_t) ---- */
 /* Ciphertext batches are [K][2][L][N] uint64 in HBM (same order as the blob
  * payload).  Work is enqueued on `stream` exactly as given (NULL = the legacy
