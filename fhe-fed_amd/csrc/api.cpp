@@ -895,8 +895,11 @@ int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out
     if (!out) return;
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     advise_huge(out, total);
-    const CtLayout dst = make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, out, &total);
+    // residues first (the parallel drains first-touch the fresh pages), framing after
+    CtLayout dst = make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, nullptr, &total);
+    dst.base = out;
     if (K) encrypt_bytes_pipeline(ctx, x, n, K, dst);
+    make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, out, &total);
   });
 }
 
@@ -1019,8 +1022,11 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     if (!out) return;  // size query
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     advise_huge(out, total);
-    const CtLayout dst = make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, out, &total);
+    // residues first (the parallel drains first-touch the fresh pages), framing after
+    CtLayout dst = make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, nullptr, &total);
+    dst.base = out;
     if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst);
+    make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, out, &total);
   });
 }
 

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--rate", type=float, default=0.1)
     ap.add_argument("--layers", default="")
     ap.add_argument("--pack", action="store_true")
+    ap.add_argument("--wire", choices=["shelfi", "palisade"], default="shelfi",
+                    help="bytes format of the ciphertexts (palisade = the reference's own archives)")
     a = ap.parse_args()
     shapes = {"lenet5": F.lenet5_shapes(), "resnet18": F.resnet_shapes(18),
               "resnet50": F.resnet_shapes(50)}[a.model]
@@ -44,6 +46,8 @@ def main():
         ck.loadCryptoParams()  # benchmark.py:481 (the reference's own keys)
     else:
         ck.genCryptoContextAndKeyGen()
+    if a.wire == "palisade":
+        ck.set_wire_format("palisade")
     t_init = time.time() - t0
     sel = F.Selection(a.select, rate=a.rate, layers=[int(x) for x in a.layers.split(",") if x])
     run = F.SecureFedAvg(ck, sel, pack=a.pack)
