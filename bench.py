@@ -55,6 +55,11 @@ def parse():
     ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--pieces", type=int, default=8,
                     help="N>1: ciphertext pieces whose RCCL reduce_scatter overlaps the next piece's wavg")
+    ap.add_argument("--shard", choices=["learners", "cts"], default="learners",
+                    help="N>1: learners = each rank aggregates its own learners, one RCCL reduce_scatter "
+                         "combines the partial sums (BASELINE config 3); cts = each rank aggregates every "
+                         "learner's slice of the ciphertexts (no collective; the host routes each upload's "
+                         "ciphertext ranges to their ranks)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,12 +226,25 @@ def main():
     delta = inf["delta"]
     dev = torch.device("cuda", local)
 
-    # synthetic learners: global learner i = rank + world * j gets
-    # default_rng(1000 + i).uniform(-1, 1, n) through float32, encrypted on device
+    # synthetic learners: learner i's vector is
+    # default_rng(1000 + i).uniform(-1, 1, n) through float32, encrypted on device.
+    # learners shard: rank r holds learners i = r + world * j, all K ciphertexts;
+    # cts shard: rank r holds every learner's ciphertexts [k_lo, k_hi)
+    cts_mode = distributed and args.shard == "cts"
+    if cts_mode:
+        k_lo, k_hi = SD.ct_slices(K, world)[rank]
+        mine = list(range(Cl * world))
+    else:
+        k_lo, k_hi = 0, K
+        mine = [rank + world * j for j in range(Cl)]
+    K_loc = k_hi - k_lo
+    C_loc = len(mine)
     cts, enc_times = [], []
-    for j in range(Cl):
-        i = rank + world * j
-        xh = np.random.default_rng(1000 + i).uniform(-1, 1, params).astype(np.float32)
+    for i in mine:
+        lo, hi = k_lo * batch, min(k_hi * batch, params)
+        g = np.random.default_rng(1000 + i)
+        g.bit_generator.advance(lo)
+        xh = g.uniform(-1, 1, hi - lo).astype(np.float32)
         x = torch.from_numpy(xh).to(dev).double()
         del xh
         torch.cuda.synchronize()
@@ -235,18 +253,19 @@ def main():
         torch.cuda.synchronize()
         enc_times.append(time.perf_counter() - t0)
         del x
-    weights = [1.0 / (Cl * world)] * Cl
+    weights = [1.0 / (Cl * world)] * C_loc
     # the aggregator's resident layout: learners interleaved in one arena (placed once,
     # before the timed region)
-    arena = D.Arena(ck, Cl, K, device=dev)
+    arena = D.Arena(ck, C_loc, K_loc, device=dev)
     for i, ct in enumerate(cts):
         arena.put(i, ct)
     torch.cuda.synchronize()
     if args.layout == "arena":
         del cts
         cts = None
-    out = torch.empty((K, 2, L, N), dtype=torch.int64, device=dev)
-    comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev) if distributed else None
+    out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
+    comb = (SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
+            if distributed and not cts_mode else None)
 
     def piece(k0, k1, view):
         if args.layout == "arena":
@@ -261,9 +280,9 @@ def main():
             D.wavg(ck, cts, weights, out=out)
 
     def full_step():
-        if not distributed:
+        if comb is None:
             local_wavg()
-            return [(0, K, out)]
+            return [(k_lo, k_hi, out)]
         return comb.run(piece, lambda s: D.modq(ck, s))
 
     for _ in range(args.warmup):
@@ -279,7 +298,7 @@ def main():
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if not distributed:
+        if comb is None:
             ev[i][0].record(stream)
             local_wavg()
             ev[i][1].record(stream)
@@ -290,7 +309,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if distributed:  # time the local kernel alone (same launches, outside the timed region)
+    if comb is not None:  # time the local kernel alone (same launches, outside the timed region)
         torch.cuda.synchronize()
         for i in range(args.steps):
             ev[i][0].record(stream)
@@ -305,7 +324,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     ms_per_step = elapsed * 1e3 / args.steps
-    units = Cl * world * K  # client ciphertexts folded per step, whole job
+    units = Cl * world * K  # client ciphertexts folded per step, whole job (either shard)
     value = units / (elapsed / args.steps)
 
     # end-to-end check of the job's result: this rank's owned aggregate ciphertexts
@@ -326,16 +345,16 @@ def main():
     local_wavg()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dec = D.decrypt(ck, out, K * batch, delta * delta)
+    dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
     torch.cuda.synchronize()
-    dec_ms_per_ct = (time.perf_counter() - t0) * 1e3 / K
+    dec_ms_per_ct = (time.perf_counter() - t0) * 1e3 / K_loc
     assert torch.isfinite(dec).all().item()
     del dec
 
     # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`
     api = None
     if args.api_cts > 0 and rank == 0:
-        Ka = min(K, args.api_cts)
+        Ka = min(K_loc, args.api_cts)
         if args.layout == "arena":
             src = [out[:Ka].clone() for _ in range(Cl)]  # any valid ciphertexts of this key
         else:
@@ -356,13 +375,13 @@ def main():
         del blobs, res_blob
 
     # roofline of the dominant kernel: algorithmic bytes = (C + 1) * K * 2 * L * N * 8
-    bytes_per_launch = (Cl + 1) * K * 2 * L * N * 8
+    bytes_per_launch = (C_loc + 1) * K_loc * 2 * L * N * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == args.workload and tj.get("learners") == Cl:
+        if tj.get("workload") == args.workload and tj.get("learners") == C_loc and K_loc == K:
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -373,7 +392,7 @@ def main():
     # encrypt / decrypt per ciphertext: SURVEY §8(d) algorithmic bytes (f64 slots + ct,
     # keys amortized) over the measured time; these are VALU-bound (NTT), the HBM
     # fraction says how far from the memory bound they run
-    enc_ms = 1e3 * sorted(enc_times)[len(enc_times) // 2] / K
+    enc_ms = 1e3 * sorted(enc_times)[len(enc_times) // 2] / K_loc
     ct_bytes = 16 * L * N
     enc_bytes = 8 * batch + ct_bytes + ct_bytes / K
     dec_bytes = ct_bytes + 8 * L * N / K + 8 * batch
@@ -392,9 +411,12 @@ def main():
                                "L=%d towers%s" % (args.workload, Cl, model, params, K, batch,
                                                   N.bit_length() - 1, L,
                                                   "" if not distributed else
+                                                  (", ciphertext-sharded: each rank aggregates all %d learners' "
+                                                   "cts [k0, k1), no collective" % (Cl * world)) if cts_mode else
                                                   ", RCCL reduce_scatter overlapped in %d pieces" % args.pieces),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
-                   "parallelism": "learner-sharded dp%d" % world, "layout": args.layout},
+                   "parallelism": ("ciphertext-sharded dp%d" if cts_mode else "learner-sharded dp%d") % world,
+                   "layout": args.layout},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(enc_ms, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),

@@ -393,6 +393,40 @@ static void fill_weights(WavgArgs& a, const Params& p, const float* w, size_t n)
   }
 }
 
+// Weight limbs [C][L][2] of wavg_arena_many in a device buffer: a ring of slots, the
+// last one reused while the weights repeat (every step of a round), a slot rewritten
+// only after the kernels that read it have completed.
+static int arena_weight_slot(shelfi_ctx* ctx, const float* w, size_t C, hipStream_t s) {
+  const Params& p = ctx->p;
+  std::vector<uint32_t> wl(C * p.L * 2);
+  for (size_t c = 0; c < C; ++c) {
+    const int64_t W = (int64_t)((double)w[c] * p.delta + 0.5);  // ckks.cpp:287-288
+    for (uint32_t t = 0; t < p.L; ++t) {
+      const uint64_t wt = mod_signed(W, p.q[t]);
+      wl[(c * p.L + t) * 2] = (uint32_t)(wt & ((1u << 30) - 1));
+      wl[(c * p.L + t) * 2 + 1] = (uint32_t)(wt >> 30);
+    }
+  }
+  const int last = ctx->wl_last_slot;
+  if (last >= 0 && ctx->wl_host[last] == wl) return last;
+  const int i = ctx->wl_next;
+  ctx->wl_next = (i + 1) % shelfi_ctx::kWeightRing;
+  if (ctx->wl_done[i]) SHELFI_HIP(hipEventSynchronize(ctx->wl_done[i]));
+  else SHELFI_HIP(hipEventCreateWithFlags(&ctx->wl_done[i], hipEventDisableTiming));
+  const size_t bytes = wl.size() * sizeof(uint32_t);
+  if (ctx->wl_cap[i] < bytes) {
+    if (ctx->wl_dev[i]) (void)hipFree(ctx->wl_dev[i]);
+    ctx->wl_dev[i] = nullptr;
+    ctx->wl_cap[i] = 0;
+    SHELFI_HIP(hipMalloc(&ctx->wl_dev[i], bytes));
+    ctx->wl_cap[i] = bytes;
+  }
+  ctx->wl_host[i] = std::move(wl);  // stays alive until the slot is reused
+  SHELFI_HIP(hipMemcpyAsync(ctx->wl_dev[i], ctx->wl_host[i].data(), bytes, hipMemcpyHostToDevice, s));
+  ctx->wl_last_slot = i;
+  return i;
+}
+
 }  // namespace shelfi
 
 // ============================================================== C ABI ======
@@ -494,6 +528,11 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     free_tables(ctx);
     delete ctx->stage;
     ctx->stage = nullptr;
+    for (int i = 0; i < shelfi_ctx::kWeightRing; ++i) {
+      if (ctx->wl_done[i]) (void)hipEventSynchronize(ctx->wl_done[i]);
+      if (ctx->wl_done[i]) (void)hipEventDestroy(ctx->wl_done[i]);
+      if (ctx->wl_dev[i]) (void)hipFree(ctx->wl_dev[i]);
+    }
     dfree(ctx->scratch);
     dfree(ctx->io);
     dfree_t(ctx->dev_flag);
@@ -1230,6 +1269,14 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
+    if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners
+      std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+      const int slot = arena_weight_slot(ctx, w, C, (hipStream_t)stream);
+      launch_wavg_arena_many(arena_dev, ctx->wl_dev[slot], (uint32_t)C, (uint64_t)K * 2 * p.L, p.L,
+                             p.logN, ctx->dt.tc, out_dev, (hipStream_t)stream);
+      SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], (hipStream_t)stream));
+      return;
+    }
     for (size_t c0 = 0; c0 < C; c0 += kWavgMaxLearners) {
       const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
       WavgArgs a;

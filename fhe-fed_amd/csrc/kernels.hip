@@ -204,6 +204,64 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(a.out + e));
 }
 
+// Arena aggregation of any number of learners in one pass: groups of up to 16
+// learners accumulate carry-free as above, each group is folded and mod-added into a
+// running sum, and the output is written once (no read-modify-write per group).
+// Weight limbs come from a device buffer wl[C][L][2] (block-uniform scalar loads).
+__global__ __launch_bounds__(kWavgThreads) void wavg_arena_many(const uint64_t* __restrict__ arena,
+                                                                const uint32_t* __restrict__ wl,
+                                                                uint32_t C, uint32_t L,
+                                                                uint32_t logN,
+                                                                const TowerConst* __restrict__ tcs,
+                                                                uint64_t* __restrict__ out) {
+  const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
+  const uint32_t t = (uint32_t)((base >> logN) % L);
+  const TowerConst c = tcs[t];
+  const uint32_t M30 = (1u << 30) - 1;
+  const uint64_t* __restrict__ src = arena + (uint64_t)blockIdx.x * C * kWavgPerBlock + 2u * threadIdx.x;
+  uint64_t r0 = 0, r1 = 0;
+  for (uint32_t k0 = 0; k0 < C; k0 += kWavgMaxLearners) {
+    const uint32_t k1 = min(C, k0 + (uint32_t)kWavgMaxLearners);
+    uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
+    uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
+#pragma unroll 8
+    for (uint32_t k = k0; k < k1; ++k) {
+      const uint32_t w0 = wl[(k * L + t) * 2], w1 = wl[(k * L + t) * 2 + 1];
+      const u32x4 v = __builtin_nontemporal_load(
+          reinterpret_cast<const u32x4*>(src + (uint64_t)k * kWavgPerBlock));
+      const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
+      const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
+      s00a += (uint64_t)xa0 * w0;
+      s01a += (uint64_t)xa0 * w1;
+      s10a += (uint64_t)xa1 * w0;
+      s11a += (uint64_t)xa1 * w1;
+      s00b += (uint64_t)xb0 * w0;
+      s01b += (uint64_t)xb0 * w1;
+      s10b += (uint64_t)xb1 * w0;
+      s11b += (uint64_t)xb1 * w1;
+    }
+    r0 = addmod(r0, wavg_fold(s00a, s01a, s10a, s11a, c), c.q);
+    r1 = addmod(r1, wavg_fold(s00b, s01b, s10b, s11b, c), c.q);
+  }
+  u32x4 o;
+  o.x = (uint32_t)r0;
+  o.y = (uint32_t)(r0 >> 32);
+  o.z = (uint32_t)r1;
+  o.w = (uint32_t)(r1 >> 32);
+  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + base + 2u * threadIdx.x));
+}
+
+void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,
+                            uint32_t L, uint32_t logN, const TowerConst* tc, uint64_t* out,
+                            hipStream_t s) {
+  const uint64_t blocks = (rows << logN) / kWavgPerBlock;
+  if (!blocks) return;
+  if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  hipLaunchKernelGGL(wavg_arena_many, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, arena, wl_dev,
+                     C, L, logN, tc, out);
+  SHELFI_HIP(hipGetLastError());
+}
+
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t total = a.rows << a.logN;
   const uint64_t blocks = total / kWavgPerBlock;

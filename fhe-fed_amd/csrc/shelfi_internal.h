@@ -118,6 +118,13 @@ struct shelfi_ctx {
   std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)
   std::string pal_keytag;        // PALISADE keys: key tag
   int wire = 0;                  // encrypt output: 0 blob, 1 PALISADE archive
+  // device weight-limb buffers of wavg_arena_many (ring; reused while weights repeat)
+  static constexpr int kWeightRing = 8;
+  uint32_t* wl_dev[kWeightRing] = {};
+  size_t wl_cap[kWeightRing] = {};
+  hipEvent_t wl_done[kWeightRing] = {};
+  std::vector<uint32_t> wl_host[kWeightRing];
+  int wl_next = 0, wl_last_slot = -1;
   // scratch arena (grown on demand, never shrunk)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -140,6 +147,9 @@ struct WavgArgs {
   uint32_t arena_learners, first_learner;          // arena width, first learner of this pass
 };
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
+void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,
+                            uint32_t L, uint32_t logN, const TowerConst* tc, uint64_t* out,
+                            hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,

@@ -48,3 +48,11 @@ def test_bench_distributed_path_one_rank():
               "--force-dist", "--pieces", "3"] + COMMON)
     assert "reduce_scatter" in r["config"]["workload"]
     assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
+
+
+def test_bench_ciphertext_sharded_path_one_rank():
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
+              "--force-dist", "--shard", "cts"] + COMMON)
+    assert r["config"]["parallelism"] == "ciphertext-sharded dp1"
+    assert r["check"]["max_abs_err"] < 1e-8

@@ -136,7 +136,7 @@ def test_wavg_device_bitexact(cfg, C, K, request):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("C,K", [(16, 3), (20, 2), (1, 1), (5, 4)])
+@pytest.mark.parametrize("C,K", [(16, 3), (20, 2), (1, 1), (5, 4), (40, 1), (128, 1)])
 def test_wavg_arena_bitexact(cfg2, C, K):
     """Learner-interleaved arena (device and host-blob placement) == oracle."""
     inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
@@ -158,6 +158,29 @@ def test_wavg_arena_bitexact(cfg2, C, K):
     got = ar.wavg(w)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+
+
+def test_wavg_arena_many_learners_ranges_and_weights(cfg2):
+    """> 16 learners in one pass (wavg_arena_many): sub-ranges of the arena, alternating
+    weight vectors (the device weight ring), residues at q-1 with weight 1.0."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    L, C, K = len(q), 48, 3
+    rng = np.random.default_rng(123)
+    cts = []
+    for c in range(C):
+        a = np.empty((K, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = (int(q[t]) - 1) if c < 16 else rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+        cts.append(a)
+    ar = D.Arena(cfg2, C, K)
+    for c in range(C):
+        ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
+    wa = [1.0] * 16 + list(rng.dirichlet(np.ones(C - 16)))
+    wb = list(rng.uniform(-1, 1, C))
+    for w in (wa, wb, wa, wb):
+        got = ar.wavg(w, k0=1, k1=3)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg([c[1:3] for c in cts], w, q, delta))
 
 
 def test_wavg_extremes(cfg2):
