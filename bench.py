@@ -3,9 +3,14 @@
 
 A *step* is one encrypted FedAvg aggregation over one batch of synthetic input: every
 learner's ciphertexts (already resident in HBM) are scaled by its float32 weight and
-summed (ckks.cpp:264-320, EvalMult + EvalAdd) by the wavg kernel.  With N GPUs the
-learners are sharded round-robin (16 per GPU, weak scaling) and the partial sums are
-combined by one RCCL reduce_scatter over xGMI + the modq kernel (SHELFI_FHE/dist.py).
+summed (ckks.cpp:264-320, EvalMult + EvalAdd) by the wavg kernel.  At N > 1 GPUs
+(weak scaling, 16 learners' worth of work per GPU) the default partitioning is by
+ciphertext index: rank r aggregates every learner's ciphertexts [k0, k1) with no
+collective (the aggregator routes each upload's ciphertext ranges to their GPU).  The
+learner-sharded alternative (BASELINE config 3's wording: each rank aggregates its own
+learners, one RCCL reduce_scatter over xGMI + modq combines the partial sums,
+SHELFI_FHE/dist.py) is measured in the same run and reported beside it
+(`alternative_partitioning`; --shard learners makes it the headline).
 
 Workload (default): BASELINE config 3's per-GPU shard — 16 learners x ResNet-18
 (11,689,512 params -> 714 ciphertexts of 16384 slots), ring 2^15, L = 4 towers;
@@ -55,7 +60,7 @@ def parse():
     ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--pieces", type=int, default=8,
                     help="N>1: ciphertext pieces whose RCCL reduce_scatter overlaps the next piece's wavg")
-    ap.add_argument("--shard", choices=["learners", "cts"], default="learners",
+    ap.add_argument("--shard", choices=["learners", "cts"], default="cts",
                     help="N>1: learners = each rank aggregates its own learners, one RCCL reduce_scatter "
                          "combines the partial sums (BASELINE config 3); cts = each rank aggregates every "
                          "learner's slice of the ciphertexts (no collective; the host routes each upload's "
@@ -65,6 +70,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N>1: skip measuring the other partitioning in the same run")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the end-to-end check (decrypt of owned aggregate cts vs plain FedAvg)")
     ap.add_argument("--api-cts", type=int, default=64,
@@ -187,6 +194,11 @@ def cpu_baseline(N, L, q, psi, delta, slots, C, seconds):
 
 def main():
     args = parse()
+    # exactly one line on stdout: libraries (RCCL prints a version banner) write to fd 1,
+    # so fd 1 becomes stderr for the run and the JSON line goes to the saved stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -225,121 +237,147 @@ def main():
     psi = np.array(inf["roots"], np.uint64)
     delta = inf["delta"]
     dev = torch.device("cuda", local)
+    weight = 1.0 / (Cl * world)
 
-    # synthetic learners: learner i's vector is
-    # default_rng(1000 + i).uniform(-1, 1, n) through float32, encrypted on device.
-    # learners shard: rank r holds learners i = r + world * j, all K ciphertexts;
-    # cts shard: rank r holds every learner's ciphertexts [k_lo, k_hi)
-    cts_mode = distributed and args.shard == "cts"
-    if cts_mode:
-        k_lo, k_hi = SD.ct_slices(K, world)[rank]
-        mine = list(range(Cl * world))
-    else:
-        k_lo, k_hi = 0, K
-        mine = [rank + world * j for j in range(Cl)]
-    K_loc = k_hi - k_lo
-    C_loc = len(mine)
-    cts, enc_times = [], []
-    for i in mine:
-        lo, hi = k_lo * batch, min(k_hi * batch, params)
-        g = np.random.default_rng(1000 + i)
-        g.bit_generator.advance(lo)
-        xh = g.uniform(-1, 1, hi - lo).astype(np.float32)
-        x = torch.from_numpy(xh).to(dev).double()
-        del xh
+    def build(shard):
+        """Resident inputs + step of one partitioning.  Learner i's vector
+        is default_rng(1000 + i).uniform(-1, 1, n) through float32,
+        encrypted on device and placed in an arena before any timing.
+          local:    N = 1, all learners, all K ciphertexts;
+          learners: rank r holds learners r + world*j, all K cts; partial sums combined by
+                    the pipelined RCCL reduce_scatter + modq (BASELINE config 3's wording);
+          cts:      rank r holds every learner's cts [k_lo, k_hi); no collective."""
+        if shard == "cts":
+            k_lo, k_hi = SD.ct_slices(K, world)[rank]
+            mine = list(range(Cl * world))
+        else:
+            k_lo, k_hi = 0, K
+            mine = [rank + world * j for j in range(Cl)]
+        K_loc, C_loc = k_hi - k_lo, len(mine)
+        cts, enc_times = [], []
+        for i in mine:
+            lo, hi = k_lo * batch, min(k_hi * batch, params)
+            g = np.random.default_rng(1000 + i)
+            g.bit_generator.advance(lo)
+            xh = g.uniform(-1, 1, hi - lo).astype(np.float32)
+            x = torch.from_numpy(xh).to(dev).double()
+            del xh
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            cts.append(D.encrypt(ck, x))
+            torch.cuda.synchronize()
+            enc_times.append(time.perf_counter() - t0)
+            del x
+        weights = [weight] * C_loc
+        # the aggregator's resident layout: learners interleaved in one arena
+        arena = D.Arena(ck, C_loc, K_loc, device=dev)
+        for i, ct in enumerate(cts):
+            arena.put(i, ct)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        cts.append(D.encrypt(ck, x))
-        torch.cuda.synchronize()
-        enc_times.append(time.perf_counter() - t0)
-        del x
-    weights = [1.0 / (Cl * world)] * C_loc
-    # the aggregator's resident layout: learners interleaved in one arena (placed once,
-    # before the timed region)
-    arena = D.Arena(ck, C_loc, K_loc, device=dev)
-    for i, ct in enumerate(cts):
-        arena.put(i, ct)
-    torch.cuda.synchronize()
-    if args.layout == "arena":
-        del cts
-        cts = None
-    out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
-    comb = (SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
-            if distributed and not cts_mode else None)
-
-    def piece(k0, k1, view):
         if args.layout == "arena":
-            arena.wavg(weights, out=view, k0=k0, k1=k1)
-        else:
-            D.wavg(ck, [c[k0:k1] for c in cts], weights, out=view)
+            cts = None
+        out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
+        comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev) if shard == "learners" else None
 
-    def local_wavg():
-        if args.layout == "arena":
-            arena.wavg(weights, out=out)
-        else:
-            D.wavg(ck, cts, weights, out=out)
+        def kernel():
+            if args.layout == "arena":
+                arena.wavg(weights, out=out)
+            else:
+                D.wavg(ck, cts, weights, out=out)
 
-    def full_step():
-        if comb is None:
-            local_wavg()
-            return [(k_lo, k_hi, out)]
-        return comb.run(piece, lambda s: D.modq(ck, s))
+        def piece(k0, k1, view):
+            if args.layout == "arena":
+                arena.wavg(weights, out=view, k0=k0, k1=k1)
+            else:
+                D.wavg(ck, [c[k0:k1] for c in cts], weights, out=view)
 
-    for _ in range(args.warmup):
-        full_step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
+        def step():
+            if comb is None:
+                kernel()
+                return [(k_lo, k_hi, out)]
+            return comb.run(piece, lambda s_: D.modq(ck, s_))
 
-    # timed region: exactly `steps` steps; per-launch wavg events on the launch stream
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if comb is None:
-            ev[i][0].record(stream)
-            local_wavg()
-            ev[i][1].record(stream)
-        else:
-            full_step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if comb is not None:  # time the local kernel alone (same launches, outside the timed region)
+        return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
+                "enc_times": enc_times, "kernel": kernel, "step": step, "comb": comb, "weights": weights,
+                "cts": cts}
+
+    def timed(mode):
+        """warmup, then exactly `steps` steps between barrier + sync; max over ranks.
+        Per-launch wavg events on the launch stream (torch's current stream)."""
+        for _ in range(args.warmup):
+            mode["step"]()
         torch.cuda.synchronize()
-        for i in range(args.steps):
-            ev[i][0].record(stream)
-            local_wavg()
-            ev[i][1].record(stream)
-        torch.cuda.synchronize()
-    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
-
-    if distributed:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    ms_per_step = elapsed * 1e3 / args.steps
-    units = Cl * world * K  # client ciphertexts folded per step, whole job (either shard)
-    value = units / (elapsed / args.steps)
-
-    # end-to-end check of the job's result: this rank's owned aggregate ciphertexts
-    # (after the collective + modq at N>1) decrypt to plain FedAvg of every learner
-    check = None
-    if not args.no_check:
-        owned = full_step()
-        torch.cuda.synchronize()
-        check = check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8)
         if distributed:
-            ce = torch.tensor([check["max_abs_err"]], dtype=torch.float64, device=dev)
+            dist.barrier()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            if mode["comb"] is None:
+                ev[i][0].record(stream)
+                mode["kernel"]()
+                ev[i][1].record(stream)
+            else:
+                mode["step"]()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if mode["comb"] is not None:  # the local kernel alone, outside the timed region
+            for i in range(args.steps):
+                ev[i][0].record(stream)
+                mode["kernel"]()
+                ev[i][1].record(stream)
+            torch.cuda.synchronize()
+        if distributed:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = tt.item()
+        return elapsed, sorted(a.elapsed_time(b) for a, b in ev)
+
+    def checked(mode):
+        """End to end: this rank's owned aggregate cts (after the collective + modq in
+        the learners shard) decrypt to plain FedAvg of every learner (max over ranks)."""
+        owned = mode["step"]()
+        torch.cuda.synchronize()
+        c = check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8)
+        if distributed:
+            ce = torch.tensor([c["max_abs_err"]], dtype=torch.float64, device=dev)
             dist.all_reduce(ce, op=dist.ReduceOp.MAX)
-            check["max_abs_err"] = ce.item()
-        if not check["max_abs_err"] < 1e-6:
-            raise SystemExit("end-to-end check failed: %r" % check)
+            c["max_abs_err"] = ce.item()
+        if not c["max_abs_err"] < 1e-6:
+            raise SystemExit("end-to-end check failed (%s): %r" % (mode["shard"], c))
+        return c
+
+    units = Cl * world * K  # client ciphertexts folded per step, whole job (any shard)
+    main_mode = build(args.shard if distributed else "local")
+    elapsed, kern_ms = timed(main_mode)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = units / (elapsed / args.steps)
+    check = None if args.no_check else checked(main_mode)
+    # the other N > 1 partitioning, measured in the same run on the same inputs
+    alt = None
+    if distributed and not args.no_alt:
+        alt_mode = build("learners" if args.shard == "cts" else "cts")
+        a_el, a_k = timed(alt_mode)
+        alt = {"parallelism": ("ciphertext-sharded dp%d (no collective)" if alt_mode["shard"] == "cts"
+                               else "learner-sharded dp%%d + RCCL reduce_scatter in %d pieces" % args.pieces)
+                              % world,
+               "value": round(units / (a_el / args.steps), 1), "unit": "client-ciphertexts/s",
+               "ms_per_step": round(a_el * 1e3 / args.steps, 4),
+               "local_wavg_ms_avg": round(sum(a_k) / len(a_k), 4)}
+        if not args.no_check:
+            alt["check"] = checked(alt_mode)
+        del alt_mode
+        torch.cuda.empty_cache()
+    out, K_loc, C_loc = main_mode["out"], main_mode["K_loc"], main_mode["C_loc"]
+    enc_times, cts, weights = main_mode["enc_times"], main_mode["cts"], main_mode["weights"]
+    cts_mode = main_mode["shard"] == "cts"
+    local_wavg = main_mode["kernel"]
 
     # device-resident decrypt+decode timing over the K aggregated ciphertexts
     local_wavg()
@@ -425,12 +463,14 @@ def main():
     }
     if check:
         res["check"] = check
+    if alt:
+        res["alternative_partitioning"] = alt
     if api:
         res["api_bytes_path"] = api
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, L, q, psi, delta, batch, Cl, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        os.write(json_fd, (json.dumps(res) + "\n").encode())
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -19,8 +19,9 @@ def _run(args, timeout=300):
     env = dict(os.environ)
     p = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
-    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
-    return json.loads(line)
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]  # the driver reads ONE JSON line
+    return json.loads(lines[0])
 
 
 def _port():
@@ -43,16 +44,24 @@ def test_bench_single_gpu_line():
 
 
 def test_bench_distributed_path_one_rank():
+    """--shard learners headline (NCCL group, pipelined reduce_scatter, modq) with the
+    ciphertext-sharded alternative measured beside it."""
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist", "--pieces", "3"] + COMMON)
+              "--force-dist", "--shard", "learners", "--pieces", "3"] + COMMON)
     assert "reduce_scatter" in r["config"]["workload"]
     assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
+    alt = r["alternative_partitioning"]
+    assert alt["parallelism"].startswith("ciphertext-sharded") and alt["value"] > 0
+    assert alt["check"]["max_abs_err"] < 1e-8
 
 
 def test_bench_ciphertext_sharded_path_one_rank():
+    """The default N > 1 layout, with the RCCL learner-sharded alternative beside it."""
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist", "--shard", "cts"] + COMMON)
+              "--force-dist"] + COMMON)
     assert r["config"]["parallelism"] == "ciphertext-sharded dp1"
     assert r["check"]["max_abs_err"] < 1e-8
+    alt = r["alternative_partitioning"]
+    assert "RCCL" in alt["parallelism"] and alt["check"]["max_abs_err"] < 1e-8
