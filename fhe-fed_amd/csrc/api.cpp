@@ -86,16 +86,8 @@ struct DeviceGuard {
   }
 };
 
-static std::mutex& ctx_mutex(const shelfi_ctx* ctx) {
-  // one mutex per context, kept in a side table to keep shelfi_ctx POD-like
-  static std::mutex table_mu;
-  static std::vector<std::pair<const shelfi_ctx*, std::mutex*>> table;
-  std::lock_guard<std::mutex> g(table_mu);
-  for (auto& e : table)
-    if (e.first == ctx) return *e.second;
-  table.emplace_back(ctx, new std::mutex());
-  return *table.back().second;
-}
+// Calls on one context are serialized (as the reference's GIL serializes its object).
+static std::mutex& ctx_mutex(const shelfi_ctx* ctx) { return ctx->mu; }
 
 template <class F>
 static int guarded(F&& f) {

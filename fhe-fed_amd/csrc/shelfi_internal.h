@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -95,6 +96,7 @@ class Stager;
 }
 
 struct shelfi_ctx {
+  mutable std::mutex mu;  // serializes calls on this context
   shelfi::Params p;
   int device = 0;
   hipStream_t stream = nullptr;   // copy / default work stream
