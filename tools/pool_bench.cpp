@@ -1,0 +1,24 @@
+// Host copy-pool throughput vs threads and slot size (sizing host_stage.cpp).
+// build: hipcc -O3 -std=c++17 -Ifhe-fed_amd/csrc -o tools/build/pool_bench tools/pool_bench.cpp fhe-fed_amd/csrc/host_stage.cpp -lpthread
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "host_stage.h"
+using namespace shelfi;
+int main(int argc, char** argv) {
+  const size_t total = (size_t)1 << 30;
+  std::vector<uint8_t> src(total, 1), dst(total, 0);
+  for (int threads : {1, 4, 8, 12, 16}) {
+    CopyPool pool(threads);
+    for (size_t slot : {(size_t)2 << 20, (size_t)8 << 20, (size_t)32 << 20}) {
+      auto t0 = std::chrono::steady_clock::now();
+      for (int rep = 0; rep < 3; ++rep)
+        for (size_t off = 0; off < total; off += slot) pool.copy(dst.data() + off, src.data() + off, slot);
+      double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 3;
+      printf("threads %d slot %3zu MiB: %.1f GB/s (%.1f us per slot)\n", threads, slot >> 20, total / s / 1e9,
+             s / (total / slot) * 1e6);
+    }
+  }
+}
