@@ -40,9 +40,9 @@ CopyPool::CopyPool(int threads) : parts_(std::max(1, threads)) {
 CopyPool::~CopyPool() {
   {
     std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
+    stop_.store(true);
   }
-  cv_go_.notify_all();
+  cv_.notify_all();
   for (auto& t : workers_) t.join();
 }
 
@@ -64,17 +64,20 @@ void CopyPool::share(int id) {
 void CopyPool::run(int id) {
   uint64_t seen = 0;
   for (;;) {
-    {
+    uint64_t g = gen_.load(std::memory_order_acquire);
+    for (int spin = 0; g == seen && spin < (1 << 14) && !stop_.load(std::memory_order_relaxed); ++spin) {
+      __builtin_ia32_pause();
+      g = gen_.load(std::memory_order_acquire);
+    }
+    if (g == seen) {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_go_.wait(lk, [&] { return stop_ || gen_ != seen; });
-      if (stop_) return;
-      seen = gen_;
+      cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
+      g = gen_.load(std::memory_order_acquire);
     }
+    if (stop_.load()) return;
+    seen = g;
     share(id);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) cv_done_.notify_one();
-    }
+    pending_.fetch_sub(1, std::memory_order_acq_rel);
   }
 }
 
@@ -86,18 +89,17 @@ void CopyPool::copy_many(const CopyJob* jobs, size_t njobs) {
     for (size_t j = 0; j < njobs; ++j) std::memcpy(jobs[j].dst, jobs[j].src, jobs[j].n);
     return;
   }
+  jobs_ = jobs;
+  njobs_ = njobs;
+  total_ = total;
+  pending_.store((int)workers_.size(), std::memory_order_relaxed);
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    jobs_ = jobs;
-    njobs_ = njobs;
-    total_ = total;
-    pending_ = (int)workers_.size();
-    ++gen_;
+    std::lock_guard<std::mutex> lk(mu_);  // no lost wake-up for a worker about to sleep
+    gen_.fetch_add(1, std::memory_order_release);
   }
-  cv_go_.notify_all();
+  cv_.notify_all();
   share(0);
-  std::unique_lock<std::mutex> lk(mu_);
-  cv_done_.wait(lk, [&] { return pending_ == 0; });
+  while (pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
 }
 
 void CopyPool::copy(void* dst, const void* src, size_t n) {

@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
@@ -46,11 +47,13 @@ class CopyPool {
   void share(int id);
   int parts_ = 1;  // set before the workers start
   std::vector<std::thread> workers_;
+  // A new list is published by bumping gen_ (release); workers spin on it for a while
+  // after each share (the staging loop issues lists back to back), then sleep on cv_.
   std::mutex mu_;
-  std::condition_variable cv_go_, cv_done_;
-  uint64_t gen_ = 0;
-  int pending_ = 0;
-  bool stop_ = false;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> pending_{0};
+  std::atomic<bool> stop_{false};
   const CopyJob* jobs_ = nullptr;
   size_t njobs_ = 0, total_ = 0;
 };
