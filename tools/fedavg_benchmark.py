@@ -6,6 +6,7 @@ same printed timing lines (benchmark.py:539-543).
   python tools/fedavg_benchmark.py --model resnet18 --clients 3            # benchmark.py
   python tools/fedavg_benchmark.py --model resnet50 --select rate --rate 0.1  # selection_rate
   python tools/fedavg_benchmark.py --model resnet18 --pack                 # one vector per client
+  python tools/fedavg_benchmark.py --model resnet50 --select mask --rate 0.1 --pack  # masking.py top-k
 """
 import argparse
 import os
@@ -29,8 +30,9 @@ def main():
     ap.add_argument("--scale-bits", type=int, default=52)
     ap.add_argument("--mult-depth", type=int, default=1)
     ap.add_argument("--cryptodir", default=os.path.join(ROOT, "tests", "golden", "palisade") + "/")
-    ap.add_argument("--select", choices=["all", "layers", "rate"], default="all")
-    ap.add_argument("--rate", type=float, default=0.1)
+    ap.add_argument("--select", choices=["all", "layers", "rate", "mask"], default="all")
+    ap.add_argument("--rate", type=float, default=0.1,
+                    help="rate: encrypted prefix fraction; mask: top-k fraction of each key")
     ap.add_argument("--layers", default="")
     ap.add_argument("--pack", action="store_true")
     ap.add_argument("--wire", choices=["shelfi", "palisade"], default="shelfi",
@@ -49,7 +51,11 @@ def main():
     if a.wire == "palisade":
         ck.set_wire_format("palisade")
     t_init = time.time() - t0
-    sel = F.Selection(a.select, rate=a.rate, layers=[int(x) for x in a.layers.split(",") if x])
+    masks = None
+    if a.select == "mask":  # masking.py:15-21 top-k of a sensitivity map (synthetic: |grad| ~ U(0,1))
+        rs = np.random.default_rng(11)
+        masks = {k: F.top_k_mask(rs.random(v.size), a.rate) for k, v in states[0].items()}
+    sel = F.Selection(a.select, rate=a.rate, layers=[int(x) for x in a.layers.split(",") if x], masks=masks)
     run = F.SecureFedAvg(ck, sel, pack=a.pack)
     agg, t = run.run(states)
     print("Init Time: {}".format(t_init))
