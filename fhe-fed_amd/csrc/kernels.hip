@@ -96,9 +96,10 @@ __device__ __forceinline__ uint64_t mulmod_generic(uint64_t a, uint64_t b, const
   return addmod(shoup_mul(hi, c.r64, c.r64_shoup, c.q), red64(lo, c.q, c.one_shoup), c.q);
 }
 __device__ __forceinline__ uint64_t mod_signed_dev(int64_t v, const TowerConst& c) {
-  if (v >= 0) return red64((uint64_t)v, c.q, c.one_shoup);
-  uint64_t r = red64((uint64_t)0 - (uint64_t)v, c.q, c.one_shoup);
-  return r ? c.q - r : 0;
+  // one reduction of |v| and a sign fix-up (two branch-free reductions cost registers)
+  const bool neg = v < 0;
+  const uint64_t r = red64(neg ? (uint64_t)0 - (uint64_t)v : (uint64_t)v, c.q, c.one_shoup);
+  return (neg && r) ? c.q - r : r;
 }
 __device__ __forceinline__ uint64_t small_mod(int64_t v, uint64_t q) {  // |v| < q
   return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v;
@@ -368,7 +369,7 @@ __device__ __forceinline__ ulonglong2 lds_get2(const uint64_t* sm, uint32_t p) {
 // Its stages are taken KCH = 3 at a time: each thread loads a set of 2^KCH elements
 // that only interact among themselves during those stages, runs them in registers
 // (2^KCH - 1 twiddle pairs), and writes the set back — one barrier per chunk instead
-// of one per stage.  256 threads, blk <= 2048 (so at most 8 elements per thread).
+// of one per stage.  256 threads; blocks of 2^blkLog <= 4096 elements (ntt_block_log).
 //
 // Forward (CT, half-size h = blk/2 .. 1): a chunk of k stages starting at half-size
 // h0 works on sets {j0 + d m}, d = h0 / 2^(k-1), j0 = g 2 h0 + off (off < d).
@@ -519,6 +520,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks(uint64_t* __restrict__ pol
 // after the columns pass) one after the other through the same LDS block, and writes
 // c0 = v*b + (m + e0), c1 = v*a + e1 (ckks.cpp:81, PALISADE Encrypt) — the transformed
 // polynomials never return to HBM.
+template <int PP>  // 16-byte pairs per thread: blk / 512
 __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __restrict__ pbuf,
                                                           uint32_t L, uint32_t logN, uint32_t sstart,
                                                           const uint64_t* __restrict__ tw,
@@ -530,7 +532,6 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
                                                           const int64_t* __restrict__ me0,
                                                           const int16_t* __restrict__ ve) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-  constexpr int PP = 4;  // 16-byte pairs per thread (blk <= 2048)
   const uint32_t blkLog = logN - sstart, blk = 1u << blkLog;
   const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
   const uint64_t rest = blockIdx.x >> sstart;
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
   const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << blkLog);  // within [L][N]
   const uint64_t LN = (uint64_t)L << logN;
-  ulonglong2 V[PP], M[PP];
+  ulonglong2 V[PP];  // NTT(v), kept for both products
 #pragma unroll
   for (int poly = 0; poly < 3; ++poly) {
     if (me0) {  // single-pass ring: expand the compact sample record (no columns pass)
@@ -567,20 +568,14 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
       const uint64_t e = off + 2 * p;
       if (poly == 0) {
         V[i] = v;
-      } else if (poly == 1) {
-        M[i] = v;
-      } else {
-        const ulonglong2 B = *reinterpret_cast<const ulonglong2*>(pk + e);
-        const ulonglong2 Bs = *reinterpret_cast<const ulonglong2*>(pksh + e);
-        const ulonglong2 A = *reinterpret_cast<const ulonglong2*>(pk + LN + e);
-        const ulonglong2 As = *reinterpret_cast<const ulonglong2*>(pksh + LN + e);
-        ulonglong2 c0, c1;
-        c0.x = addmod(shoup_mul(V[i].x, B.x, Bs.x, q), M[i].x, q);
-        c0.y = addmod(shoup_mul(V[i].y, B.y, Bs.y, q), M[i].y, q);
-        c1.x = addmod(shoup_mul(V[i].x, A.x, As.x, q), v.x, q);
-        c1.y = addmod(shoup_mul(V[i].y, A.y, As.y, q), v.y, q);
-        *reinterpret_cast<ulonglong2*>(ct + k * 2 * LN + e) = c0;
-        *reinterpret_cast<ulonglong2*>(ct + (k * 2 + 1) * LN + e) = c1;
+      } else {  // poly 1: c0 = v*b + (m + e0); poly 2: c1 = v*a + e1
+        const uint64_t off_pk = (poly == 1 ? 0 : LN) + e;
+        const ulonglong2 P = *reinterpret_cast<const ulonglong2*>(pk + off_pk);
+        const ulonglong2 Ps = *reinterpret_cast<const ulonglong2*>(pksh + off_pk);
+        ulonglong2 c;
+        c.x = addmod(shoup_mul(V[i].x, P.x, Ps.x, q), v.x, q);
+        c.y = addmod(shoup_mul(V[i].y, P.y, Ps.y, q), v.y, q);
+        *reinterpret_cast<ulonglong2*>(ct + (k * 2 + (poly - 1)) * LN + e) = c;
       }
     }
     __syncthreads();  // LDS is refilled by the next polynomial
@@ -692,7 +687,7 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
                 const DeviceTables& dt, hipStream_t s) {
   if (!P) return;
   const uint32_t N = 1u << logN;
-  const uint32_t blkLog = logN < (uint32_t)kNttBlockLog ? logN : (uint32_t)kNttBlockLog;
+  const uint32_t blkLog = ntt_block_log(logN);
   const int logR = (int)(logN - blkLog);
   const uint32_t blk = 1u << blkLog;
   const size_t lds = (size_t)blk * sizeof(uint64_t);
@@ -723,7 +718,7 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
 // FFTSpecialInv (encode): DIF stages len = S..2 with twiddle finv[len/2 + (x mod
 // len)], then BitReverse and /S (both folded into enc_prep).  First LOGR stages
 // on register columns (reading the learner's real vector directly), the rest in
-// LDS blocks of 2^kFftBlockLog complex values.
+// LDS blocks of 2^fft_block_log(logS) complex values.
 template <int LOGR>
 __global__ __launch_bounds__(256) void fft_inv_cols(const double* __restrict__ x, uint64_t n,
                                                     double2* __restrict__ buf, uint32_t logS,
@@ -997,18 +992,9 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
   const uint32_t c = (blockIdx.x % bpp) * 256 + threadIdx.x;
   const uint64_t LN = (uint64_t)L << logN;
   const uint64_t j0 = (k << logN) + c;
-  // POLY: 0 = v, 1 = m + e0, 2 = e1 (one launch each keeps one source array live)
-  int64_t val[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint64_t j = j0 + (uint64_t)BLK * r;
-    if (POLY == 1) {
-      val[r] = me0[j];
-    } else {
-      const int32_t sv = ve[j];
-      val[r] = POLY == 0 ? (int32_t)(int8_t)(sv & 0xFF) : (sv >> 8);
-    }
-  }
+  // POLY: 0 = v, 1 = m + e0, 2 = e1 (one launch each).  The record is re-read for every
+  // tower (L1/L2 hits) rather than kept live beside the R residues: keeping R int64
+  // sources across the tower loop cost 2 waves/SIMD of occupancy (170 VGPRs).
 #pragma unroll 1
   for (uint32_t t = 0; t < L; ++t) {
     const TowerConst cst = tcs[t];
@@ -1017,7 +1003,16 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
     const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
     uint64_t x[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = POLY == 1 ? mod_signed_dev(val[r], cst) : small_mod(val[r], q);
+    for (int r = 0; r < R; ++r) {
+      const uint64_t j = j0 + (uint64_t)BLK * r;
+      if (POLY == 1) {
+        x[r] = mod_signed_dev(me0[j], cst);
+        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+      } else {
+        const int32_t sv = ve[j];
+        x[r] = small_mod(POLY == 0 ? (int32_t)(int8_t)(sv & 0xFF) : (sv >> 8), q);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < LOGR; ++s) {
       const int m = 1 << s, tr = R >> (s + 1);
@@ -1051,7 +1046,7 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   double2* fbuf = reinterpret_cast<double2*>(scratch);
   uint64_t* pbuf = reinterpret_cast<uint64_t*>(fbuf + K * (uint64_t)p.batch);
   // 1. FFTSpecialInv of each ciphertext's slot vector
-  const uint32_t blkLog = logS < (uint32_t)kFftBlockLog ? logS : (uint32_t)kFftBlockLog;
+  const uint32_t blkLog = fft_block_log(logS);
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;
   if (logR > 0) {
@@ -1076,7 +1071,7 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   SHELFI_HIP(hipGetLastError());
   // 3. NTT of v, m + e0, e1 per tower (columns pass expands the record), then the
   // blocks pass fused with the public-key combine writes the ciphertexts
-  const uint32_t nblkLog = p.logN < (uint32_t)kNttBlockLog ? p.logN : (uint32_t)kNttBlockLog;
+  const uint32_t nblkLog = ntt_block_log(p.logN);
   const int nlogR = (int)(p.logN - nblkLog);
   if (nlogR > 0) {
     const uint64_t nb = K * ((p.N >> nlogR) / 256);
@@ -1101,7 +1096,13 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   }
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
-  hipLaunchKernelGGL(ntt_fwd_blocks_enc, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
+  if (nblkLog > 11)
+    hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
+                     pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
+                     dk.pk_sh, ct, nlogR > 0 ? (const int64_t*)nullptr : me0,
+                     nlogR > 0 ? (const int16_t*)nullptr : ve);
+  else
+    hipLaunchKernelGGL(ntt_fwd_blocks_enc<4>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
                      pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
                      dk.pk_sh, ct, nlogR > 0 ? (const int64_t*)nullptr : me0,
                      nlogR > 0 ? (const int16_t*)nullptr : ve);
@@ -1295,7 +1296,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
   // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts)
   {
-    const uint32_t blkLog = p.logN < (uint32_t)kNttBlockLog ? p.logN : (uint32_t)kNttBlockLog;
+    const uint32_t blkLog = ntt_block_log(p.logN);
     const int logR = (int)(p.logN - blkLog);
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
@@ -1321,7 +1322,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        dn->flags);
     SHELFI_HIP(hipGetLastError());
   }
-  const uint32_t blkLog = logS < (uint32_t)kFftBlockLog ? logS : (uint32_t)kFftBlockLog;
+  const uint32_t blkLog = fft_block_log(logS);
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;
   hipLaunchKernelGGL(fft_fwd_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, fbuf, logS,

@@ -30,8 +30,18 @@ struct Error {
 
 // ----------------------------------------------------------- host params ----
 constexpr int kMaxTowers = 16;
-constexpr int kFftBlockLog = 10;  // complex f64 block staged in LDS by FFT pass 2
-constexpr int kNttBlockLog = 11;  // u64 block staged in LDS by NTT pass 2
+constexpr int kFftBlockLog = 10;     // complex f64 block staged in LDS by FFT pass 2
+constexpr int kFftBlockLogBig = 11;  // batch >= 2^15: 32 KiB blocks keep pass 1 at 16 columns
+inline uint32_t fft_block_log(uint32_t logS) {
+  const uint32_t b = logS >= 15 ? (uint32_t)kFftBlockLogBig : (uint32_t)kFftBlockLog;
+  return logS < b ? logS : b;
+}
+constexpr int kNttBlockLog = 11;     // u64 block staged in LDS by NTT pass 2 (N <= 2^15)
+constexpr int kNttBlockLogBig = 12;  // N >= 2^16: 32 KiB blocks keep pass 1 at 16 columns
+inline uint32_t ntt_block_log(uint32_t logN) {
+  const uint32_t b = logN >= 16 ? (uint32_t)kNttBlockLogBig : (uint32_t)kNttBlockLog;
+  return logN < b ? logN : b;
+}
 
 struct Params {
   uint32_t N = 0, logN = 0, L = 0, batch = 0, gap = 0, scale_bits = 0, first_mod_bits = 0;
