@@ -382,10 +382,15 @@ def main():
     # device-resident decrypt+decode timing over the K aggregated ciphertexts
     local_wavg()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
+    dec = D.decrypt(ck, out, K_loc * batch, delta * delta)  # warm: sizes the scratch arena
     torch.cuda.synchronize()
-    dec_ms_per_ct = (time.perf_counter() - t0) * 1e3 / K_loc
+    dts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+    dec_ms_per_ct = sorted(dts)[1] * 1e3 / K_loc
     assert torch.isfinite(dec).all().item()
     del dec
 
