@@ -50,33 +50,49 @@ __device__ __forceinline__ uint64_t red64(uint64_t x, uint64_t q, uint64_t one_s
   return r >= q ? r - q : r;
 }
 // ---- lazy NTT arithmetic (bit-exact after the final canonicalisation) -----
-// High 64 bits of x*y from three 32x32 partial products (x0*y0 dropped): equals the
-// exact value or one less.
+// High 64 bits of x*y from three 32x32 partial products, all carries out of the low
+// 64 bits dropped (x0*y0 and the sum of the middle low halves): the exact value minus
+// 0, 1 or 2.  Six VALU ops (three quarter-rate) instead of eight for the carried form.
 __device__ __forceinline__ uint64_t umulhi_approx(uint64_t x, uint64_t y) {
   const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
-  const uint64_t t = (uint64_t)x1 * y0;
-  const uint64_t u = (uint64_t)x0 * y1 + (uint32_t)t;
-  return (uint64_t)x1 * y1 + (t >> 32) + (u >> 32);
+  return (uint64_t)x1 * y1 + (((uint64_t)x1 * y0) >> 32) + (((uint64_t)x0 * y1) >> 32);
 }
-// x * w mod q up to 2 extra q: result in [0, 3q) for any 64-bit x (Shoup, no correction).
+// x * w mod q up to 3 extra q: result in [0, 4q) for any 64-bit x (Shoup with the
+// quotient short by at most 2).  x*w - h*q is formed as x*w + h*(2^64 - q) so the
+// second 64-bit product takes the first as its v_mad_u64_u32 addend (no borrow chain).
 __device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
+  const uint64_t h = umulhi_approx(x, wp), nq = (uint64_t)0 - q;
+  const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+  const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+  const uint64_t lo = (uint64_t)h0 * n0 + (uint64_t)x0 * w0;  // mod 2^64
+  const uint32_t cross = x1 * w0 + x0 * w1 + h1 * n0 + h0 * n1;
+  return lo + ((uint64_t)cross << 32);
+}
+// Same bound, as x*w - h*q (the form the inverse butterflies schedule better).
+__device__ __forceinline__ uint64_t shoup_lazy_sub(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
   return x * w - umulhi_approx(x, wp) * q;
+}
+// X >= 4q ? X - 4q : X, selected on the subtraction's own borrow.
+__device__ __forceinline__ uint64_t sub4q_if_ge(uint64_t X, uint64_t q) {
+  uint64_t d;
+  const bool borrow = __builtin_sub_overflow(X, q << 2, &d);
+  return borrow ? X : d;
 }
 // Forward (CT) butterfly keeping values in [0, 8q) (q < 2^60, so 8q < 2^63).
 __device__ __forceinline__ void ct_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                        uint64_t q, uint64_t q3, uint64_t q4) {
-  const uint64_t x = X >= q4 ? X - q4 : X;  // [0, 4q)
-  const uint64_t t = shoup_lazy(Y, W, Wp, q);  // [0, 3q)
-  X = x + t;                                 // [0, 7q)
-  Y = x - t + q3;                            // (0, 7q)
+                                        uint64_t q) {
+  const uint64_t x = sub4q_if_ge(X, q);      // [0, 4q)
+  const uint64_t t = shoup_lazy(Y, W, Wp, q);  // [0, 4q)
+  X = x + t;                                 // [0, 8q)
+  Y = x + (q << 2) - t;                      // (0, 8q)
 }
 // Inverse (GS) butterfly keeping values in [0, 4q).
 __device__ __forceinline__ void gs_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                        uint64_t q, uint64_t q4) {
+                                        uint64_t q) {
   const uint64_t s = X + Y;                  // [0, 8q)
-  const uint64_t d = X - Y + q4;             // (0, 8q)
-  X = s >= q4 ? s - q4 : s;                  // [0, 4q)
-  Y = shoup_lazy(d, W, Wp, q);               // [0, 3q)
+  const uint64_t d = X + (q << 2) - Y;       // (0, 8q)
+  X = sub4q_if_ge(s, q);                     // [0, 4q)
+  Y = shoup_lazy_sub(d, W, Wp, q);           // [0, 4q)
 }
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t canon8(uint64_t x, uint64_t q) {
@@ -312,7 +328,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols(uint64_t* __restrict__ polys
   const uint64_t poly = blockIdx.x / bpp;
   const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
   const uint32_t t = (uint32_t)(poly % L);
-  const uint64_t q = tcs[t].q, q3 = 3 * q, q4 = 4 * q;
+  const uint64_t q = tcs[t].q;
   const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
   const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
   uint64_t* __restrict__ a = polys + poly * N + col;
@@ -328,7 +344,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        ct_bfly(x[r0], x[r1], W, Wp, q, q3, q4);
+        ct_bfly(x[r0], x[r1], W, Wp, q);
       }
     }
   }
@@ -400,7 +416,7 @@ __device__ __forceinline__ void fwd_chunk(uint64_t* sm, uint32_t blk, uint32_t h
 #pragma unroll
         for (int mm = 0; mm < hm; ++mm) {
           const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
-          ct_bfly(x[m0], x[m1], W, Wp, q, 3 * q, 4 * q);
+          ct_bfly(x[m0], x[m1], W, Wp, q);
         }
       }
     }
@@ -461,7 +477,7 @@ __device__ __forceinline__ void inv_chunk(uint64_t* sm, uint32_t blk, uint32_t t
 #pragma unroll
         for (int mm = 0; mm < hm; ++mm) {
           const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
-          gs_bfly(x[m0], x[m1], W, Wp, q, 4 * q);
+          gs_bfly(x[m0], x[m1], W, Wp, q);
         }
       }
     }
@@ -663,7 +679,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        gs_bfly(x[r0], x[r1], W, Wp, q, 4 * q);
+        gs_bfly(x[r0], x[r1], W, Wp, q);
       }
     }
   }
@@ -998,7 +1014,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 #pragma unroll 1
   for (uint32_t t = 0; t < L; ++t) {
     const TowerConst cst = tcs[t];
-    const uint64_t q = cst.q, q3 = 3 * q, q4 = 4 * q;
+    const uint64_t q = cst.q;
     const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
     const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
     uint64_t x[R];
@@ -1022,7 +1038,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 #pragma unroll
         for (int jj = 0; jj < tr; ++jj) {
           const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-          ct_bfly(x[r0], x[r1], W, Wp, q, q3, q4);
+          ct_bfly(x[r0], x[r1], W, Wp, q);
         }
       }
     }
