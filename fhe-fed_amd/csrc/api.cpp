@@ -279,7 +279,9 @@ static void build_tables(shelfi_ctx* ctx) {
   ctx->dt.fft_inv = upload(tinv.data(), S);
   ctx->dt.fft_fwd = upload(tfwd.data(), S);
   uint64_t cdt[64];
-  ctx->dt.cdt_len = gauss_cdt(p.sigma, cdt, 64);
+  // <= 63 entries: the samplers' 6-step binary search over the 64-padded table counts
+  // at most 63 (sigma <= 4.77; the default 3.19 gives 43)
+  ctx->dt.cdt_len = gauss_cdt(p.sigma, cdt, 63);
   if (ctx->dt.cdt_len < 0) throw Error{SHELFI_ERR_ARG, "Gaussian table too large"};
   ctx->dt.cdt = upload(cdt, (size_t)ctx->dt.cdt_len);
   ctx->params_id = compute_params_id(p);

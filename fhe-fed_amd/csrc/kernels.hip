@@ -936,6 +936,16 @@ __device__ __forceinline__ int64_t gauss_sample(uint64_t r, const uint64_t* __re
   return (r & 1) ? -k : k;
 }
 __device__ __forceinline__ int64_t ternary_sample(uint64_t r) { return (int64_t)(r % 3) - 1; }
+// The same count by branch-free binary search over the table padded to 64 entries with
+// 2^64 - 1 (never <= a 63-bit u) and staged in LDS: 6 steps instead of T = 43 64-bit
+// compares (the table is non-decreasing, so #{i : u >= cdt[i]} is an upper bound).
+__device__ __forceinline__ int64_t gauss_sample_lds(uint64_t r, const uint64_t* tab) {
+  const uint64_t u = r >> 1;
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) k += (u >= tab[k + step - 1]) ? step : 0u;
+  return (r & 1) ? -(int64_t)k : (int64_t)k;
+}
 
 // -------------------------------------------------------------- encrypt ----
 // One thread = ChaCha20 block bb of each sampled polynomial, which feeds the 8
@@ -953,6 +963,9 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
                                                        int16_t* __restrict__ ve,
                                                        uint32_t* __restrict__ flag) {
   const uint32_t N = 1u << logN, S = 1u << logS, E = N >> 3;
+  __shared__ uint64_t tab[64];
+  if (threadIdx.x < 64) tab[threadIdx.x] = (int)threadIdx.x < T ? cdt[threadIdx.x] : ~0ull;
+  __syncthreads();
   const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = gid >> (logN - 3);
   if (k >= K) return;
@@ -978,12 +991,12 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
       if (!(fabs(val) <= lim)) atomicOr(flag, 1u);  // also catches NaN / inf
       m = round_half_away(val);
     }
-    me0[(k << logN) + j] = m + gauss_sample(w[u], cdt, T);
+    me0[(k << logN) + j] = m + gauss_sample_lds(w[u], tab);
   }
   chacha20_block(key, 2 * E + bb, nonce, w);
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    const int32_t e1 = (int32_t)gauss_sample(w[u], cdt, T);
+    const int32_t e1 = (int32_t)gauss_sample_lds(w[u], tab);
     ve[(k << logN) + bb + u * E] = (int16_t)((e1 << 8) | (vv[u] & 0xFF));
   }
 }

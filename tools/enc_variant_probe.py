@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Device encrypt (and decrypt) time per ciphertext under two settings of a launch-time
+switch (the environment variable named by VAR, read by the launch code under test), alternated A/B/A/B in one
+process, with the seeded ciphertexts checked bit-identical between the settings.
+  VAR=SHELFI_ENC_PARK BATCH=16384 DEPTH=3 K=238 python tools/enc_variant_probe.py"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fhe-fed_amd"))
+import torch  # noqa: E402
+
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+
+def main():
+    var = os.environ["VAR"]
+    batch, depth = int(os.environ.get("BATCH", "16384")), int(os.environ.get("DEPTH", "3"))
+    K = int(os.environ.get("K", "238"))
+    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, seed=7)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    inf = ck.info()
+    B = inf["batch"]
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = (torch.rand(K * B, generator=g, device="cuda", dtype=torch.float64) * 2 - 1)
+    outs = {}
+    times = {"0": [], "1": []}
+    dtimes = {"0": [], "1": []}
+    for rep in range(3):
+        for v in ("0", "1"):
+            os.environ[var] = v
+            ck.set_seed(11)
+            out = D.encrypt(ck, x)  # warm (allocations)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(5):
+                ck.set_seed(11)
+                t0 = time.perf_counter()
+                D.encrypt(ck, x, out=out)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            times[v].append(sorted(ts)[2] * 1e3 / K)
+            dec = D.decrypt(ck, out, K * B, inf["delta"])
+            torch.cuda.synchronize()
+            ds = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                D.decrypt(ck, out, K * B, inf["delta"], out=dec)
+                torch.cuda.synchronize()
+                ds.append(time.perf_counter() - t0)
+            dtimes[v].append(sorted(ds)[2] * 1e3 / K)
+            outs[v] = out.clone()
+    same = bool(torch.equal(outs["0"], outs["1"]))
+    err = float((dec - x).abs().max())
+    print("%s N=%d L=%d K=%d  encrypt ms/ct: 0 %s | 1 %s   decrypt ms/ct: 0 %s | 1 %s  identical=%s "
+          "max|dec-x|=%.2e" % (var, inf["ring_dim"], inf["num_towers"], K,
+                               ["%.5f" % t for t in times["0"]], ["%.5f" % t for t in times["1"]],
+                               ["%.5f" % t for t in dtimes["0"]], ["%.5f" % t for t in dtimes["1"]],
+                               same, err), flush=True)
+
+
+if __name__ == "__main__":
+    main()
