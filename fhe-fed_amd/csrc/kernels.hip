@@ -1151,10 +1151,22 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
                                                          double inv_scale,
                                                          double2* __restrict__ fbuf) {
   const uint32_t N = 1u << logN, S = 1u << logS;
-  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const uint64_t k = gid >> logS;
-  if (k >= K) return;
-  const uint32_t i = (uint32_t)(gid & (S - 1));
+  // S >= 256: a block owns the 256 slots i = hi.2^(logS-4) | mid.16 | lo (hi, lo < 16) of one
+  // middle value, so the tower reads (16 consecutive i) and, after a transpose through LDS,
+  // the bit-reversed stores (16 consecutive outputs, 256 B) are both contiguous.
+  const bool tiled = logS >= 8;
+  uint64_t k;
+  uint32_t i, mid = 0;
+  if (tiled) {
+    k = blockIdx.x >> (logS - 8);
+    mid = blockIdx.x & ((1u << (logS - 8)) - 1);
+    i = ((threadIdx.x >> 4) << (logS - 4)) | (mid << 4) | (threadIdx.x & 15);
+  } else {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    k = gid >> logS;
+    i = (uint32_t)(gid & (S - 1));
+  }
+  if (k >= K) return;  // block-uniform when tiled (the grid is exact)
   const uint32_t gapLog = logN - 1 - logS;
   const uint64_t* __restrict__ d = dbuf + k * ((uint64_t)L << logN);
   double res[2];
@@ -1188,7 +1200,17 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
     if (neg) v = -v;
     res[part] = __dmul_rn(v, inv_scale);
   }
-  fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
+  if (!tiled) {
+    fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
+    return;
+  }
+  // bitrev(i) = bitrev4(lo).2^(logS-4) | bitrev(mid).16 | bitrev4(hi): slot (lo, hi) goes to
+  // tile row bitrev4(lo), column bitrev4(hi); rows padded to 17 entries (conflict-free).
+  __shared__ double2 tile[16][17];
+  tile[bitrev_dev(threadIdx.x & 15, 4)][bitrev_dev(threadIdx.x >> 4, 4)] = make_double2(res[0], res[1]);
+  __syncthreads();
+  const uint32_t a = threadIdx.x >> 4, b = threadIdx.x & 15;
+  fbuf[k * S + ((a << (logS - 4)) | (bitrev_dev(mid, logS - 8) << 4) | b)] = tile[a][b];
 }
 
 // ------------------------------------------------- decode noise flooding ----
