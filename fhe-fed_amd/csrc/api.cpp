@@ -181,6 +181,8 @@ static void free_tables(shelfi_ctx* ctx) {
   dfree_t(ctx->dt.psi_rev_sh);
   dfree_t(ctx->dt.ipsi_rev);
   dfree_t(ctx->dt.ipsi_rev_sh);
+  dfree_t(ctx->dt.tw_fwd_blk);
+  dfree_t(ctx->dt.tw_inv_blk);
   dfree_t(ctx->dt.fft_inv);
   dfree_t(ctx->dt.fft_fwd);
   dfree_t(ctx->dt.cdt);
@@ -246,6 +248,15 @@ static void build_tables(shelfi_ctx* ctx) {
     c.qhat_lo = (uint64_t)qhat128;
     c.qhat_hi = (uint64_t)(qhat128 >> 64);
     c.inv_q = 1.0 / (double)q;
+    c.nq = (uint64_t)0 - q;
+    c.n4q = (uint64_t)0 - (q << 2);
+    c.n8q = (uint64_t)0 - (q << 3);
+    {
+      const uint32_t E = 63 - (uint32_t)__builtin_clzll(q);  // 2^E <= q < 2^(E+1)
+      c.red_ok = E >= 40;
+      c.red_sh = E >= 32 ? E - 32 : 0;
+      c.red_r = c.red_ok ? (uint32_t)(((u128)1 << (32 + E)) / q) : 0;
+    }
     // twiddles: psi^bitrev(i), psi^-bitrev(i)
     const uint64_t ipsi = invmod(p.psi[t], q);
     uint64_t a = 1, b = 1;
@@ -264,10 +275,29 @@ static void build_tables(shelfi_ctx* ctx) {
   ctx->dt.qmod128_lo = (uint64_t)Q128;
   ctx->dt.qmod128_hi = (uint64_t)(Q128 >> 64);
   ctx->dt.tc = upload(tc.data(), L);
+  ctx->dt.red_ok = true;
+  for (uint32_t t = 0; t < L; ++t) ctx->dt.red_ok = ctx->dt.red_ok && tc[t].red_ok;
   ctx->dt.psi_rev = upload(pr.data(), pr.size());
   ctx->dt.psi_rev_sh = upload(prs.data(), prs.size());
   ctx->dt.ipsi_rev = upload(ipr.data(), ipr.size());
   ctx->dt.ipsi_rev_sh = upload(iprs.data(), iprs.size());
+  {
+    const uint32_t BL = ntt_block_log(p.logN), sstart = p.logN - BL;
+    std::vector<ulonglong2> fb((size_t)L * N), ib((size_t)L * N);
+    for (uint32_t t = 0; t < L; ++t)
+      for (uint32_t b = 0; b < (1u << sstart); ++b) {
+        const size_t base = (size_t)t * N + ((size_t)b << BL);
+        fb[base] = ib[base] = make_ulonglong2(0, 0);
+        for (uint32_t l = 0; l < BL; ++l)
+          for (uint32_t i = 0; i < (1u << l); ++i) {
+            const size_t src = (size_t)t * N + (1ull << (sstart + l)) + ((size_t)b << l) + i;
+            fb[base + (1u << l) + i] = make_ulonglong2(pr[src], prs[src]);
+            ib[base + (1u << l) + i] = make_ulonglong2(ipr[src], iprs[src]);
+          }
+      }
+    ctx->dt.tw_fwd_blk = upload(fb.data(), fb.size());
+    ctx->dt.tw_inv_blk = upload(ib.data(), ib.size());
+  }
   const uint32_t S = p.batch;
   std::vector<double> ir(S), ii(S), fr(S), fi(S);
   fft_twiddles(S, ir.data(), ii.data(), fr.data(), fi.data());

@@ -65,8 +65,12 @@ __device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t 
   const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
   const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
   const uint64_t lo = (uint64_t)h0 * n0 + (uint64_t)x0 * w0;  // mod 2^64
-  const uint32_t cross = x1 * w0 + x0 * w1 + h1 * n0 + h0 * n1;
-  return lo + ((uint64_t)cross << 32);
+  // the cross terms only touch the high word: one v_add3_u32 there (left to itself the
+  // compiler zero-extends them and spends a v_mov + 64-bit add)
+  const uint32_t c1 = x1 * w0 + x0 * w1, c2 = h1 * n0 + h0 * n1;
+  uint32_t hi;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(lo >> 32)), "v"(c1), "v"(c2));
+  return ((uint64_t)hi << 32) | (uint32_t)lo;
 }
 // Same bound, as x*w - h*q (the form the inverse butterflies schedule better).
 __device__ __forceinline__ uint64_t shoup_lazy_sub(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
@@ -93,6 +97,62 @@ __device__ __forceinline__ void gs_bfly(uint64_t& X, uint64_t& Y, uint64_t W, ui
   const uint64_t d = X + (q << 2) - Y;       // (0, 8q)
   X = sub4q_if_ge(s, q);                     // [0, 4q)
   Y = shoup_lazy_sub(d, W, Wp, q);           // [0, 4q)
+}
+// ---- borrow-free conditional subtraction and one-step reduction ------------
+// d = x - c as x + (2^64 - c) (v_lshl_add_u64, no VCC carry chain); when x < c < 2^63
+// d wraps to >= 2^63, so its sign selects x (v_bfi_b32 on the sign mask).
+// (v_bfi_b32 spelled out: left to itself the compiler rebuilds the select from a 64-bit
+// compare + v_cndmask and v_max_i32 + v_and_or_b32, 6 instructions instead of 4.)
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, bitwise
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint64_t csub_neg(uint64_t x, uint64_t negc) {
+  const uint64_t d = x + negc;
+  const uint32_t m = (uint32_t)((int32_t)(uint32_t)(d >> 32) >> 31);
+  const uint32_t lo = bfi32(m, (uint32_t)x, (uint32_t)d);
+  const uint32_t hi = bfi32(m, (uint32_t)(x >> 32), (uint32_t)(d >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+// any u64 x -> [0, q) (TowerConst::red_ok, q >= 2^40): quotient estimate from x's high
+// word, short by at most 1, then one conditional subtraction.
+__device__ __forceinline__ uint64_t red_any(uint64_t x, const TowerConst& c) {
+  const uint32_t k = __umulhi((uint32_t)(x >> 32), c.red_r) >> c.red_sh;
+  const uint64_t r = x + (uint64_t)k * (uint32_t)c.nq + ((uint64_t)(k * (uint32_t)(c.nq >> 32)) << 32);
+  return csub_neg(r, c.nq);
+}
+// Reduction schedule for canonical inputs (bounds in units of q): stage s reduces its x
+// inputs only when its outputs could otherwise reach 16q; fwd_bound(S) bounds the
+// outputs after S stages.
+constexpr bool fwd_red_at(int s) {
+  int B = 1;
+  for (int i = 0; i < s; ++i) B = (B + 4 > 16 ? 8 : B) + 4;
+  return B + 4 > 16;
+}
+constexpr int fwd_bound(int S) {
+  int B = 1;
+  for (int i = 0; i < S; ++i) B = (B + 4 > 16 ? 8 : B) + 4;
+  return B;
+}
+// Forward (CT) butterfly with the input reduction scheduled by the caller: inputs
+// x < 16q (RED: x -= 8q when x >= 8q, so x < 8q) or x < 12q (no reduction), any y;
+// outputs X = x + t, Y = x + 4q - t with t = y w mod q in [0, 4q): below 16q (q < 2^60).
+template <bool RED>
+__device__ __forceinline__ void ct_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
+                                          uint64_t q, uint64_t n8q) {
+  const uint64_t x = RED ? csub_neg(X, n8q) : X;
+  const uint64_t t = shoup_lazy(Y, W, Wp, q);
+  X = x + t;
+  Y = x + (q << 2) - t;
+}
+
+// Inverse (GS) butterfly, [0, 4q) in and out, borrow-free reduction of the sum.
+__device__ __forceinline__ void gs_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
+                                          uint64_t q, uint64_t n4q) {
+  const uint64_t x = X, y = Y;
+  X = csub_neg(x + y, n4q);
+  Y = shoup_lazy(x + (q << 2) - y, W, Wp, q);
 }
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t canon8(uint64_t x, uint64_t q) {
@@ -598,6 +658,225 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
   }
 }
 
+// ---- compile-time block passes over per-block twiddle tables ---------------
+// For blocks of 2^BL elements (BL = ntt_block_log), block b owns the twiddle slice
+// tb = tw_*_blk[t][b << BL]: local stage l (the l-th of the block's stages, in the
+// transform's own order) and group i sit at tb[2^l + i] as one 16-byte {w, w'} pair
+// (DeviceTables::tw_fwd_blk / tw_inv_blk).  Every shift below is a compile-time constant
+// and every twiddle address is a block-uniform base plus a 32-bit offset: the generic
+// passes above spend ~40 VALU instructions per butterfly, mostly on 64-bit index math.
+//
+// Forward chunk of KC stages starting at local half-size 2^H0: set s -> g = s >> dLog,
+// j0 = g 2^(H0+1) + (s mod 2^dLog), elements j0 + m 2^dLog (dLog = H0 - KC + 1); its
+// stage-i twiddles are tb[2^l + g 2^i + gs], gs < 2^i, l = BL - 1 - H0 + i.
+//
+// Reduction schedule: the stage at local half-size 2^h reduces its x inputs iff h is
+// even, so the block's last stage (h = 0) always does: inputs below 12q (the columns
+// pass leaves < 8q), outputs below 12q, never above 16q in between (ct_bfly_s).
+template <int BL, int H0, int KC>
+__device__ __forceinline__ void fwd_set_ct(uint64_t (&x)[1 << KC], uint32_t g,
+                                           const ulonglong2* __restrict__ tb, uint64_t q,
+                                           uint64_t n8q) {
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    const int hm = 1 << (KC - 1 - i);
+    const ulonglong2* __restrict__ tw = tb + (1u << (BL - 1 - H0 + i)) + (g << i);
+#pragma unroll
+    for (int gs = 0; gs < (1 << i); ++gs) {
+      const ulonglong2 W = tw[gs];
+#pragma unroll
+      for (int mm = 0; mm < hm; ++mm) {
+        if (((H0 - i) & 1) == 0)
+          ct_bfly_s<true>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+        else
+          ct_bfly_s<false>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+      }
+    }
+  }
+}
+// One forward chunk over all 2^(BL-KC) sets of the block (NS per thread): Load(j) gives
+// element j, Store(r, j0, x) receives set r's transformed elements (positions j0 + m 2^dLog).
+template <int BL, int H0, int KC, class Load, class Store>
+__device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, uint64_t q,
+                                             uint64_t n8q, Load ld, Store st) {
+  constexpr int M = 1 << KC, dLog = H0 - KC + 1, NS = (1 << (BL - KC)) / 256;
+  static_assert(NS >= 1 && dLog >= 0, "chunk plan");
+#pragma unroll
+  for (int r = 0; r < NS; ++r) {
+    const uint32_t s = threadIdx.x + 256u * r;
+    const uint32_t g = (H0 == BL - 1) ? 0u : s >> dLog;  // first chunk: one group
+    const uint32_t j0 = (g << (H0 + 1)) + (s & ((1u << dLog) - 1));
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << dLog));
+    fwd_set_ct<BL, H0, KC>(x, g, tb, q, n8q);
+    st(r, j0, x);
+  }
+}
+// Inverse (GS) chunk of KC stages starting at local half-size 2^T0: set s -> g = s >> T0,
+// j0 = g 2^(T0+KC) + (s mod 2^T0), elements j0 + m 2^T0; stage-i twiddles are
+// tb[2^l + g 2^(KC-1-i) + gs], gs < 2^(KC-1-i), l = BL - 1 - T0 - i.
+template <int BL, int T0, int KC, class Load, class Store>
+__device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, uint64_t q,
+                                             uint64_t n4q, Load ld, Store st) {
+  constexpr int M = 1 << KC, NS = (1 << (BL - KC)) / 256;
+  static_assert(NS >= 1, "chunk plan");
+#pragma unroll
+  for (int r = 0; r < NS; ++r) {
+    const uint32_t s = threadIdx.x + 256u * r;
+    const uint32_t g = s >> T0;
+    const uint32_t j0 = (g << (T0 + KC)) + (s & ((1u << T0) - 1));
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << T0));
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int hm = 1 << i;
+      const ulonglong2* __restrict__ tw = tb + (1u << (BL - 1 - T0 - i)) + (g << (KC - 1 - i));
+#pragma unroll
+      for (int gs = 0; gs < (M >> (i + 1)); ++gs) {
+        const ulonglong2 W = tw[gs];
+#pragma unroll
+        for (int mm = 0; mm < hm; ++mm) gs_bfly_s(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n4q);
+      }
+    }
+    st(r, j0, x);
+  }
+}
+
+// Encrypt's blocks pass at compile-time shape: chunks K1..K4 (sum BL) per polynomial,
+// the first read straight from pbuf into registers, the last combined with the public
+// key straight from registers (3 LDS round trips and 3 barriers per polynomial instead
+// of 5 and 5).  Same contract as ntt_fwd_blocks_enc.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(const uint64_t* __restrict__ pbuf,
+                                                             uint32_t L, uint32_t logN,
+                                                             const ulonglong2* __restrict__ twb,
+                                                             const TowerConst* __restrict__ tcs,
+                                                             const uint64_t* __restrict__ pk,
+                                                             const uint64_t* __restrict__ pksh,
+                                                             uint64_t* __restrict__ ct,
+                                                             uint32_t zero) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
+  __shared__ __attribute__((aligned(16))) uint64_t sm[1 << BL];
+  const uint32_t sstart = logN - BL;
+  const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
+  const uint32_t rest = blockIdx.x >> sstart;
+  const uint32_t t = rest % L, k = rest / L;
+  const TowerConst& cst = tcs[t];
+  const uint64_t q = cst.q, n8q = cst.n8q;
+  const ulonglong2* tb0 = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t LN = (uint64_t)L << logN;
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  uint64_t V[NSL][ML];  // canonical NTT(v) at this thread's last-chunk positions
+#pragma unroll 1
+  for (int poly = 0; poly < 3; ++poly) {
+    const uint64_t* __restrict__ src = pbuf + ((uint64_t)k * 3 + poly) * LN + off;
+    // reload the twiddles per polynomial (zero == 0 is opaque to the compiler): hoisted
+    // out of this loop they would hold ~100 VGPRs for the whole kernel
+    const ulonglong2* __restrict__ tb = tb0 + poly * zero;
+    fwd_chunk_ct<BL, BL - 1, K1>(tb, q, n8q, [&](uint32_t j) { return src[j]; },
+                                 [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+                                   for (int m = 0; m < (1 << K1); ++m) sm[j0 + (m << (BL - K1))] = x[m];
+                                 });
+    __syncthreads();
+    fwd_chunk_ct<BL, BL - 1 - K1, K2>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+      for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << (BL - K1 - K2))] = x[m];
+    });
+    __syncthreads();
+    fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+      for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (BL - K1 - K2 - K3))] = x[m];
+    });
+    __syncthreads();
+    // last chunk (contiguous sets of ML, written inline: V captured by a lambda would
+    // live in scratch)
+#pragma unroll
+    for (int r = 0; r < NSL; ++r) {
+      const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4;
+      uint64_t x[ML];
+#pragma unroll
+      for (int m = 0; m < ML; ++m) x[m] = sm[j0 + m];
+      fwd_set_ct<BL, K4 - 1, K4>(x, g, tb, q, n8q);
+      if (poly == 0) {  // NTT(v), lazy (< 12q): only ever a Shoup multiplicand
+#pragma unroll
+        for (int m = 0; m < ML; ++m) V[r][m] = x[m];
+      } else {  // poly 1: c0 = v*b + (m + e0); poly 2: c1 = v*a + e1 (< 4q + 12q, then [0, q))
+        const uint64_t e = off + j0;
+        const uint64_t off_pk = (poly == 1 ? 0 : LN) + e;
+        uint64_t* __restrict__ dst = ct + ((uint64_t)k * 2 + (poly - 1)) * LN + e;
+#pragma unroll
+        for (int m = 0; m < ML; m += 2) {
+          const ulonglong2 P = *reinterpret_cast<const ulonglong2*>(pk + off_pk + m);
+          const ulonglong2 Ps = *reinterpret_cast<const ulonglong2*>(pksh + off_pk + m);
+          ulonglong2 c;
+          c.x = red_any(shoup_lazy(V[r][m], P.x, Ps.x, q) + x[m], cst);
+          c.y = red_any(shoup_lazy(V[r][m + 1], P.y, Ps.y, q) + x[m + 1], cst);
+          *reinterpret_cast<ulonglong2*>(dst + m) = c;
+        }
+      }
+    }
+    __syncthreads();  // LDS is refilled by the next polynomial
+  }
+}
+
+// Decrypt's first INTT pass at compile-time shape (chunks K1..K4, sum BL; needs
+// logN > BL): c0 + c1*s is formed straight into the first chunk's registers from the
+// ciphertext batch [K][2][L][N], and the last chunk writes the lazy ([0, 4q)) block to
+// dbuf [K][L][N] from registers for ntt_inv_cols.  Same contract as ntt_inv_blocks with
+// ct != nullptr and scale_ninv = 0.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restrict__ dbuf, uint32_t L,
+                                                             uint32_t logN,
+                                                             const ulonglong2* __restrict__ twb,
+                                                             const TowerConst* __restrict__ tcs,
+                                                             const uint64_t* __restrict__ ct,
+                                                             const uint64_t* __restrict__ sk,
+                                                             const uint64_t* __restrict__ sksh) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  __shared__ __attribute__((aligned(16))) uint64_t sm[1 << BL];
+  const uint32_t sstart = logN - BL;
+  const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
+  const uint32_t poly = blockIdx.x >> sstart;  // k * L + t
+  const uint32_t t = poly % L, k = poly / L;
+  const uint64_t q = tcs[t].q, n4q = tcs[t].n4q;
+  const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t* __restrict__ c0 = ct + (uint64_t)k * 2 * LN + off;
+  const uint64_t* __restrict__ c1 = c0 + LN;
+  const uint64_t* __restrict__ s = sk + off;
+  const uint64_t* __restrict__ ss = sksh + off;
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  // first chunk: contiguous sets of 2^K1 (T0 = 0)
+  inv_chunk_ct<BL, 0, K1>(tb, q, n4q,
+                          [&](uint32_t j) { return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q); },
+                          [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+                            for (int m = 0; m < (1 << K1); ++m) sm[j0 + m] = x[m];
+                          });
+  __syncthreads();
+  inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << K1)] = x[m];
+  });
+  __syncthreads();
+  inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (K1 + K2))] = x[m];
+  });
+  __syncthreads();
+  uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
+  inv_chunk_ct<BL, BL - K4, K4>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = x[m];
+  });
+}
+
 // Inverse blocks pass: small half-sizes first (LDS), then the top LOGR stages on
 // register columns (ntt_inv_cols), scaled by N^-1 in the last pass.
 // With ct != nullptr the input is decrypt's c0 + c1*s (ckks.cpp:189), formed while
@@ -679,7 +958,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        gs_bfly(x[r0], x[r1], W, Wp, q);
+        gs_bfly_s(x[r0], x[r1], W, Wp, q, c.n4q);
       }
     }
   }
@@ -1051,13 +1330,17 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 #pragma unroll
         for (int jj = 0; jj < tr; ++jj) {
           const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-          ct_bfly(x[r0], x[r1], W, Wp, q);
+          if (fwd_red_at(s))
+            ct_bfly_s<true>(x[r0], x[r1], W, Wp, q, cst.n8q);
+          else
+            ct_bfly_s<false>(x[r0], x[r1], W, Wp, q, cst.n8q);
         }
       }
     }
     uint64_t* __restrict__ o = out + (k * 3 + POLY) * LN + ((uint64_t)t << logN) + c;
+    // the blocks passes take inputs below 8q
 #pragma unroll
-    for (int r = 0; r < R; ++r) o[(uint64_t)r * BLK] = x[r];
+    for (int r = 0; r < R; ++r) o[(uint64_t)r * BLK] = fwd_bound(LOGR) > 8 ? csub_neg(x[r], cst.n8q) : x[r];
   }
 }
 
@@ -1125,7 +1408,13 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   }
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
-  if (nblkLog > 11)
+  if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
+  else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
+  else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
                      pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
                      dk.pk_sh, ct, nlogR > 0 ? (const int64_t*)nullptr : me0,
@@ -1351,9 +1640,16 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const int logR = (int)(p.logN - blkLog);
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
-    hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
-                       s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
-                       logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh);
+    if (logR > 0 && blkLog == 11 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh);
+    else if (logR > 0 && blkLog == 12 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh);
+    else
+      hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
+                         s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
+                         logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh);
     if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, dbuf, p.L, p.logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);

@@ -76,7 +76,11 @@ struct TowerConst {
   uint64_t qhat_inv, qhat_inv_shoup;  // (Q/q_t)^-1 mod q_t
   uint64_t qhat_lo, qhat_hi;  // (Q/q_t) mod 2^128
   double inv_q;               // 1.0 / q (CRT k estimate)
-  uint64_t pad;
+  uint64_t nq, n4q, n8q;      // 2^64 - q, - 4q, - 8q (borrow-free conditional subtractions)
+  // any u64 x -> [0, 2q): k = (x_hi * red_r) >> (32 + red_sh), x - k q (red_any; needs
+  // q >= 2^40, red_ok): red_r = floor(2^(32 + E) / q) < 2^32, E = bitlength(q) - 1
+  uint32_t red_r, red_sh, red_ok, pad32;
+  uint64_t pad[2];
 };
 
 struct DeviceTables {
@@ -85,6 +89,12 @@ struct DeviceTables {
   uint64_t* psi_rev_sh = nullptr;   // [L][N]  Shoup companions
   uint64_t* ipsi_rev = nullptr;     // [L][N]  psi^-bitrev(i)
   uint64_t* ipsi_rev_sh = nullptr;  // [L][N]
+  // per-block {w, w'} twiddle slices for the compile-time block passes: [L][nb][2^BL],
+  // entry 2^l + i of block b = index 2^(sstart + l) + b 2^l + i of psi_rev / ipsi_rev
+  // (BL = ntt_block_log(logN), sstart = logN - BL, nb = 2^sstart)
+  ulonglong2* tw_fwd_blk = nullptr;
+  ulonglong2* tw_inv_blk = nullptr;
+  bool red_ok = false;  // every tower has TowerConst::red_ok (q >= 2^40): *_ct kernels usable
   double2* fft_inv = nullptr;       // [B] flat special-FFT twiddles (FFTSpecialInv)
   double2* fft_fwd = nullptr;       // [B] (FFTSpecial)
   uint64_t* cdt = nullptr;          // Gaussian CDT [64]
