@@ -744,20 +744,25 @@ __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, 
   }
 }
 
+// LDS slot of element i in the compile-time block passes: XOR of bits 2-4 with the
+// row (i >> 5) & 7, so the strided sets of the middle chunks (stride 4: 16 lanes on the
+// same 4 slots) spread over all 32 eight-byte slots; groups of 4 stay contiguous.
+template <bool SW>
+__device__ __forceinline__ uint32_t lds_slot(uint32_t i) {
+  return SW ? i ^ (((i >> 5) & 7u) << 2) : i;
+}
+
 // Encrypt's blocks pass at compile-time shape: chunks K1..K4 (sum BL) per polynomial,
-// the first read straight from pbuf into registers, the last combined with the public
-// key straight from registers (3 LDS round trips and 3 barriers per polynomial instead
-// of 5 and 5).  Same contract as ntt_fwd_blocks_enc.
-template <int BL, int K1, int K2, int K3, int K4>
-__global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(const uint64_t* __restrict__ pbuf,
-                                                             uint32_t L, uint32_t logN,
-                                                             const ulonglong2* __restrict__ twb,
-                                                             const TowerConst* __restrict__ tcs,
-                                                             const uint64_t* __restrict__ pk,
-                                                             const uint64_t* __restrict__ pksh,
-                                                             uint64_t* __restrict__ ct,
-                                                             uint32_t zero) {
+// the first on registers loaded straight from pbuf, the last combined with the public key straight
+// from registers (3 LDS round trips and 3 barriers per polynomial instead of 5 and 5).
+// Same contract as ntt_fwd_blocks_enc.
+template <int BL, int K1, int K2, int K3, int K4, bool SW, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void ntt_fwd_blocks_enc_ct(
+    const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
+    const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk,
+    const uint64_t* __restrict__ pksh, uint64_t* __restrict__ ct, uint32_t zero) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
   constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
   __shared__ __attribute__((aligned(16))) uint64_t sm[1 << BL];
   const uint32_t sstart = logN - BL;
@@ -769,28 +774,32 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(const uint64_t* __r
   const ulonglong2* tb0 = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
-  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
-  uint64_t V[NSL][ML];  // canonical NTT(v) at this thread's last-chunk positions
+  const auto lds_ld = [&](uint32_t j) { return sm[lds_slot<SW>(j)]; };
+  uint64_t V[NSL][ML];  // NTT(v) at this thread's last-chunk positions
 #pragma unroll 1
   for (int poly = 0; poly < 3; ++poly) {
-    const uint64_t* __restrict__ src = pbuf + ((uint64_t)k * 3 + poly) * LN + off;
     // reload the twiddles per polynomial (zero == 0 is opaque to the compiler): hoisted
     // out of this loop they would hold ~100 VGPRs for the whole kernel
     const ulonglong2* __restrict__ tb = tb0 + poly * zero;
-    fwd_chunk_ct<BL, BL - 1, K1>(tb, q, n8q, [&](uint32_t j) { return src[j]; },
-                                 [&](int, uint32_t j0, auto& x) {
+    const uint64_t* __restrict__ src = pbuf + ((uint64_t)k * 3 + poly) * LN + off;
 #pragma unroll
-                                   for (int m = 0; m < (1 << K1); ++m) sm[j0 + (m << (BL - K1))] = x[m];
-                                 });
+    for (int r = 0; r < NS1; ++r) {  // first chunk: one group, block-uniform twiddles
+      uint64_t x[M1];
+#pragma unroll
+      for (int m = 0; m < M1; ++m) x[m] = src[threadIdx.x + 256u * r + (m << D1)];
+      fwd_set_ct<BL, BL - 1, K1>(x, 0u, tb, q, n8q);
+#pragma unroll
+      for (int m = 0; m < M1; ++m) sm[lds_slot<SW>(threadIdx.x + 256u * r + (m << D1))] = x[m];
+    }
     __syncthreads();
     fwd_chunk_ct<BL, BL - 1 - K1, K2>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << (BL - K1 - K2))] = x[m];
+      for (int m = 0; m < (1 << K2); ++m) sm[lds_slot<SW>(j0 + (m << (BL - K1 - K2)))] = x[m];
     });
     __syncthreads();
     fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (BL - K1 - K2 - K3))] = x[m];
+      for (int m = 0; m < (1 << K3); ++m) sm[lds_slot<SW>(j0 + (m << (BL - K1 - K2 - K3)))] = x[m];
     });
     __syncthreads();
     // last chunk (contiguous sets of ML, written inline: V captured by a lambda would
@@ -800,7 +809,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(const uint64_t* __r
       const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4;
       uint64_t x[ML];
 #pragma unroll
-      for (int m = 0; m < ML; ++m) x[m] = sm[j0 + m];
+      for (int m = 0; m < ML; ++m) x[m] = sm[lds_slot<SW>(j0 + (m & ~3)) + (m & 3)];
       fwd_set_ct<BL, K4 - 1, K4>(x, g, tb, q, n8q);
       if (poly == 0) {  // NTT(v), lazy (< 12q): only ever a Shoup multiplicand
 #pragma unroll
@@ -851,23 +860,23 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint64_t* __restrict__ c1 = c0 + LN;
   const uint64_t* __restrict__ s = sk + off;
   const uint64_t* __restrict__ ss = sksh + off;
-  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  const auto lds_ld = [&](uint32_t j) { return sm[lds_slot<true>(j)]; };
   // first chunk: contiguous sets of 2^K1 (T0 = 0)
   inv_chunk_ct<BL, 0, K1>(tb, q, n4q,
                           [&](uint32_t j) { return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q); },
                           [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-                            for (int m = 0; m < (1 << K1); ++m) sm[j0 + m] = x[m];
+                            for (int m = 0; m < (1 << K1); ++m) sm[lds_slot<true>(j0 + (m & ~3)) + (m & 3)] = x[m];
                           });
   __syncthreads();
   inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << K1)] = x[m];
+    for (int m = 0; m < (1 << K2); ++m) sm[lds_slot<true>(j0 + (m << K1))] = x[m];
   });
   __syncthreads();
   inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (K1 + K2))] = x[m];
+    for (int m = 0; m < (1 << K3); ++m) sm[lds_slot<true>(j0 + (m << (K1 + K2)))] = x[m];
   });
   __syncthreads();
   uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
@@ -1409,10 +1418,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
   if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
-    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2, true, 5>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
-    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3, true, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
   else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,

@@ -2,7 +2,7 @@
 """Device encrypt (and decrypt) time per ciphertext under two settings of a launch-time
 switch (the environment variable named by VAR, read by the launch code under test), alternated A/B/A/B in one
 process, with the seeded ciphertexts checked bit-identical between the settings.
-  VAR=SHELFI_ENC_PARK BATCH=16384 DEPTH=3 K=238 python tools/enc_variant_probe.py"""
+  VAR=SHELFI_ENC_PARK BATCH=16384 DEPTH=3 K=238 [VALS=0,1] python tools/enc_variant_probe.py"""
 import os
 import sys
 import time
@@ -25,11 +25,12 @@ def main():
     B = inf["batch"]
     g = torch.Generator(device="cuda").manual_seed(3)
     x = (torch.rand(K * B, generator=g, device="cuda", dtype=torch.float64) * 2 - 1)
+    vals = os.environ.get("VALS", "0,1").split(",")
     outs = {}
-    times = {"0": [], "1": []}
-    dtimes = {"0": [], "1": []}
+    times = {v: [] for v in vals}
+    dtimes = {v: [] for v in vals}
     for rep in range(3):
-        for v in ("0", "1"):
+        for v in vals:
             os.environ[var] = v
             ck.set_seed(11)
             out = D.encrypt(ck, x)  # warm (allocations)
@@ -52,13 +53,14 @@ def main():
                 ds.append(time.perf_counter() - t0)
             dtimes[v].append(sorted(ds)[2] * 1e3 / K)
             outs[v] = out.clone()
-    same = bool(torch.equal(outs["0"], outs["1"]))
+    same = all(torch.equal(outs[vals[0]], outs[v]) for v in vals)
     err = float((dec - x).abs().max())
-    print("%s N=%d L=%d K=%d  encrypt ms/ct: 0 %s | 1 %s   decrypt ms/ct: 0 %s | 1 %s  identical=%s "
-          "max|dec-x|=%.2e" % (var, inf["ring_dim"], inf["num_towers"], K,
-                               ["%.5f" % t for t in times["0"]], ["%.5f" % t for t in times["1"]],
-                               ["%.5f" % t for t in dtimes["0"]], ["%.5f" % t for t in dtimes["1"]],
-                               same, err), flush=True)
+    print("%s N=%d L=%d K=%d identical=%s max|dec-x|=%.2e" % (var, inf["ring_dim"], inf["num_towers"], K,
+                                                             same, err))
+    for v in vals:
+        print("  %s=%-4s encrypt ms/ct %s   decrypt ms/ct %s" % (
+            var, v, " ".join("%.5f" % t for t in times[v]), " ".join("%.5f" % t for t in dtimes[v])),
+              flush=True)
 
 
 if __name__ == "__main__":
