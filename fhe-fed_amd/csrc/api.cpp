@@ -245,6 +245,8 @@ static void build_tables(shelfi_ctx* ctx) {
       }
     c.qhat_inv = invmod(qhat_mod, q);
     c.qhat_inv_shoup = shoup(c.qhat_inv, q);
+    c.ninv_qhat = (uint64_t)(((u128)c.ninv * c.qhat_inv) % q);
+    c.ninv_qhat_shoup = shoup(c.ninv_qhat, q);
     c.qhat_lo = (uint64_t)qhat128;
     c.qhat_hi = (uint64_t)(qhat128 >> 64);
     c.inv_q = 1.0 / (double)q;

@@ -744,20 +744,12 @@ __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, 
   }
 }
 
-// LDS slot of element i in the compile-time block passes: XOR of bits 2-4 with the
-// row (i >> 5) & 7, so the strided sets of the middle chunks (stride 4: 16 lanes on the
-// same 4 slots) spread over all 32 eight-byte slots; groups of 4 stay contiguous.
-template <bool SW>
-__device__ __forceinline__ uint32_t lds_slot(uint32_t i) {
-  return SW ? i ^ (((i >> 5) & 7u) << 2) : i;
-}
-
 // Encrypt's blocks pass at compile-time shape: chunks K1..K4 (sum BL) per polynomial,
 // the first on registers loaded straight from pbuf, the last combined with the public key straight
 // from registers (3 LDS round trips and 3 barriers per polynomial instead of 5 and 5).
 // Same contract as ntt_fwd_blocks_enc.
-template <int BL, int K1, int K2, int K3, int K4, bool SW, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void ntt_fwd_blocks_enc_ct(
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
     const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
     const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk,
     const uint64_t* __restrict__ pksh, uint64_t* __restrict__ ct, uint32_t zero) {
@@ -774,7 +766,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const ulonglong2* tb0 = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
-  const auto lds_ld = [&](uint32_t j) { return sm[lds_slot<SW>(j)]; };
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
   uint64_t V[NSL][ML];  // NTT(v) at this thread's last-chunk positions
 #pragma unroll 1
   for (int poly = 0; poly < 3; ++poly) {
@@ -789,17 +781,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       for (int m = 0; m < M1; ++m) x[m] = src[threadIdx.x + 256u * r + (m << D1)];
       fwd_set_ct<BL, BL - 1, K1>(x, 0u, tb, q, n8q);
 #pragma unroll
-      for (int m = 0; m < M1; ++m) sm[lds_slot<SW>(threadIdx.x + 256u * r + (m << D1))] = x[m];
+      for (int m = 0; m < M1; ++m) sm[threadIdx.x + 256u * r + (m << D1)] = x[m];
     }
     __syncthreads();
     fwd_chunk_ct<BL, BL - 1 - K1, K2>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K2); ++m) sm[lds_slot<SW>(j0 + (m << (BL - K1 - K2)))] = x[m];
+      for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << (BL - K1 - K2))] = x[m];
     });
     __syncthreads();
     fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K3); ++m) sm[lds_slot<SW>(j0 + (m << (BL - K1 - K2 - K3)))] = x[m];
+      for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (BL - K1 - K2 - K3))] = x[m];
     });
     __syncthreads();
     // last chunk (contiguous sets of ML, written inline: V captured by a lambda would
@@ -809,7 +801,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4;
       uint64_t x[ML];
 #pragma unroll
-      for (int m = 0; m < ML; ++m) x[m] = sm[lds_slot<SW>(j0 + (m & ~3)) + (m & 3)];
+      for (int m = 0; m < ML; ++m) x[m] = sm[j0 + m];
       fwd_set_ct<BL, K4 - 1, K4>(x, g, tb, q, n8q);
       if (poly == 0) {  // NTT(v), lazy (< 12q): only ever a Shoup multiplicand
 #pragma unroll
@@ -860,23 +852,23 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint64_t* __restrict__ c1 = c0 + LN;
   const uint64_t* __restrict__ s = sk + off;
   const uint64_t* __restrict__ ss = sksh + off;
-  const auto lds_ld = [&](uint32_t j) { return sm[lds_slot<true>(j)]; };
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
   // first chunk: contiguous sets of 2^K1 (T0 = 0)
   inv_chunk_ct<BL, 0, K1>(tb, q, n4q,
                           [&](uint32_t j) { return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q); },
                           [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-                            for (int m = 0; m < (1 << K1); ++m) sm[lds_slot<true>(j0 + (m & ~3)) + (m & 3)] = x[m];
+                            for (int m = 0; m < (1 << K1); ++m) sm[j0 + m] = x[m];
                           });
   __syncthreads();
   inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K2); ++m) sm[lds_slot<true>(j0 + (m << K1))] = x[m];
+    for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << K1)] = x[m];
   });
   __syncthreads();
   inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K3); ++m) sm[lds_slot<true>(j0 + (m << (K1 + K2)))] = x[m];
+    for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (K1 + K2))] = x[m];
   });
   __syncthreads();
   uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
@@ -1418,10 +1410,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
   if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
-    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2, true, 5>), dim3((uint32_t)nbb), dim3(256), 0, s,
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
-    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3, true, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
+    hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
   else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
@@ -1509,6 +1501,98 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
   __syncthreads();
   const uint32_t a = threadIdx.x >> 4, b = threadIdx.x & 15;
   fbuf[k * S + ((a << (logS - 4)) | (bitrev_dev(mid, logS - 8) << 4) | b)] = tile[a][b];
+}
+
+// Decrypt's last INTT pass fused with the exact CRT decode (ntt_inv_cols + crt_decode_kernel
+// without the round trip of the [K][L][N] residues through HBM).  A workgroup owns 64
+// columns (coefficients j = c + BLK r, r < R) of one ciphertext for every tower: wave w
+// runs the top LOGR stages of towers t = w, w + 4, ... and leaves y_t = b_t (N^-1 (Q/q_t)^-1)
+// mod q_t in LDS; then each (real, imaginary) coefficient pair (r, r + R/2) is
+// CRT-reconstructed exactly as crt_decode_kernel does (same operation order) and stored
+// at bitrev(slot).  Needs L R 512 B of LDS <= kCrtFuseLds and gap = N / 2S <= 64.
+constexpr size_t kCrtFuseLds = 48 << 10;
+template <int LOGR>
+__global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restrict__ dbuf, uint32_t L,
+                                                        uint32_t logN, uint32_t logS,
+                                                        const uint64_t* __restrict__ tw,
+                                                        const uint64_t* __restrict__ twp,
+                                                        const TowerConst* __restrict__ tcs, uint64_t Qlo,
+                                                        uint64_t Qhi, double inv_scale,
+                                                        double2* __restrict__ fbuf) {
+  constexpr int R = 1 << LOGR, CW = 64;
+  extern __shared__ uint64_t ys_flat[];  // [L][R][CW]
+  uint64_t(*ys)[R][CW] = reinterpret_cast<uint64_t(*)[R][CW]>(ys_flat);
+  const uint32_t N = 1u << logN, BLK = N >> LOGR, S = 1u << logS;
+  const uint32_t cpb = BLK / CW;
+  const uint64_t k = blockIdx.x / cpb;
+  const uint32_t c0 = (blockIdx.x % cpb) * CW;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll 1
+  for (uint32_t t = wv; t < L; t += 4) {
+    const TowerConst& c = tcs[t];
+    const uint64_t q = c.q;
+    const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
+    const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
+    const uint64_t* __restrict__ a = dbuf + ((k * L + t) << logN) + c0 + lane;
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = a[(uint64_t)r * BLK];
+#pragma unroll
+    for (int v = 0; v < LOGR; ++v) {
+      const int tr = 1 << v, h = R >> (v + 1);
+#pragma unroll
+      for (int i = 0; i < h; ++i) {
+        const uint64_t W = w[h + i], Wp = wp[h + i];
+#pragma unroll
+        for (int jj = 0; jj < tr; ++jj) gs_bfly_s(x[2 * i * tr + jj], x[2 * i * tr + jj + tr], W, Wp, q, c.n4q);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) ys[t][r][lane] = canon4(shoup_lazy(x[r], c.ninv_qhat, c.ninv_qhat_shoup, q), q);
+  }
+  __syncthreads();
+  const uint32_t gapLog = logN - 1 - logS, gap = 1u << gapLog;
+  // pair p -> half-row r (< R/2) fastest, so 8 consecutive threads store 8 consecutive
+  // bit-reversed slots (one 128-byte segment)
+#pragma unroll 1
+  for (uint32_t p = threadIdx.x; p < (uint32_t)(R / 2) * CW; p += 256) {
+    const uint32_t r = p % (R / 2), u = p / (R / 2);
+    const uint32_t col = c0 + u;
+    if (col & (gap - 1)) continue;  // coefficient not on a slot
+    double res[2];
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const uint32_t rr = r + part * (R / 2);
+      double frac = 0.0;
+      uint64_t xlo = 0, xhi = 0;
+#pragma unroll 1
+      for (uint32_t t = 0; t < L; ++t) {
+        const TowerConst& c = tcs[t];
+        const uint64_t y = ys[t][rr][u];
+        frac += (double)y * c.inv_q;
+        const uint64_t plo = y * c.qhat_lo;
+        const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
+        xlo += plo;
+        xhi += phi + (xlo < plo ? 1 : 0);
+      }
+      const uint64_t kk = (uint64_t)(frac + 0.5);
+      const uint64_t slo = kk * Qlo;
+      const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
+      const uint64_t borrow = xlo < slo ? 1 : 0;
+      xlo -= slo;
+      xhi = xhi - shi - borrow;
+      const bool neg = (int64_t)xhi < 0;
+      if (neg) {
+        xlo = ~xlo + 1;
+        xhi = ~xhi + (xlo == 0 ? 1 : 0);
+      }
+      double v = __dadd_rn(__dmul_rn((double)xhi, 18446744073709551616.0), (double)xlo);
+      if (neg) v = -v;
+      res[part] = __dmul_rn(v, inv_scale);
+    }
+    const uint32_t i = (col + BLK * r) >> gapLog;
+    fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
+  }
 }
 
 // ------------------------------------------------- decode noise flooding ----
@@ -1643,10 +1727,14 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
-  // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts)
+  // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts); the
+  // last pass fused with the CRT decode where its shape allows
+  const uint32_t blkLog = ntt_block_log(p.logN);
+  const int logR = (int)(p.logN - blkLog);
+  const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
+  const bool fuse = logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
+                    ((p.N >> logR) % 64) == 0;
   {
-    const uint32_t blkLog = ntt_block_log(p.logN);
-    const int logR = (int)(p.logN - blkLog);
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
     if (logR > 0 && blkLog == 11 && dt.red_ok)
@@ -1659,16 +1747,21 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
                          logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh);
-    if (logR > 0) {
+    if (logR > 0 && fuse) {
+      const uint64_t nbf = K * ((p.N >> logR) / 64);
+      NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, logS,
+                   dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale, fbuf);
+    } else if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, dbuf, p.L, p.logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
     }
     SHELFI_HIP(hipGetLastError());
   }
   const uint64_t slots = K * (uint64_t)p.batch;
-  hipLaunchKernelGGL(crt_decode_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, s,
-                     dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
-                     fbuf);
+  if (!fuse)
+    hipLaunchKernelGGL(crt_decode_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, s,
+                       dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
+                       fbuf);
   SHELFI_HIP(hipGetLastError());
   if (dn && dn->enabled) {
     Key8 k8;
@@ -1678,15 +1771,15 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        dn->flags);
     SHELFI_HIP(hipGetLastError());
   }
-  const uint32_t blkLog = fft_block_log(logS);
-  const int logR = (int)(logS - blkLog);
-  const size_t lds = sizeof(double2) << blkLog;
-  hipLaunchKernelGGL(fft_fwd_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, fbuf, logS,
-                     blkLog, dt.fft_fwd, out, n, logR == 0 ? 1 : 0);
+  const uint32_t fblkLog = fft_block_log(logS);
+  const int flogR = (int)(logS - fblkLog);
+  const size_t lds = sizeof(double2) << fblkLog;
+  hipLaunchKernelGGL(fft_fwd_blocks, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
+                     fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0);
   SHELFI_HIP(hipGetLastError());
-  if (logR > 0) {
-    const uint64_t nb = K * ((p.batch >> logR) / 256);
-    FFT_DISPATCH(logR, fft_fwd_cols, dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd,
+  if (flogR > 0) {
+    const uint64_t nb = K * ((p.batch >> flogR) / 256);
+    FFT_DISPATCH(flogR, fft_fwd_cols, dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd,
                  out, n);
     SHELFI_HIP(hipGetLastError());
   }

@@ -80,7 +80,7 @@ struct TowerConst {
   // any u64 x -> [0, 2q): k = (x_hi * red_r) >> (32 + red_sh), x - k q (red_any; needs
   // q >= 2^40, red_ok): red_r = floor(2^(32 + E) / q) < 2^32, E = bitlength(q) - 1
   uint32_t red_r, red_sh, red_ok, pad32;
-  uint64_t pad[2];
+  uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
 };
 
 struct DeviceTables {
