@@ -13,9 +13,11 @@
 //   enc_prep_kernel    round/scale the encoded slots + ChaCha20 sampling of (v, e0, e1)
 //                      into a compact 10-byte record per coefficient (ckks.cpp:80-81)
 //   ntt_fwd_cols_enc   expand the record per tower + first NTT stages
-//   ntt_fwd_blocks_enc last NTT stages of v, m+e0, e1 + c0 = v*b + (m+e0), c1 = v*a + e1
-//   ntt_inv_blocks     (decrypt) c0 + c1*s formed in its LDS fill (ckks.cpp:189)
-//   crt_decode_kernel  exact centered CRT -> double / scale, bit-reversed scatter
+//   ntt_fwd_blocks_enc(_ct)  last NTT stages of v, m+e0, e1 + c0 = v*b + (m+e0), c1 = v*a + e1
+//                      (_ct: compile-time shape over per-block twiddle slices)
+//   ntt_inv_blocks(_dec_ct)  (decrypt) c0 + c1*s formed on load (ckks.cpp:189) + first INTT stages
+//   ntt_inv_cols_crt   last INTT stages fused with the exact centered CRT -> double / scale
+//   crt_decode_kernel  the CRT alone (shapes the fused kernel does not cover)
 //   keygen_*           ternary s, Gaussian e, uniform a; b = e - a*s
 //
 // 64-bit modular arithmetic: CDNA4 has no 64x64->128 multiply; products are
