@@ -65,6 +65,10 @@ def parse():
                          "combines the partial sums (BASELINE config 3); cts = each rank aggregates every "
                          "learner's slice of the ciphertexts (no collective; the host routes each upload's "
                          "ciphertext ranges to their ranks)")
+    ap.add_argument("--combine", choices=["torch", "shelfi"], default="torch",
+                    help="learner-sharded combine: torch = pipelined torch.distributed reduce_scatter + "
+                         "modq; shelfi = the library's own RCCL communicator through the C ABI "
+                         "(shelfi_dev_reduce_scatter, one collective after the local wavg)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -80,6 +84,31 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
                     help="PMC-derived HBM bytes per wavg launch (from tools/pmc_traffic.py)")
     return ap.parse_args()
+
+
+class ShelfiCombine:
+    """Learner-sharded combine through the C ABI (include/shelfi.h): local wavg into a
+    partial padded to a multiple of the world size, then shelfi_dev_reduce_scatter (RCCL
+    uint64 SUM + mod-q fold inside the library).  Same result as PipelinedCombine."""
+
+    def __init__(self, ck, K, ct_shape, dev):
+        import torch
+        import torch.distributed as dist
+
+        from SHELFI_FHE import dist as SD
+
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.K, self.per = K, -(-K // self.world)
+        self.partial = torch.zeros((self.per * self.world,) + tuple(ct_shape), dtype=torch.int64, device=dev)
+        self.share = torch.empty((self.per,) + tuple(ct_shape), dtype=torch.int64, device=dev)
+        self.comm = SD.Comm(ck, self.rank, self.world)
+
+    def run(self, compute_piece, fold_share=None):
+        compute_piece(0, self.K, self.partial[:self.K])
+        self.comm.reduce_scatter(self.partial, out=self.share)
+        a, b = self.rank * self.per, min(self.K, (self.rank + 1) * self.per)
+        return [(a, b, self.share[:b - a])] if b > a else []
 
 
 def check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8):
@@ -278,7 +307,11 @@ def main():
         if args.layout == "arena":
             cts = None
         out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
-        comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev) if shard == "learners" else None
+        comb = None
+        if shard == "learners" and args.combine == "torch":
+            comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
+        elif shard == "learners":
+            comb = ShelfiCombine(ck, K, (2, L, N), dev)
 
         def kernel():
             if args.layout == "arena":
@@ -457,7 +490,9 @@ def main():
                                                   "" if not distributed else
                                                   (", ciphertext-sharded: each rank aggregates all %d learners' "
                                                    "cts [k0, k1), no collective" % (Cl * world)) if cts_mode else
-                                                  ", RCCL reduce_scatter overlapped in %d pieces" % args.pieces),
+                                                  (", RCCL reduce_scatter overlapped in %d pieces" % args.pieces
+                                                   if args.combine == "torch" else
+                                                   ", RCCL reduce_scatter through shelfi_dev_reduce_scatter")),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
                    "parallelism": ("ciphertext-sharded dp%d" if cts_mode else "learner-sharded dp%d") % world,
                    "layout": args.layout},

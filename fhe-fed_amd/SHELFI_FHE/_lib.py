@@ -112,6 +112,13 @@ SIGNATURES = {
     "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
     "shelfi_dev_modq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "shelfi_comm_unique_id": (C.c_int, [u8p]),
+    "shelfi_comm_init": (C.c_int, [C.c_void_p, u8p, C.c_int, C.c_int]),
+    "shelfi_comm_destroy": (C.c_int, [C.c_void_p]),
+    "shelfi_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "shelfi_dev_reduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
+    "shelfi_dev_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "shelfi_dev_reduce_scatter": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_encrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_size_t,
                                      C.c_void_p, C.c_void_p]),

@@ -175,3 +175,104 @@ def slice_of_rank(K: int, world: int, rank: int):
     slices, the last rank possibly shorter)."""
     per = -(-K // world)
     return min(K, rank * per), min(K, (rank + 1) * per)
+
+
+class Comm:
+    """The library's own RCCL communicator (C ABI: shelfi_comm_* / shelfi_dev_reduce*),
+    bound to a CKKS context's GPU.  The torch.distributed path above (reduce_partials)
+    and this one compute the same bit-identical combine; this one is what a host
+    without PyTorch (C++, cgo, JNI, ...) drives through include/shelfi.h.
+
+    The 128-byte unique id is made on rank 0 and handed to the others out of band:
+    pass `unique_id` yourself, or a torch.distributed `group` (any backend, e.g. gloo)
+    to broadcast it.  Collective methods must be called by every rank in the same order."""
+
+    def __init__(self, ckks, rank: int, world: int, unique_id: bytes = None, group=None):
+        from ._lib import load
+
+        lib = load()
+        if unique_id is None:
+            if world == 1:
+                unique_id = make_unique_id()
+            else:
+                import torch.distributed as dist
+
+                box = [make_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(box, src=0, group=group)
+                unique_id = box[0]
+        if len(unique_id) != COMM_ID_BYTES:
+            raise ValueError("unique id must be %d bytes" % COMM_ID_BYTES)
+        import ctypes as C
+
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(unique_id)
+        self._ckks = ckks
+        self.rank, self.world = rank, world
+        _check(lib.shelfi_comm_init(ckks._ctx, buf, int(rank), int(world)), "comm_init")
+
+    def _call(self, name, *args):
+        from ._lib import load
+
+        _check(getattr(load(), name)(self._ckks._ctx, *args), name)
+
+    def reduce(self, partial, root: int = 0):
+        """In place; the combined aggregate (mod q) lands on `root`."""
+        import ctypes as C
+        from .device import _check_ct, _stream_ptr
+
+        _check_ct(partial, self._ckks)
+        self._call("shelfi_dev_reduce", C.c_void_p(partial.data_ptr()), partial.shape[0], int(root),
+                   C.c_void_p(_stream_ptr(partial)))
+        return partial
+
+    def allreduce(self, partial):
+        """In place; the combined aggregate (mod q) on every rank."""
+        import ctypes as C
+        from .device import _check_ct, _stream_ptr
+
+        _check_ct(partial, self._ckks)
+        self._call("shelfi_dev_allreduce", C.c_void_p(partial.data_ptr()), partial.shape[0],
+                   C.c_void_p(_stream_ptr(partial)))
+        return partial
+
+    def reduce_scatter(self, partial, out=None):
+        """This rank's ciphertexts [r K/W, (r+1) K/W) of the combined aggregate (K % W == 0)."""
+        import ctypes as C
+        from .device import _check_ct, _stream_ptr, empty_ct
+
+        _check_ct(partial, self._ckks)
+        K = partial.shape[0]
+        if K % self.world:
+            raise ValueError("reduce_scatter needs K divisible by the world size")
+        if out is None:
+            out = empty_ct(self._ckks, K // self.world, device=partial.device)
+        _check_ct(out, self._ckks, K // self.world)
+        self._call("shelfi_dev_reduce_scatter", C.c_void_p(partial.data_ptr()), K,
+                   C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(out)))
+        return out
+
+    def close(self):
+        if self._ckks is not None and self._ckks._ctx:
+            from ._lib import load
+
+            load().shelfi_comm_destroy(self._ckks._ctx)
+        self._ckks = None
+
+
+COMM_ID_BYTES = 128
+
+
+def make_unique_id() -> bytes:
+    """shelfi_comm_unique_id: a fresh RCCL unique id (rank 0)."""
+    import ctypes as C
+
+    from ._lib import load
+
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check(load().shelfi_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+def _check(rc, what):
+    from ._lib import check
+
+    check(rc, what)

@@ -550,6 +550,7 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
+    comm_release(ctx);
     free_keys(ctx);
     free_tables(ctx);
     delete ctx->stage;

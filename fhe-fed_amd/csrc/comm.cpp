@@ -1,0 +1,217 @@
+// comm.cpp — the C-ABI multi-GPU combine over RCCL (SURVEY §8 b/e): per-context
+// communicator, and the uint64 SUM reduce / allreduce / reduce-scatter of per-rank
+// partial aggregates followed by the mod-q fold.
+//
+// Why this is exact: each rank's partial is sum_{c in rank} W_c ct_c mod q_t, a residue
+// below q_t < 2^60; a uint64 sum of W <= 16 of them stays below 2^64, and EvalAdd is
+// order-independent, so RCCL's reduction order (ring, tree) cannot change the result.
+// The fold back into [0, q_t) is launch_modq (kernels.hip).
+//
+// RCCL is opened with dlopen(RTLD_LOCAL | RTLD_DEEPBIND) on first use, from the ROCm
+// install this library's HIP runtime comes from: a PyTorch process already carries its
+// own librccl (same soname, built against its own HIP runtime), and a stream of ours
+// must not reach a communicator of theirs.  Nothing here runs unless a communicator is
+// created, so single-GPU users never load RCCL.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/shelfi.h"
+#include "shelfi_internal.h"
+
+namespace shelfi {
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclReduce) reduce = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string load_error;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* env = getenv("SHELFI_RCCL_LIB");
+    const char* cands[] = {env, "/opt/rocm/lib/librccl.so.1", "librccl.so.1"};
+    for (const char* path : cands) {
+      if (!path || !*path) continue;
+      r.handle = dlopen(path, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+      if (r.handle) break;
+      r.load_error = dlerror();
+    }
+    if (!r.handle) return;
+#define SHELFI_SYM(field, name)                                                  \
+  r.field = reinterpret_cast<decltype(r.field)>(dlsym(r.handle, #name));          \
+  if (!r.field) {                                                                \
+    r.load_error = std::string("librccl lacks ") + #name;                        \
+    r.handle = nullptr;                                                          \
+    return;                                                                      \
+  }
+    SHELFI_SYM(get_unique_id, ncclGetUniqueId)
+    SHELFI_SYM(comm_init_rank, ncclCommInitRank)
+    SHELFI_SYM(comm_destroy, ncclCommDestroy)
+    SHELFI_SYM(reduce, ncclReduce)
+    SHELFI_SYM(all_reduce, ncclAllReduce)
+    SHELFI_SYM(reduce_scatter, ncclReduceScatter)
+    SHELFI_SYM(error_string, ncclGetErrorString)
+#undef SHELFI_SYM
+  });
+  if (!r.handle) throw Error{SHELFI_ERR_DEVICE, "RCCL unavailable: " + r.load_error};
+  return r;
+}
+
+void check(ncclResult_t rc, const char* what) {
+  if (rc != ncclSuccess)
+    throw Error{SHELFI_ERR_DEVICE, std::string(what) + ": " + rccl().error_string(rc)};
+}
+
+template <class F>
+int guarded_comm(F&& f) {
+  try {
+    f();
+    return SHELFI_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return SHELFI_ERR_DEVICE;
+  }
+}
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    SHELFI_HIP(hipSetDevice(dev));
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+ncclComm_t comm_of(shelfi_ctx* ctx) {
+  if (!ctx->comm) throw Error{SHELFI_ERR_STATE, "no communicator: call shelfi_comm_init first"};
+  return reinterpret_cast<ncclComm_t>(ctx->comm);
+}
+
+}  // namespace
+
+void comm_release(shelfi_ctx* ctx) {
+  if (ctx && ctx->comm) {
+    (void)rccl().comm_destroy(reinterpret_cast<ncclComm_t>(ctx->comm));
+    ctx->comm = nullptr;
+    ctx->comm_rank = 0;
+    ctx->comm_world = 0;
+  }
+}
+
+}  // namespace shelfi
+
+using namespace shelfi;
+
+extern "C" {
+
+int shelfi_comm_unique_id(uint8_t* id_out) {
+  if (!id_out) return SHELFI_ERR_ARG;
+  return guarded_comm([&] {
+    static_assert(sizeof(ncclUniqueId) == SHELFI_COMM_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    check(rccl().get_unique_id(&id), "ncclGetUniqueId");
+    std::memcpy(id_out, &id, sizeof(id));
+  });
+}
+
+int shelfi_comm_init(shelfi_ctx* ctx, const uint8_t* id, int rank, int world) {
+  if (!ctx || !id || world < 1 || rank < 0 || rank >= world) return SHELFI_ERR_ARG;
+  if (world > kMaxCommRanks) {
+    set_error("world size above 16: a uint64 sum of the partial aggregates could wrap");
+    return SHELFI_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded_comm([&] {
+    comm_release(ctx);
+    DevGuard g(ctx->device);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t c = nullptr;
+    check(rccl().comm_init_rank(&c, world, uid, rank), "ncclCommInitRank");
+    ctx->comm = c;
+    ctx->comm_rank = rank;
+    ctx->comm_world = world;
+  });
+}
+
+int shelfi_comm_destroy(shelfi_ctx* ctx) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded_comm([&] {
+    DevGuard g(ctx->device);
+    comm_release(ctx);
+  });
+}
+
+int shelfi_dev_reduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, int root, void* stream) {
+  if (!ctx || (K && !partial_dev)) return SHELFI_ERR_ARG;
+  return guarded_comm([&] {
+    ncclComm_t c = comm_of(ctx);
+    if (root < 0 || root >= ctx->comm_world) throw Error{SHELFI_ERR_ARG, "root outside the communicator"};
+    if (!K) return;
+    DevGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t words = K * 2ull * p.L * p.N;
+    check(rccl().reduce(partial_dev, partial_dev, words, ncclUint64, ncclSum, root, c, s), "ncclReduce");
+    if (ctx->comm_rank == root) launch_modq(partial_dev, (uint64_t)K * 2 * p.L, p.L, p.logN, ctx->dt.tc, s);
+  });
+}
+
+int shelfi_dev_allreduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, void* stream) {
+  if (!ctx || (K && !partial_dev)) return SHELFI_ERR_ARG;
+  return guarded_comm([&] {
+    ncclComm_t c = comm_of(ctx);
+    if (!K) return;
+    DevGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t words = K * 2ull * p.L * p.N;
+    check(rccl().all_reduce(partial_dev, partial_dev, words, ncclUint64, ncclSum, c, s), "ncclAllReduce");
+    launch_modq(partial_dev, (uint64_t)K * 2 * p.L, p.L, p.logN, ctx->dt.tc, s);
+  });
+}
+
+int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size_t K, uint64_t* out_dev,
+                              void* stream) {
+  if (!ctx || (K && (!partial_dev || !out_dev))) return SHELFI_ERR_ARG;
+  return guarded_comm([&] {
+    ncclComm_t c = comm_of(ctx);
+    const size_t W = (size_t)ctx->comm_world;
+    if (K % W) throw Error{SHELFI_ERR_ARG, "reduce_scatter needs K divisible by the world size"};
+    if (!K) return;
+    DevGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t Ks = K / W, words = Ks * 2ull * p.L * p.N;
+    check(rccl().reduce_scatter(partial_dev, out_dev, words, ncclUint64, ncclSum, c, s), "ncclReduceScatter");
+    launch_modq(out_dev, (uint64_t)Ks * 2 * p.L, p.L, p.logN, ctx->dt.tc, s);
+  });
+}
+
+int shelfi_comm_info(const shelfi_ctx* ctx, int* rank, int* world) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  if (rank) *rank = ctx->comm ? ctx->comm_rank : -1;
+  if (world) *world = ctx->comm ? ctx->comm_world : 0;
+  return SHELFI_OK;
+}
+
+}  // extern "C"

@@ -30,6 +30,7 @@ struct Error {
 
 // ----------------------------------------------------------- host params ----
 constexpr int kMaxTowers = 16;
+constexpr int kMaxCommRanks = 16;  // W partials below q < 2^60 sum exactly in a uint64
 constexpr int kFftBlockLog = 10;     // complex f64 block staged in LDS by FFT pass 2
 constexpr int kFftBlockLogBig = 11;  // batch >= 2^15: 32 KiB blocks keep pass 1 at 16 columns
 inline uint32_t fft_block_log(uint32_t logS) {
@@ -152,6 +153,9 @@ struct shelfi_ctx {
   size_t scratch_bytes = 0;
   void* io = nullptr;            // bytes-API staging arena (inputs/outputs)
   size_t io_bytes = 0;
+  // RCCL communicator of the multi-GPU combine (comm.cpp; ncclComm_t, opaque here)
+  void* comm = nullptr;
+  int comm_rank = 0, comm_world = 0;
 };
 
 namespace shelfi {
@@ -196,5 +200,8 @@ size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
 void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
                    uint64_t* pk, void* scratch, hipStream_t s);
 size_t keygen_scratch_bytes(const Params& p);
+
+// comm.cpp: drop the context's RCCL communicator (if any)
+void comm_release(shelfi_ctx* ctx);
 
 }  // namespace shelfi

@@ -193,6 +193,30 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
 /* Folds a collective's uint64 SUM of G <= 15 reduced partial sums back into [0, q_t)
  * (multi-GPU combine: local shelfi_dev_wavg -> RCCL reduce/reduce_scatter -> this). */
 int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream);
+/* ---- multi-GPU combine over RCCL (one process per GPU, SURVEY §8 e) --------
+ * Each rank aggregates its own learners with shelfi_dev_wavg / _arena into a partial
+ * of K ciphertexts; these calls combine the partials exactly (uint64 SUM over <= 16
+ * ranks, then the mod-q fold of shelfi_dev_modq), bit-identical to aggregating every
+ * learner on one GPU.  Collective: every rank of the communicator makes the same call
+ * in the same order.  Replaces, for the multi-GPU path, the serial EvalAdd loop of
+ * CKKS::computeWeightedAverage (ckks.cpp:291-297). */
+#define SHELFI_COMM_ID_BYTES 128
+/* rank 0 makes the 128-byte id and hands it to every rank out of band */
+int shelfi_comm_unique_id(uint8_t* id_out);
+/* bind a communicator of `world` (<= 16) ranks to ctx (its device), replacing any previous one */
+int shelfi_comm_init(shelfi_ctx* ctx, const uint8_t* id, int rank, int world);
+int shelfi_comm_destroy(shelfi_ctx* ctx);
+/* rank/world of ctx's communicator (-1 / 0 if none) */
+int shelfi_comm_info(const shelfi_ctx* ctx, int* rank, int* world);
+/* in place: the combined aggregate lands on `root` (other ranks' buffers are scratch) */
+int shelfi_dev_reduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, int root, void* stream);
+/* in place: the combined aggregate on every rank */
+int shelfi_dev_allreduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, void* stream);
+/* rank r receives ciphertexts [r K/W, (r+1) K/W) of the combined aggregate in out_dev
+ * (K % W == 0): each rank then decrypts its own slice, nothing is gathered */
+int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size_t K,
+                              uint64_t* out_dev, void* stream);
+
 /* encode + encrypt n doubles (device) into K = ceil(n/batch) ciphertexts. */
 int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
                        void* stream);

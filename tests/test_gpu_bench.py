@@ -65,3 +65,13 @@ def test_bench_ciphertext_sharded_path_one_rank():
     assert r["check"]["max_abs_err"] < 1e-8
     alt = r["alternative_partitioning"]
     assert "RCCL" in alt["parallelism"] and alt["check"]["max_abs_err"] < 1e-8
+
+
+def test_bench_learner_sharded_c_abi_combine_one_rank():
+    """--combine shelfi: the learner-sharded step through the library's own RCCL
+    communicator (shelfi_comm_init / shelfi_dev_reduce_scatter), id broadcast over the
+    torch process group; bench's end-to-end check on the owned aggregate."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
+              "--force-dist", "--shard", "learners", "--combine", "shelfi", "--no-alt"] + COMMON)
+    assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
