@@ -217,9 +217,7 @@ class CKKS(Scheme):
             print("Error: learner_data and scaling_factors size mismatch")
             return b""
         blobs = _as_bytes_list(learner_data)
-        C_ = len(blobs)
-        if C_ == 0:
-            raise ValueError("computeWeightedAverage: no learners")
+        C_ = len(blobs)  # 0 learners -> the empty batch (ckks.cpp:273-309)
         w = np.asarray([float(s) for s in scaling_factors], dtype=np.float32)
         arr = (_lib.u8p * C_)()
         lens = (C.c_size_t * C_)()

@@ -1076,6 +1076,20 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
   if (!ctx || !out_len || (C && (!blobs || !lens || !weights))) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
+    if (C == 0) {
+      // ckks.cpp:270-309: with no learners the loop never runs and the empty
+      // vector<Ciphertext> is serialized; here an empty batch in the ctx's wire format
+      // (depth 2 / scale Delta^2: what a weighted average of fresh ciphertexts carries)
+      const bool pal = ctx->wire == 1;
+      const double scale = ctx->p.delta * ctx->p.delta;
+      size_t total = 0;
+      make_output(ctx, pal, 0, 2, 0, scale, nullptr, &total);
+      *out_len = total;
+      if (!out) return;
+      if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
+      make_output(ctx, pal, 0, 2, 0, scale, out, &total);
+      return;
+    }
     DeviceGuard g(ctx->device);
     const std::vector<CtLayout> in = wavg_inputs(ctx, blobs, lens, C);
     const CtLayout& h0 = in.front();

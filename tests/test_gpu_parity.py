@@ -316,6 +316,9 @@ def test_api_behaviour(cfg1, cfg2, capsys):
     e0 = cfg1.encrypt(np.zeros(0))
     assert m.blob_info(e0)["num_cts"] == 0
     assert cfg1.decrypt(e0, 0).shape == (0,)
+    # no learners -> the empty batch (ckks.cpp:273-309 serializes an empty vector)
+    agg0 = cfg1.computeWeightedAverage([], [])
+    assert m.blob_info(agg0)["num_cts"] == 0 and cfg1.decrypt(agg0, 0).shape == (0,)
     # float32 / list inputs are widened like py::array_t<double> forcecast
     d = cfg1.decrypt(cfg1.encrypt([0.25, -0.5, 1.0]), 3)
     assert np.allclose(d, [0.25, -0.5, 1.0], atol=1e-9)
