@@ -1346,6 +1346,18 @@ int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream) 
   });
 }
 
+// Ciphertexts per launch chain of the device-resident encrypt/decrypt: as many as a
+// 4 GiB scratch holds (1149 at N = 2^15, L = 4: one chain for a ResNet-18 learner),
+// split into equal chunks, so no launch runs a short tail chunk.
+// SHELFI_DEV_CHUNK_MIB overrides the budget (read per call, for A/B probes).
+static uint64_t dev_chunk(uint64_t K, size_t scratch_per_ct) {
+  const char* env = getenv("SHELFI_DEV_CHUNK_MIB");
+  const uint64_t mib = env && atoll(env) > 0 ? (uint64_t)atoll(env) : 4096;
+  const uint64_t cap = std::max<uint64_t>(1, (mib << 20) / scratch_per_ct);
+  const uint64_t n = (K + cap - 1) / cap;
+  return n ? (K + n - 1) / n : 1;
+}
+
 int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
                        void* stream) {
   if (!ctx || (n && (!x_dev || !ct_dev))) return SHELFI_ERR_ARG;
@@ -1360,8 +1372,7 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
     uint32_t key[8];
     uint64_t g0;
     draw_key(ctx, K, key, &g0);
-    const uint64_t chunk = std::max<uint64_t>(1, (1024ull << 20) / encrypt_scratch_bytes(p, 1));
-    const uint64_t kc_max = std::min<uint64_t>(chunk, K);
+    const uint64_t kc_max = dev_chunk(K, encrypt_scratch_bytes(p, 1));
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
     SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, s));
     const size_t ct_words = 2ull * p.L * p.N;
@@ -1392,8 +1403,7 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
     hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     const uint64_t Kn = (n + p.batch - 1) / p.batch;
     if (!Kn) return;
-    const uint64_t chunk = std::max<uint64_t>(1, (1024ull << 20) / decrypt_scratch_bytes(p, 1));
-    const uint64_t kc_max = std::min<uint64_t>(chunk, Kn);
+    const uint64_t kc_max = dev_chunk(Kn, decrypt_scratch_bytes(p, 1));
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
     const size_t ct_words = 2ull * p.L * p.N;
     DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
