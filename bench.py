@@ -71,6 +71,9 @@ def parse():
                          "(shelfi_dev_reduce_scatter, one collective after the local wavg)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
+    ap.add_argument("--place-output", type=int, default=8,
+                    help="arena layout, no collective: time this many candidate output buffers before "
+                         "the timed region and keep the fastest placement (0 = one plain buffer)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
@@ -306,8 +309,16 @@ def main():
         torch.cuda.synchronize()
         if args.layout == "arena":
             cts = None
-        out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
         comb = None
+        placement = None
+        if args.layout == "arena" and shard != "learners" and args.place_output > 0:
+            # where the aggregate lands in HBM relative to the arena moves the launch time by
+            # up to 12%: keep the fastest of a few candidate buffers
+            out, cand_ms = arena.place_output(weights, candidates=args.place_output)
+            placement = {"candidates": len(cand_ms), "candidate_launch_ms": cand_ms,
+                         "chosen": cand_ms.index(min(cand_ms))}
+        else:
+            out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
         if shard == "learners" and args.combine == "torch":
             comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
         elif shard == "learners":
@@ -333,7 +344,7 @@ def main():
 
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
                 "enc_times": enc_times, "kernel": kernel, "step": step, "comb": comb, "weights": weights,
-                "cts": cts}
+                "cts": cts, "placement": placement}
 
     def timed(mode):
         """warmup, then exactly `steps` steps between barrier + sync; max over ranks.
@@ -495,7 +506,7 @@ def main():
                                                    ", RCCL reduce_scatter through shelfi_dev_reduce_scatter")),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
                    "parallelism": ("ciphertext-sharded dp%d" if cts_mode else "learner-sharded dp%d") % world,
-                   "layout": args.layout},
+                   "layout": args.layout, "output_placement": main_mode["placement"]},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(enc_ms, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),

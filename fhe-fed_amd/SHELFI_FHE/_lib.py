@@ -111,6 +111,9 @@ SIGNATURES = {
                                        C.c_void_p, C.c_void_p]),
     "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
+    "shelfi_dev_wavg_arena_pick_output": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t,
+                                                    C.POINTER(C.c_void_p), C.c_size_t, C.c_int,
+                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_float), C.c_void_p]),
     "shelfi_dev_modq": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "shelfi_comm_unique_id": (C.c_int, [u8p]),
     "shelfi_comm_init": (C.c_int, [C.c_void_p, u8p, C.c_int, C.c_int]),

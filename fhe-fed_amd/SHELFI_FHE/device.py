@@ -126,6 +126,27 @@ class Arena:
         return out
 
 
+    def place_output(self, weights: Sequence[float], candidates: int = 8, launches: int = 2):
+        """A [K][2][L][N] output buffer placed well for this arena.  The launch time
+        depends on where the output lands in physical HBM relative to the arena (up to
+        12%, reproducible per buffer pair), so `candidates` buffers are
+        allocated side by side, timed (shelfi_dev_wavg_arena_pick_output) and all but the
+        fastest released.  Returns (buffer, per-candidate ms)."""
+        torch = _torch()
+        cands = [torch.empty((self.K, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
+                 for _ in range(max(1, int(candidates)))]
+        ptrs = (C.c_void_p * len(cands))(*[t.data_ptr() for t in cands])
+        w = (C.c_float * self.C)(*[float(x) for x in weights])
+        best = C.c_size_t()
+        ms = (C.c_float * len(cands))()
+        check(_lib.load().shelfi_dev_wavg_arena_pick_output(
+            self.ckks._ctx, C.c_void_p(self.buf.data_ptr()), w, self.C, self.K, ptrs, len(cands),
+            int(launches), C.byref(best), ms, C.c_void_p(_stream_ptr(self.buf))), "arena_pick_output")
+        out = cands[best.value]
+        del cands
+        return out, [round(float(x), 4) for x in ms]
+
+
 def modq(ckks, buf):
     """Fold a collective's uint64 sum of <= 15 partial sums back into [0, q_t)."""
     _check_ct(buf, ckks)

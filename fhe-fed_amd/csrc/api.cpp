@@ -1337,6 +1337,46 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
   });
 }
 
+int shelfi_dev_wavg_arena_pick_output(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w,
+                                      size_t C, size_t K, uint64_t* const* candidates, size_t n,
+                                      int launches, size_t* best, float* ms, void* stream) {
+  if (!ctx || !candidates || !best || !n || launches < 1) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    struct Events {
+      hipEvent_t a = nullptr, b = nullptr;
+      ~Events() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+      }
+    } ev;
+    SHELFI_HIP(hipEventCreate(&ev.a));
+    SHELFI_HIP(hipEventCreate(&ev.b));
+    auto run = [&](uint64_t* out) {
+      const int rc = shelfi_dev_wavg_arena(ctx, arena_dev, w, C, K, out, stream);
+      if (rc) throw Error{rc, shelfi_last_error()};
+    };
+    float best_ms = 0.f;
+    for (size_t i = 0; i < n; ++i) {
+      if (!candidates[i]) throw Error{SHELFI_ERR_ARG, "null candidate buffer"};
+      run(candidates[i]);  // warm-up
+      SHELFI_HIP(hipEventRecord(ev.a, s));
+      for (int l = 0; l < launches; ++l) run(candidates[i]);
+      SHELFI_HIP(hipEventRecord(ev.b, s));
+      SHELFI_HIP(hipEventSynchronize(ev.b));
+      float t = 0.f;
+      SHELFI_HIP(hipEventElapsedTime(&t, ev.a, ev.b));
+      t /= (float)launches;
+      if (ms) ms[i] = t;
+      if (i == 0 || t < best_ms) {
+        best_ms = t;
+        *best = i;
+      }
+    }
+  });
+}
+
 int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream) {
   if (!ctx || !buf_dev) return SHELFI_ERR_ARG;
   return guarded([&] {

@@ -190,6 +190,16 @@ int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size
 /* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream);
+/* Output placement for a resident arena (no reference counterpart: a property of where
+ * the aggregate lands in HBM).  The arena launch's time depends on the physical
+ * placement of its output buffer relative to the arena (up to 12%,
+ * reproducible per buffer pair).  Runs shelfi_dev_wavg_arena into each of the n
+ * candidate [K][2][L][N] buffers (1 warm-up + `launches` timed launches each, HIP
+ * events on `stream`), writes each one's mean launch time to ms[i] (if ms), and the
+ * index of the fastest to *best.  Every candidate ends up holding the aggregate. */
+int shelfi_dev_wavg_arena_pick_output(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w,
+                                      size_t C, size_t K, uint64_t* const* candidates, size_t n,
+                                      int launches, size_t* best, float* ms, void* stream);
 /* Folds a collective's uint64 SUM of G <= 15 reduced partial sums back into [0, q_t)
  * (multi-GPU combine: local shelfi_dev_wavg -> RCCL reduce/reduce_scatter -> this). */
 int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream);

@@ -157,7 +157,14 @@ def test_wavg_arena_bitexact(cfg2, C, K):
             ar.put(c, m.blob_pack(cfg2, cts[c]))
     got = ar.wavg(w)
     torch.cuda.synchronize()
-    assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+    ref = O.wavg(cts, w, q, delta)
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), ref)
+    # output placement tuning: every candidate gets the aggregate, the fastest is kept
+    buf, ms = ar.place_output(w, candidates=3, launches=1)
+    torch.cuda.synchronize()
+    assert len(ms) == 3 and all(t > 0 for t in ms) and buf.shape == (K, 2, L, N)
+    assert np.array_equal(buf.cpu().numpy().view(np.uint64), ref)
+    assert ar.wavg(w, out=buf) is buf
 
 
 def test_wavg_arena_many_learners_ranges_and_weights(cfg2):
