@@ -23,6 +23,14 @@ int default_copy_threads() {
   return std::max(1, std::min(8, n));
 }
 
+int default_h2d_copy_threads() {
+  if (const char* e = std::getenv("SHELFI_H2D_COPY_THREADS")) {
+    const int v = std::atoi(e);
+    if (v >= 1) return std::min(v, 64);
+  }
+  return 4;
+}
+
 void advise_huge(void* p, size_t n) {
   const uintptr_t kHuge = 2u << 20;
   if (n < 2 * kHuge) return;
@@ -50,7 +58,8 @@ CopyPool::~CopyPool() {
 // jobs, page-aligned so first-touch faults of a fresh destination land on different
 // threads.
 void CopyPool::share(int id) {
-  const size_t per = ((total_ / parts_) + 4095) & ~size_t(4095);
+  if (id >= active_) return;
+  const size_t per = ((total_ / active_) + 4095) & ~size_t(4095);
   const size_t a = std::min(total_, per * (size_t)id), b = std::min(total_, per * (size_t)(id + 1));
   size_t base = 0;
   for (size_t j = 0; j < njobs_ && base < b; ++j) {
@@ -81,17 +90,19 @@ void CopyPool::run(int id) {
   }
 }
 
-void CopyPool::copy_many(const CopyJob* jobs, size_t njobs) {
+void CopyPool::copy_many(const CopyJob* jobs, size_t njobs, int parts) {
   size_t total = 0;
   for (size_t j = 0; j < njobs; ++j) total += jobs[j].n;
   if (total == 0) return;
-  if (workers_.empty() || total < (512u << 10)) {
+  const int active = (parts >= 1 && parts < parts_) ? parts : parts_;
+  if (workers_.empty() || active == 1 || total < (512u << 10)) {
     for (size_t j = 0; j < njobs; ++j) std::memcpy(jobs[j].dst, jobs[j].src, jobs[j].n);
     return;
   }
   jobs_ = jobs;
   njobs_ = njobs;
   total_ = total;
+  active_ = active;
   pending_.store((int)workers_.size(), std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> lk(mu_);  // no lost wake-up for a worker about to sleep
@@ -109,7 +120,8 @@ void CopyPool::copy(void* dst, const void* src, size_t n) {
 
 // --------------------------------------------------------------- Stager ----
 Stager::Stager(size_t slot_bytes, int n_in, int n_out, int threads)
-    : slot_bytes_(slot_bytes), in_(n_in), out_(n_out), pool_(threads) {
+    : slot_bytes_(slot_bytes), in_(n_in), out_(n_out), pool_(threads),
+      h2d_parts_(std::min(pool_.threads(), default_h2d_copy_threads())) {
   try {
     for (auto* ring : {&in_, &out_})
       for (Slot& s : *ring) {
@@ -191,7 +203,7 @@ void Stager::h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s) 
       }
     }
     if (!fill) break;
-    pool_.copy_many(jobs.data(), jobs.size());
+    pool_.copy_many(jobs.data(), jobs.size(), h2d_parts_);
     SHELFI_HIP(hipMemcpyAsync(dst, sl.host, fill, hipMemcpyHostToDevice, s));
     SHELFI_HIP(hipEventRecord(sl.ev, s));
     sl.used = true;

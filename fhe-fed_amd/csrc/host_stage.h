@@ -39,7 +39,8 @@ class CopyPool {
   CopyPool(const CopyPool&) = delete;
   CopyPool& operator=(const CopyPool&) = delete;
   void copy(void* dst, const void* src, size_t n);
-  void copy_many(const CopyJob* jobs, size_t njobs);
+  // parts = how many of the pool's threads share the list (0 = all of them).
+  void copy_many(const CopyJob* jobs, size_t njobs, int parts = 0);
   int threads() const { return parts_; }
 
  private:
@@ -56,6 +57,7 @@ class CopyPool {
   std::atomic<bool> stop_{false};
   const CopyJob* jobs_ = nullptr;
   size_t njobs_ = 0, total_ = 0;
+  int active_ = 1;  // threads sharing the current list
 };
 
 // A host range of a scatter/gather transfer.
@@ -110,6 +112,10 @@ class Stager {
   size_t in_next_ = 0, out_next_ = 0;
   std::deque<size_t> pending_;  // out slot indices in enqueue order
   CopyPool pool_;
+  // Threads that fill an upload slot: fewer than the pool (pageable -> pinned copies
+  // compete with the DMA engine reading pinned memory; 4 of 8 measured +8-16% H2D,
+  // DESIGN.md §5.3).  Drains into fresh output pages keep the whole pool (page faults).
+  int h2d_parts_ = 1;
 };
 
 // Ask for transparent huge pages on the 2 MiB-aligned interior of a large output
@@ -119,5 +125,6 @@ void advise_huge(void* p, size_t n);
 
 // Worker threads for a Stager: SHELFI_COPY_THREADS, else min(8, CPUs this process may use).
 int default_copy_threads();
+int default_h2d_copy_threads();  // SHELFI_H2D_COPY_THREADS, default 4
 
 }  // namespace shelfi
