@@ -1,6 +1,7 @@
 """The bytes API's host copy pool (fhe-fed_amd/csrc/host_stage.cpp CopyPool), host
 only: tools/pool_bench.cpp copies 64 MiB in 2 / 8 / 32 MiB lists with 1-8 workers
-(spin-then-sleep hand-off) and checks every byte."""
+(spin-then-sleep hand-off) and checks every byte, also for lists shared by only some
+of the workers (the upload fills)."""
 import os
 import shutil
 import subprocess
@@ -23,3 +24,4 @@ def test_copy_pool_is_exact(tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     assert "MISMATCH" not in p.stdout
     assert p.stdout.count("GB/s") == 4 * 3
+    assert p.stdout.count("partial shares ok") == 4  # lists shared by 1, half and all workers

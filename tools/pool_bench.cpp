@@ -28,5 +28,16 @@ int main(int argc, char** argv) {
       printf("threads %d slot %3zu MiB: %.1f GB/s (%.1f us per slot)\n", threads, slot >> 20, total / s / 1e9,
              s / (total / slot) * 1e6);
     }
+    // a 3-piece list shared by only some of the workers (the upload fill of Stager::h2dv)
+    for (int parts : {1, (threads + 1) / 2, threads}) {
+      for (size_t i = 0; i < total; ++i) src[i] = (uint8_t)(i * 7 + parts);
+      const size_t a = total / 3, b = total / 2;
+      const CopyJob jobs[3] = {{dst.data(), src.data(), a}, {dst.data() + a, src.data() + a, b - a},
+                               {dst.data() + b, src.data() + b, total - b}};
+      pool.copy_many(jobs, 3, parts);
+      if (std::memcmp(dst.data(), src.data(), total) != 0) { printf("MISMATCH parts %d\n", parts); return 1; }
+      std::memset(dst.data(), 0, total);
+    }
+    printf("threads %d: partial shares ok\n", threads);
   }
 }
