@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -37,10 +38,20 @@ inline uint32_t fft_block_log(uint32_t logS) {
   const uint32_t b = logS >= 15 ? (uint32_t)kFftBlockLogBig : (uint32_t)kFftBlockLog;
   return logS < b ? logS : b;
 }
-constexpr int kNttBlockLog = 11;     // u64 block staged in LDS by NTT pass 2 (N <= 2^15)
-constexpr int kNttBlockLogBig = 12;  // N >= 2^16: 32 KiB blocks keep pass 1 at 16 columns
+constexpr int kNttBlockLog = 11;     // u64 block staged in LDS by NTT pass 2 (N <= 2^16)
+constexpr int kNttBlockLogBig = 12;  // N >= 2^17: 32 KiB blocks keep pass 1 at 32 columns
+// 2^16 runs 2^11 blocks + a 32-column pass 1: 5% faster encrypt and decrypt than 2^12
+// blocks at L = 6 (A/B in one box, tools/enc_variant_probe.py); 2^17 is a tie.
+// SHELFI_NTT_BLOCK_LOG_BIG=11|12 overrides the block size for N >= 2^16 in a whole
+// process (read once: tables and launches must agree; A/B runs use separate processes).
 inline uint32_t ntt_block_log(uint32_t logN) {
-  const uint32_t b = logN >= 16 ? (uint32_t)kNttBlockLogBig : (uint32_t)kNttBlockLog;
+  static const uint32_t ovr = [] {
+    const char* e = std::getenv("SHELFI_NTT_BLOCK_LOG_BIG");
+    const int v = e ? std::atoi(e) : 0;
+    return (uint32_t)((v == 11 || v == 12) ? v : 0);
+  }();
+  uint32_t b = logN >= 17 ? (uint32_t)kNttBlockLogBig : (uint32_t)kNttBlockLog;
+  if (ovr && logN >= 16) b = ovr;
   return logN < b ? logN : b;
 }
 

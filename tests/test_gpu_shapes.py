@@ -4,6 +4,8 @@ bit-for-bit, on small inputs (1-2 ciphertexts):
   - rings 2^12, 2^14: compile-time block passes with 1- and 3-stage columns passes;
   - sparse packing (gap = N / 2 batch of 2 and 4): the fused INTT + CRT decode with
     coefficients that are not slots;
+  - ring 2^16, L = 2: 11-stage blocks, 5-stage columns, fused CRT at 32 KiB of LDS
+    (cfg4, 2^16 with L = 6, takes the unfused CRT: tests/test_gpu_parity.py);
   - ring 2^17, L = 2: 12-stage blocks, 5-stage columns, fused CRT at 32 KiB of LDS;
   - ring 2^17, L = 4: fused CRT over its LDS limit -> unfused columns pass + CRT kernel;
   - 30-bit scaling primes (q < 2^40): the generic block kernels (no one-step reduction).
@@ -27,6 +29,7 @@ SHAPES = [
     (8192, 0, 2, 52, 60),      # N = 2^14, L = 3
     (8192, 32768, 3, 52, 60),  # N = 2^15, gap 2
     (4096, 32768, 3, 52, 60),  # N = 2^15, gap 4
+    (32768, 0, 1, 52, 60),     # N = 2^16, L = 2: 2^11 blocks, 5-stage columns, fused CRT
     (65536, 0, 1, 52, 60),     # N = 2^17, L = 2
     (65536, 0, 3, 52, 60),     # N = 2^17, L = 4
     (4096, 0, 1, 30, 40),      # 30-bit scaling prime
