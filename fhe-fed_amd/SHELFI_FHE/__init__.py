@@ -9,8 +9,10 @@ the C ABI in include/shelfi.h; nothing here computes on the CPU.
 Extensions over the reference (keyword-only, defaults reproduce it):
 ``multDepth`` (L = multDepth + 1 towers; reference fixes 1, ckks.cpp:26),
 ``firstModBits`` (60), ``ringDim`` (0 = PALISADE's choice), ``device``
-(HIP ordinal; default LOCAL_RANK or 0), and ``seed`` (deterministic encryption
-randomness for parity tests; 0 = OS entropy).
+(HIP ordinal; default LOCAL_RANK or 0), ``seed`` (deterministic encryption
+randomness for parity tests; 0 = OS entropy) and ``decodeNoise`` (PALISADE's decode
+noise flooding, on by default like the reference's Decrypt; False = the exact,
+deterministic decode the parity tests compare bit for bit).
 """
 from __future__ import annotations
 
@@ -82,7 +84,7 @@ class CKKS(Scheme):
     def __init__(self, scheme: str = "ckks", batchSize: int = 4096, scaleFactorBits: int = 52,
                  cryptodir: str = "../resources/cryptoparams/", *, multDepth: int = 1,
                  firstModBits: int = 60, ringDim: int = 0, device: int | None = None,
-                 seed: int = 0):
+                 seed: int = 0, decodeNoise: bool = True):
         super().__init__(scheme)
         if scheme.lower() != "ckks":
             raise ValueError("only the 'ckks' scheme is implemented")
@@ -97,6 +99,8 @@ class CKKS(Scheme):
                                           C.byref(self._ctx)), "CKKS()")
         if seed:
             check(self._lib.shelfi_set_seed(self._ctx, int(seed)))
+        if not decodeNoise:
+            self.set_decode_noise(False)
 
     # ------------------------------------------------------------ lifecycle --
     def __del__(self):
@@ -141,8 +145,9 @@ class CKKS(Scheme):
         """PALISADE 1.11's decode noise flooding (CKKSPackedEncoding::Decode): Gaussian
         noise of stddev sqrt(m_factor + 1) * max(sigma, sqrt(N)/8) at scale 2^p, where
         sigma is estimated from the decryption's anti-symmetric part, and a RuntimeError
-        when log2 sigma > scaleFactorBits - 5.  Off by default: decrypt is then exact
-        and deterministic (the noise-free value PALISADE floods)."""
+        when log2 sigma > scaleFactorBits - 5.  On by default, as in the reference's
+        Decrypt (ckks.cpp:189); off, decrypt is exact and deterministic (the noise-free
+        value PALISADE floods), which is what the parity tests compare."""
         check(self._lib.shelfi_set_decode_noise(self._ctx, 1 if enabled else 0, float(m_factor)),
               "set_decode_noise")
 
@@ -329,18 +334,50 @@ def _take_lib_bytes(lib, out, n) -> bytes:
 
 
 def palisade_write(ctx_obj: bytes, keytag: str, moduli, residues: np.ndarray, depth: int = 1,
-                   level: int = 0, scale: float = 0.0, vector_archive: bool = True) -> bytes:
+                   level: int = 0, scale: float = 0.0, vector_archive: bool = True,
+                   key_params: bool = False) -> bytes:
     """Write residues [K][2][L][N] as a PALISADE archive around an embedded context
-    object (palisade_key_context) and key tag."""
+    object (palisade_key_context) and key tag.  key_params: the form the reference's
+    encrypt / computeWeightedAverage write (the key's own parameter objects embedded at
+    the first ciphertext, palisade_codec.h); False: CT1.txt's form."""
     lib = _lib.load()
     r = np.ascontiguousarray(residues, dtype=np.uint64)
     K, two, L, N = r.shape
     q = np.ascontiguousarray(moduli, dtype=np.uint64)
     out, n = _lib.u8p(), C.c_size_t()
     ob = bytes(ctx_obj)
+    flags = (1 if vector_archive else 0) | (2 if key_params else 0)
     check(lib.shelfi_palisade_write(ob, len(ob), keytag.encode(), N, L, q.ctypes.data_as(_lib.u64p), K,
                                     r.ctypes.data_as(_lib.u64p), int(depth), int(level), float(scale),
-                                    1 if vector_archive else 0, C.byref(out), C.byref(n)), "palisade_write")
+                                    flags, C.byref(out), C.byref(n)), "palisade_write")
+    return _take_lib_bytes(lib, out, n.value)
+
+
+def palisade_context_file(ring_dim: int, moduli, roots, scaleFactorBits: int = 52,
+                          batchSize: int = 4096) -> bytes:
+    """cryptocontext.txt as the reference's genCryptoContextAndKeyGen writes it
+    (ckks.cpp:41) for these towers."""
+    lib = _lib.load()
+    q = np.ascontiguousarray(moduli, dtype=np.uint64)
+    r = np.ascontiguousarray(roots, dtype=np.uint64)
+    out, n = _lib.u8p(), C.c_size_t()
+    check(lib.shelfi_palisade_context_file(int(ring_dim), q.size, q.ctypes.data_as(_lib.u64p),
+                                           r.ctypes.data_as(_lib.u64p), int(scaleFactorBits),
+                                           int(batchSize), C.byref(out), C.byref(n)),
+          "palisade_context_file")
+    return _take_lib_bytes(lib, out, n.value)
+
+
+def palisade_key_file(ctx_obj: bytes, keytag: str, polys: np.ndarray, public: bool) -> bytes:
+    """key-public.txt (polys [2][L][N]: b, a) or key-private.txt (polys [L][N]: s)
+    around an embedded context object (ckks.cpp:48,53)."""
+    lib = _lib.load()
+    ob = bytes(ctx_obj)
+    pp = np.ascontiguousarray(polys, dtype=np.uint64)
+    out, n = _lib.u8p(), C.c_size_t()
+    check(lib.shelfi_palisade_key_file(ob, len(ob), keytag.encode(), pp.ctypes.data_as(_lib.u64p),
+                                       1 if public else 0, C.byref(out), C.byref(n)),
+          "palisade_key_file")
     return _take_lib_bytes(lib, out, n.value)
 
 

@@ -87,6 +87,10 @@ SIGNATURES = {
     "shelfi_palisade_write": (C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_uint32, C.c_uint32, u64p,
                                         C.c_uint64, u64p, C.c_uint64, C.c_uint64, C.c_double, C.c_int,
                                         C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_palisade_context_file": (C.c_int, [C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32, C.c_uint32,
+                                               C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "shelfi_palisade_key_file": (C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, u64p, C.c_int,
+                                           C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "shelfi_palisade_key_context": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                               C.c_char_p]),
     "shelfi_palisade_embed_context": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(u8p),

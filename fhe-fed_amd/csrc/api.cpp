@@ -65,8 +65,12 @@ static BlobHeader parse_blob(const uint8_t* blob, size_t len, const shelfi_ctx* 
     throw Error{SHELFI_ERR_FORMAT, "not a SHELFI ciphertext blob (bad magic/version)"};
   if (h.L == 0 || h.L > kMaxTowers || h.logN < 10 || h.logN > 17)
     throw Error{SHELFI_ERR_FORMAT, "corrupt ciphertext blob header"};
-  const uint64_t need = sizeof(BlobHeader) + h.K * 2ull * h.L * (8ull << h.logN);
-  if (len != need) throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
+  // K comes from an untrusted header: bound it by the payload before multiplying, so a
+  // forged K whose K * ct_bytes wraps mod 2^64 cannot pass the length check.
+  const uint64_t ct_bytes = 2ull * h.L * (8ull << h.logN);
+  if (h.K > (len - sizeof(BlobHeader)) / ct_bytes ||
+      len != sizeof(BlobHeader) + h.K * ct_bytes)
+    throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
   if (ctx) {
     if (h.logN != ctx->p.logN || h.L != ctx->p.L || h.params_id != ctx->params_id)
       throw Error{SHELFI_ERR_FORMAT, "ciphertext was produced under different crypto parameters"};
@@ -407,10 +411,55 @@ static T get(const std::string& s, size_t& off) {
   return v;
 }
 
-// W = (int64)((double)(float)w * Delta + 0.5) per learner, split into 30-bit limbs
+// PALISADE context parameters of ctx->p, as genCryptoContextCKKS(multDepth, scaleFactorBits,
+// batchSize) records them (ckks.cpp:28): the scaling-factor bits in the plaintext-modulus
+// field, the batch in the encoding parameters, the default RLWE fields of the reference's
+// committed cryptocontext.txt.
+static PalisadeCtxParams palisade_params_of(const Params& p) {
+  PalisadeCtxParams cp;
+  cp.N = p.N;
+  cp.L = p.L;
+  cp.q.assign(p.q, p.q + p.L);
+  cp.psi.assign(p.psi, p.psi + p.L);
+  cp.plaintext_modulus = p.scale_bits;
+  cp.batch = p.batch;
+  cp.sigma = (float)p.sigma;
+  return cp;
+}
+
+// PALISADE's GenerateUniqueKeyID: four 32-bit draws, 8 lowercase hex digits each
+static std::string make_keytag(const shelfi_ctx* ctx) {
+  uint32_t r[4];
+  if (ctx->seed) {
+    uint32_t k[8];
+    seed_to_key(ctx->seed ^ 0x6b65797461670000ull, k);  // "keytag"
+    std::memcpy(r, k, sizeof(r));
+  } else {
+    os_random(r, sizeof(r));
+  }
+  char buf[33];
+  for (int i = 0; i < 4; ++i) std::snprintf(buf + 8 * i, 9, "%08x", r[i]);
+  return std::string(buf, 32);
+}
+
+// W = (int64)((double)(float)w * Delta + 0.5) (ckks.cpp:287-288, PALISADE EvalMult by a
+// constant). The cast is undefined for NaN, +-inf and |w * Delta| >= 2^63, so such weights
+// are rejected instead of producing a garbage aggregate.
+static int64_t weight_int(float w, double delta) {
+  const double v = (double)w * delta + 0.5;
+  if (!std::isfinite(v) || v >= 9223372036854775808.0 || v < -9223372036854775808.0)
+    throw Error{SHELFI_ERR_RANGE, "scaling factor is not finite or |w * scale| >= 2^63"};
+  return (int64_t)v;
+}
+
+static void check_weights(const float* w, size_t n, double delta) {
+  for (size_t c = 0; c < n; ++c) (void)weight_int(w[c], delta);
+}
+
+// W per learner, split into 30-bit limbs
 static void fill_weights(WavgArgs& a, const Params& p, const float* w, size_t n) {
   for (size_t c = 0; c < n; ++c) {
-    const int64_t W = (int64_t)((double)w[c] * p.delta + 0.5);  // ckks.cpp:287-288
+    const int64_t W = weight_int(w[c], p.delta);
     for (uint32_t t = 0; t < p.L; ++t) {
       const uint64_t wt = mod_signed(W, p.q[t]);
       a.wl[c][t][0] = (uint32_t)(wt & ((1u << 30) - 1));
@@ -426,7 +475,7 @@ static int arena_weight_slot(shelfi_ctx* ctx, const float* w, size_t C, hipStrea
   const Params& p = ctx->p;
   std::vector<uint32_t> wl(C * p.L * 2);
   for (size_t c = 0; c < C; ++c) {
-    const int64_t W = (int64_t)((double)w[c] * p.delta + 0.5);  // ckks.cpp:287-288
+    const int64_t W = weight_int(w[c], p.delta);  // ckks.cpp:287-288
     for (uint32_t t = 0; t < p.L; ++t) {
       const uint64_t wt = mod_signed(W, p.q[t]);
       wl[(c * p.L + t) * 2] = (uint32_t)(wt & ((1u << 30) - 1));
@@ -650,31 +699,19 @@ int shelfi_keygen(shelfi_ctx* ctx, const char* cryptodir) {
     (void)hipFree(sk_d);
     (void)hipFree(pk_d);
     std::memset(key, 0, sizeof(key));
-    install_keys(ctx, pk.data(), sk.data(), false);
+    install_keys(ctx, pk.data(), sk.data(), true);
+    // ckks.cpp:36-56: context first, then public, then private key, in PALISADE 1.11's
+    // cereal PortableBinary format (palisade_codec.h), so PALISADE clients can load them
+    const PalisadeCtxParams cp = palisade_params_of(ctx->p);
+    std::string tag = make_keytag(ctx);
     if (cryptodir && *cryptodir) {
       const std::string dir(cryptodir);
-      std::string cc("SHCC", 4), ps("SHPK", 4), ss("SHSK", 4);
-      const uint32_t ver = 1;
-      put(cc, ver);
-      put(cc, p.N);
-      put(cc, p.L);
-      put(cc, p.batch);
-      put(cc, p.scale_bits);
-      put(cc, p.first_mod_bits);
-      put(cc, p.sigma);
-      for (uint32_t t = 0; t < p.L; ++t) put(cc, p.q[t]);
-      for (uint32_t t = 0; t < p.L; ++t) put(cc, p.psi[t]);
-      put(ps, ver);
-      put(ps, ctx->params_id);
-      ps.append(reinterpret_cast<const char*>(pk.data()), pk.size() * 8);
-      put(ss, ver);
-      put(ss, ctx->params_id);
-      ss.append(reinterpret_cast<const char*>(sk.data()), sk.size() * 8);
-      // ckks.cpp:36-56: context first, then public, then private key
-      write_file(dir + "cryptocontext.txt", cc);
-      write_file(dir + "key-public.txt", ps);
-      write_file(dir + "key-private.txt", ss);
+      write_file(dir + "cryptocontext.txt", palisade_context_file(cp));
+      write_file(dir + "key-public.txt", palisade_key_file(cp, tag, pk.data(), true));
+      write_file(dir + "key-private.txt", palisade_key_file(cp, tag, sk.data(), false));
     }
+    ctx->pal_ctx_obj = palisade_context_object(cp, 3);
+    ctx->pal_keytag = std::move(tag);
   });
 }
 
@@ -719,13 +756,18 @@ int shelfi_load(shelfi_ctx* ctx, const char* cryptodir) {
       PalisadeContext pc = palisade_read_context(cc);
       const uint32_t N = pc.N, L = (uint32_t)pc.q.size();
       const uint32_t batch = std::min<uint32_t>(ctx->p.batch, N / 2);
-      validate_params(N, L, ctx->p.scale_bits, ctx->p.first_mod_bits < ctx->p.scale_bits
-                                                   ? ctx->p.scale_bits
-                                                   : ctx->p.first_mod_bits,
-                      batch);
+      // the scaling-factor bits the context was generated with (its plaintext-modulus
+      // field), when the file has the layout palisade_codec.h restates
+      uint32_t sb = ctx->p.scale_bits;
+      try {
+        const PalisadeCtxParams cp = palisade_parse_context_file(cc);
+        if (cp.plaintext_modulus >= 10 && cp.plaintext_modulus <= 58) sb = (uint32_t)cp.plaintext_modulus;
+      } catch (const Error&) {
+      }
+      const uint32_t fb = std::max(ctx->p.first_mod_bits, sb);
+      validate_params(N, L, sb, fb, batch);
       free_keys(ctx);
-      set_params(ctx, N, L, ctx->p.scale_bits, ctx->p.first_mod_bits, batch, pc.q.data(),
-                 pc.psi.data());
+      set_params(ctx, N, L, sb, fb, batch, pc.q.data(), pc.psi.data());
       std::vector<uint64_t> pk, sk;
       const std::string pub = read_file(dir + "key-public.txt");
       palisade_read_keys(pub, read_file(dir + "key-private.txt"), N, pc.q, pk, sk);
@@ -812,8 +854,9 @@ static CtLayout make_output(const shelfi_ctx* ctx, bool pal, uint64_t K, uint32_
   if (pal) {
     if (ctx->pal_ctx_obj.empty())
       throw Error{SHELFI_ERR_STATE, "PALISADE wire format needs keys loaded from PALISADE files"};
+    // key_params: what the reference writes (its keys always come from key-public.txt)
     v.off = palisade_layout(ctx->pal_ctx_obj, ctx->pal_keytag, p.N, p.L, p.q, K, depth, level, scale,
-                            4, true, buf, total);
+                            4, true, true, buf, total);
     return v;
   }
   *total = sizeof(BlobHeader) + K * 2ull * p.L * p.N * 8;
@@ -1090,6 +1133,7 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
       make_output(ctx, pal, 0, 2, 0, scale, out, &total);
       return;
     }
+    check_weights(weights, C, ctx->p.delta);
     DeviceGuard g(ctx->device);
     const std::vector<CtLayout> in = wavg_inputs(ctx, blobs, lens, C);
     const CtLayout& h0 = in.front();
@@ -1263,6 +1307,7 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
   if (!ctx || !out_dev || (C && (!in_dev || !w))) return SHELFI_ERR_ARG;
   return guarded([&] {
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
+    check_weights(w, C, ctx->p.delta);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
@@ -1308,6 +1353,7 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
   if (!ctx || !out_dev || (C && (!arena_dev || !w))) return SHELFI_ERR_ARG;
   return guarded([&] {
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
+    check_weights(w, C, ctx->p.delta);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners
@@ -1520,7 +1566,7 @@ int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_in
 int shelfi_palisade_write(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
                           uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
                           uint64_t num_cts, const uint64_t* residues, uint64_t depth, uint64_t level,
-                          double scale, int vector_archive, uint8_t** out, size_t* out_len) {
+                          double scale, int flags, uint8_t** out, size_t* out_len) {
   if (!ctx_obj || !keytag || !moduli || !out || !out_len || (num_cts && !residues) ||
       num_towers < 1 || num_towers > (uint32_t)kMaxTowers)
     return SHELFI_ERR_ARG;
@@ -1528,18 +1574,57 @@ int shelfi_palisade_write(const uint8_t* ctx_obj, size_t ctx_len, const char* ke
   *out_len = 0;
   return guarded([&] {
     const std::string obj((const char*)ctx_obj, ctx_len), tag(keytag);
+    const bool vec = (flags & SHELFI_PAL_VECTOR) != 0, kp = (flags & SHELFI_PAL_KEY_PARAMS) != 0;
     size_t total = 0;
-    palisade_layout(obj, tag, ring_dim, num_towers, moduli, num_cts, depth, level, scale, 4,
-                    vector_archive != 0, nullptr, &total);
+    palisade_layout(obj, tag, ring_dim, num_towers, moduli, num_cts, depth, level, scale, 4, vec, kp,
+                    nullptr, &total);
     uint8_t* buf = (uint8_t*)std::malloc(total);
     if (!buf) throw std::bad_alloc();
     const std::vector<size_t> off = palisade_layout(obj, tag, ring_dim, num_towers, moduli, num_cts,
-                                                    depth, level, scale, 4, vector_archive != 0,
-                                                    buf, &total);
+                                                    depth, level, scale, 4, vec, kp, buf, &total);
     for (size_t i = 0; i < off.size(); ++i)
       std::memcpy(buf + off[i], residues + i * (size_t)ring_dim, (size_t)ring_dim * 8);
     *out = buf;
     *out_len = total;
+  });
+}
+
+static void take_string(const std::string& s, uint8_t** out, size_t* out_len) {
+  uint8_t* buf = (uint8_t*)std::malloc(s.size() ? s.size() : 1);
+  if (!buf) throw std::bad_alloc();
+  std::memcpy(buf, s.data(), s.size());
+  *out = buf;
+  *out_len = s.size();
+}
+
+int shelfi_palisade_context_file(uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
+                                 const uint64_t* roots, uint32_t scale_bits, uint32_t batch,
+                                 uint8_t** out, size_t* out_len) {
+  if (!moduli || !roots || !out || !out_len || num_towers < 1 || num_towers > (uint32_t)kMaxTowers)
+    return SHELFI_ERR_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    PalisadeCtxParams cp;
+    cp.N = ring_dim;
+    cp.L = num_towers;
+    cp.q.assign(moduli, moduli + num_towers);
+    cp.psi.assign(roots, roots + num_towers);
+    cp.plaintext_modulus = scale_bits;
+    cp.batch = batch;
+    take_string(palisade_context_file(cp), out, out_len);
+  });
+}
+
+int shelfi_palisade_key_file(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
+                             const uint64_t* polys, int is_public, uint8_t** out, size_t* out_len) {
+  if (!ctx_obj || !keytag || !polys || !out || !out_len) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    uint32_t id0 = 0;
+    const PalisadeCtxParams cp =
+        palisade_parse_context_object(std::string((const char*)ctx_obj, ctx_len), &id0);
+    if (id0 != 3) throw Error{SHELFI_ERR_FORMAT, "context object must be in embedded form (ids from 3)"};
+    take_string(palisade_key_file(cp, keytag, polys, is_public != 0), out, out_len);
   });
 }
 

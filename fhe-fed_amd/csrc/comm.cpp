@@ -163,6 +163,8 @@ int shelfi_comm_destroy(shelfi_ctx* ctx) {
 
 int shelfi_dev_reduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, int root, void* stream) {
   if (!ctx || (K && !partial_dev)) return SHELFI_ERR_ARG;
+  // comm_init/comm_destroy replace the communicator under ctx->mu
+  std::lock_guard<std::mutex> lk(ctx->mu);
   return guarded_comm([&] {
     ncclComm_t c = comm_of(ctx);
     if (root < 0 || root >= ctx->comm_world) throw Error{SHELFI_ERR_ARG, "root outside the communicator"};
@@ -178,6 +180,8 @@ int shelfi_dev_reduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, int root
 
 int shelfi_dev_allreduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, void* stream) {
   if (!ctx || (K && !partial_dev)) return SHELFI_ERR_ARG;
+  // comm_init/comm_destroy replace the communicator under ctx->mu
+  std::lock_guard<std::mutex> lk(ctx->mu);
   return guarded_comm([&] {
     ncclComm_t c = comm_of(ctx);
     if (!K) return;
@@ -193,6 +197,8 @@ int shelfi_dev_allreduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, void*
 int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size_t K, uint64_t* out_dev,
                               void* stream) {
   if (!ctx || (K && (!partial_dev || !out_dev))) return SHELFI_ERR_ARG;
+  // comm_init/comm_destroy replace the communicator under ctx->mu
+  std::lock_guard<std::mutex> lk(ctx->mu);
   return guarded_comm([&] {
     ncclComm_t c = comm_of(ctx);
     const size_t W = (size_t)ctx->comm_world;

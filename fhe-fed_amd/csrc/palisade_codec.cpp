@@ -106,7 +106,328 @@ std::vector<uint32_t> context_ids(const std::string& obj, uint32_t first) {
   return ids;
 }
 
+constexpr const char* kParamsName = "lbcrypto::LPCryptoParametersCKKS<lbcrypto::DCRTPoly>";
+constexpr const char* kSchemeName = "lbcrypto::LPPublicKeyEncryptionSchemeCKKS<lbcrypto::DCRTPoly>";
+
+struct Out {
+  std::string s;
+  void put(const void* v, size_t n) { s.append((const char*)v, n); }
+  void u8(uint8_t v) { put(&v, 1); }
+  void u16(uint16_t v) { put(&v, 2); }
+  void u32(uint32_t v) { put(&v, 4); }
+  void u64(uint64_t v) { put(&v, 8); }
+  void f32(float v) { put(&v, 4); }
+  void str(const std::string& v) {
+    u64(v.size());
+    s += v;
+  }
+};
+
+// prod(q) as little-endian u32 limbs
+std::vector<uint32_t> modulus_product(const std::vector<uint64_t>& q) {
+  std::vector<uint32_t> r{1};
+  for (uint64_t x : q) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    std::vector<uint32_t> t(r.size() + 2, 0);
+    for (int half = 0; half < 2; ++half) {
+      const uint64_t m = half ? hi : lo;
+      uint64_t carry = 0;
+      size_t i = 0;
+      for (; i < r.size(); ++i) {
+        const uint64_t v = (uint64_t)r[i] * m + t[i + half] + carry;
+        t[i + half] = (uint32_t)v;
+        carry = v >> 32;
+      }
+      for (size_t j = i + half; carry; ++j) {
+        const uint64_t v = (uint64_t)t[j] + carry;
+        t[j] = (uint32_t)v;
+        carry = v >> 32;
+      }
+    }
+    while (t.size() > 1 && !t.back()) t.pop_back();
+    r.swap(t);
+  }
+  return r;
+}
+
+// BigIntegerFixedT<uint32_t, 3500>: limbs most significant first, then u16 bit length
+void put_bigint(Out& o, const std::vector<uint32_t>& le, uint32_t nbytes) {
+  const size_t nl = (nbytes - 2) / 4;
+  size_t used = le.size();
+  while (used && !le[used - 1]) --used;
+  if (used > nl) bad("modulus product exceeds the BigInteger width");
+  for (size_t i = 0; i < nl; ++i) {
+    const size_t li = nl - 1 - i;
+    o.u32(li < used ? le[li] : 0);
+  }
+  o.u16(used ? (uint16_t)(32 * (used - 1) + (32 - __builtin_clz(le[used - 1]))) : 0);
+}
+
+std::vector<uint32_t> read_bigint(Cursor& c, uint32_t nbytes) {
+  const size_t nl = (nbytes - 2) / 4;
+  std::vector<uint32_t> le(nl);
+  for (size_t i = 0; i < nl; ++i) le[nl - 1 - i] = c.u32();
+  c.get<uint16_t>();
+  return le;
+}
+
+std::string get_str(Cursor& c, size_t max) {
+  const uint64_t n = c.u64();
+  if (n > max) bad("string length");
+  c.need((size_t)n);
+  std::string v((const char*)c.b + c.p, (size_t)n);
+  c.p += (size_t)n;
+  return v;
+}
+
+// A tower's ILNativeParams object body (after its pointer id; no class versions)
+void put_tower_params(Out& o, uint32_t N, uint64_t q, uint64_t psi) {
+  o.u32(2 * N);
+  o.u32(N);
+  o.u8(1);
+  o.u64(q);
+  o.u64(psi);
+  o.u64(0);
+  o.u64(0);
+}
+
+// The ILDCRTParams object body (after its pointer id; no class versions) with its
+// towers given as references (the form a ciphertext archive uses for the key's
+// parameters, whose towers were embedded at the first polynomial's residue vectors)
+void put_dcrt_params_refs(Out& o, const PalisadeCtxParams& p, uint32_t tower_id0) {
+  o.u32(2 * p.N);
+  o.u32(p.N);
+  o.u8(1);
+  put_bigint(o, modulus_product(p.q), p.bigint_bytes);
+  if (p.elem_bigints.size() == 3ull * p.bigint_bytes) {
+    o.s += p.elem_bigints;
+  } else {
+    for (int i = 0; i < 3; ++i) put_bigint(o, {}, p.bigint_bytes);
+  }
+  o.u64(p.L);
+  for (uint32_t t = 0; t < p.L; ++t) {
+    o.u32(kPoly);
+    o.u32(tower_id0 + t);
+  }
+  put_bigint(o, {}, p.bigint_bytes);  // originalModulus
+}
+
 }  // namespace
+
+PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id) {
+  PalisadeCtxParams p;
+  Cursor c{(const uint8_t*)obj.data(), obj.size(), 0};
+  if (c.u32() != 1) bad("context version");
+  if (c.u32() != (kNew | 1u) || get_str(c, 256) != kParamsName) bad("crypto parameters type");
+  const uint32_t id = c.u32();
+  if (!(id & kNew)) bad("crypto parameters pointer");
+  const uint32_t id0 = id & ~kNew;
+  for (int i = 0; i < 3; ++i) c.u32();  // class versions
+  c.expect32(kPoly, "element parameters pointer");
+  if (c.u32() != (kNew | (id0 + 1))) bad("element parameters id");
+  c.u32();
+  c.u32();
+  const uint32_t M = c.u32();
+  p.N = c.u32();
+  if (p.N < 2 || (p.N & (p.N - 1)) || M != 2 * p.N) bad("context ring dimension");
+  c.get<uint8_t>();
+  c.u32();  // BigInteger version
+  // BigInteger width: the four element BigIntegers are followed by u64 L and the
+  // first tower's new pointer
+  uint32_t B = 0;
+  for (uint32_t b = 10; b <= 4096; b += 4) {
+    const size_t at = c.p + 4ull * b;
+    if (at + 16 > obj.size()) break;
+    uint64_t L;
+    uint32_t m, t0;
+    std::memcpy(&L, obj.data() + at, 8);
+    std::memcpy(&m, obj.data() + at + 8, 4);
+    std::memcpy(&t0, obj.data() + at + 12, 4);
+    if (L >= 1 && L <= 64 && m == kPoly && t0 == (kNew | (id0 + 2))) {
+      B = b;
+      break;
+    }
+  }
+  if (!B) bad("context BigInteger layout");
+  p.bigint_bytes = B;
+  const std::vector<uint32_t> Q = read_bigint(c, B);
+  p.elem_bigints.assign(obj.data() + c.p, 3ull * B);
+  c.need(3ull * B);
+  c.p += 3ull * B;
+  const uint64_t L = c.u64();
+  if (L < 1 || L > (uint64_t)kMaxTowers) bad("context tower count");
+  p.L = (uint32_t)L;
+  for (uint32_t t = 0; t < p.L; ++t) {
+    c.expect32(kPoly, "tower parameters pointer");
+    if (c.u32() != (kNew | (id0 + 2 + t))) bad("tower parameters id");
+    if (t == 0) {
+      c.u32();
+      c.u32();
+    }
+    if (c.u32() != M || c.u32() != p.N) bad("tower ring dimension");
+    c.get<uint8_t>();
+    if (t == 0) c.u32();  // NativeInteger version
+    p.q.push_back(c.u64());
+    p.psi.push_back(c.u64());
+    c.u64();
+    c.u64();
+  }
+  read_bigint(c, B);  // originalModulus
+  c.expect32(kPoly, "encoding parameters pointer");
+  if (c.u32() != (kNew | (id0 + 2 + p.L))) bad("encoding parameters id");
+  c.u32();
+  p.plaintext_modulus = c.u64();
+  c.u64();
+  c.u64();
+  c.u64();
+  c.u32();
+  p.batch = c.u32();
+  p.sigma = c.get<float>();
+  p.assurance = c.get<float>();
+  p.root_hermite = c.get<float>();
+  p.fields.clear();
+  for (;;) {
+    const uint32_t v = c.u32();
+    if (v == (kNew | 2u)) break;
+    p.fields.push_back(v);
+    if (p.fields.size() > 16) bad("crypto parameter fields");
+  }
+  if (get_str(c, 256) != kSchemeName) bad("scheme type");
+  if (c.u32() != (kNew | (id0 + 3 + p.L))) bad("scheme id");
+  c.u32();
+  c.u32();
+  p.enabled = c.u32();
+  if (get_str(c, 64) != "CKKS") bad("scheme id string");
+  if (c.p != obj.size()) bad("trailing bytes after the context");
+  if (modulus_product(p.q) != [&] {
+        std::vector<uint32_t> q = Q;
+        while (q.size() > 1 && !q.back()) q.pop_back();
+        return q;
+      }())
+    bad("context modulus is not the product of the towers");
+  if (first_id) *first_id = id0;
+  return p;
+}
+
+std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t id0) {
+  if (p.L < 1 || p.q.size() != p.L || p.psi.size() != p.L) bad("context parameters");
+  Out o;
+  o.u32(1);  // CryptoContextImpl version
+  o.u32(kNew | 1u);
+  o.str(kParamsName);
+  o.u32(kNew | id0);
+  for (int i = 0; i < 3; ++i) o.u32(0);
+  o.u32(kPoly);
+  o.u32(kNew | (id0 + 1));
+  o.u32(1);
+  o.u32(1);
+  o.u32(2 * p.N);
+  o.u32(p.N);
+  o.u8(1);
+  o.u32(1);  // BigInteger version
+  put_bigint(o, modulus_product(p.q), p.bigint_bytes);
+  if (p.elem_bigints.size() == 3ull * p.bigint_bytes) {
+    o.s += p.elem_bigints;
+  } else {
+    for (int i = 0; i < 3; ++i) put_bigint(o, {}, p.bigint_bytes);
+  }
+  o.u64(p.L);
+  for (uint32_t t = 0; t < p.L; ++t) {
+    o.u32(kPoly);
+    o.u32(kNew | (id0 + 2 + t));
+    if (t == 0) {
+      o.u32(1);
+      o.u32(1);
+    }
+    o.u32(2 * p.N);
+    o.u32(p.N);
+    o.u8(1);
+    if (t == 0) o.u32(1);  // NativeInteger version
+    o.u64(p.q[t]);
+    o.u64(p.psi[t]);
+    o.u64(0);
+    o.u64(0);
+  }
+  put_bigint(o, {}, p.bigint_bytes);  // originalModulus
+  o.u32(kPoly);
+  o.u32(kNew | (id0 + 2 + p.L));
+  o.u32(1);
+  o.u64(p.plaintext_modulus);
+  o.u64(0);
+  o.u64(0);
+  o.u64(0);
+  o.u32(0);
+  o.u32(p.batch);
+  o.f32(p.sigma);
+  o.f32(p.assurance);
+  o.f32(p.root_hermite);
+  for (uint32_t v : p.fields) o.u32(v);
+  o.u32(kNew | 2u);
+  o.str(kSchemeName);
+  o.u32(kNew | (id0 + 3 + p.L));
+  o.u32(0);
+  o.u32(0);
+  o.u32(p.enabled);
+  o.str("CKKS");
+  return o.s;
+}
+
+PalisadeCtxParams palisade_parse_context_file(const std::string& f) {
+  uint32_t a, id, id0 = 0;
+  if (f.size() < 64 || (uint8_t)f[0] != 0x01) bad("context file");
+  std::memcpy(&a, f.data() + 1, 4);
+  std::memcpy(&id, f.data() + 5, 4);
+  if (a != kPoly || id != (kNew | 1u)) bad("context file header");
+  PalisadeCtxParams p = palisade_parse_context_object(f.substr(9), &id0);
+  if (id0 != 2) bad("context file ids");
+  return p;
+}
+
+std::string palisade_context_file(const PalisadeCtxParams& p) {
+  Out o;
+  o.u8(0x01);
+  o.u32(kPoly);
+  o.u32(kNew | 1u);
+  o.s += palisade_context_object(p, 2);
+  return o.s;
+}
+
+std::string palisade_key_file(const PalisadeCtxParams& p, const std::string& keytag,
+                              const uint64_t* polys, bool is_public) {
+  const uint32_t N = p.N, L = p.L;
+  Out o;
+  o.u8(0x01);
+  o.u32(kPoly);
+  o.u32(kNew | 1u);
+  for (int i = 0; i < 3; ++i) o.u32(0);  // LPPublicKeyImpl / LPPrivateKeyImpl, LPKey, CryptoObject
+  o.u32(kPoly);
+  o.u32(kNew | 2u);
+  o.s += palisade_context_object(p, 3);
+  o.str(keytag);
+  const int nelem = is_public ? 2 : 1;
+  if (is_public) o.u64(2);
+  o.s.reserve(o.s.size() + (size_t)nelem * L * (N * 8 + 64) + 64);
+  for (int e = 0; e < nelem; ++e) {
+    if (e == 0) o.u32(1);  // DCRTPoly version
+    o.u64(L);
+    for (uint32_t t = 0; t < L; ++t) {
+      if (e == 0 && t == 0) o.u32(1);  // PolyImpl version
+      o.u32(kPoly);
+      o.u8(0x01);
+      if (e == 0 && t == 0) o.u32(1);  // NativeVector version
+      o.u64(N);
+      o.put(polys + ((size_t)e * L + t) * N, (size_t)N * 8);
+      o.u64(p.q[t]);
+      o.u32(0);  // EVALUATION
+      o.u32(kPoly);
+      o.u32(5 + t);  // the context's tower parameters (ids from 3: params, element, towers)
+    }
+    o.u32(0);
+    o.u32(kPoly);
+    o.u32(4);
+  }
+  return o.s;
+}
 
 bool palisade_looks_like_archive(const uint8_t* b, size_t len) {
   if (len < 9 || b[0] != 0x01) return false;
@@ -199,13 +520,41 @@ PalisadeArchive palisade_parse_archive(const uint8_t* b, size_t len) {
         else if (q != A.q[t]) bad("tower moduli differ");
         if (c.u32() != 0) bad("residues must be in EVALUATION format");
         c.expect32(kPoly, "tower params pointer");
-        const uint32_t pid = c.u32();
+        uint32_t pid = c.u32();
+        if (pid & kNew) {  // the key's own tower parameters (palisade_layout key_params)
+          if (k || e) bad("tower params object outside the first polynomial");
+          pid &= ~kNew;
+          if (c.u32() != 2 * A.N || c.u32() != A.N) bad("tower params ring dimension");
+          c.get<uint8_t>();
+          if (c.u64() != A.q[t]) bad("tower params modulus");
+          c.u64();
+          c.u64();
+          c.u64();
+        }
         if (k == 0 && e == 0) tower_ids[t] = pid;
         else if (pid != tower_ids[t]) bad("tower params reference");
       }
       if (c.u32() != 0) bad("element must be in EVALUATION format");
       c.expect32(kPoly, "element params pointer");
-      const uint32_t eid = c.u32();
+      uint32_t eid = c.u32();
+      if (eid & kNew) {  // the key's own ILDCRTParams: towers by reference
+        if (k || e) bad("element params object outside the first polynomial");
+        eid &= ~kNew;
+        if (!ctx_id || !A.ctx_len) bad("element params before the context");
+        const PalisadeCtxParams cp = palisade_parse_context_object(
+            std::string((const char*)b + A.ctx_off, A.ctx_len), nullptr);
+        if (c.u32() != 2 * A.N || c.u32() != A.N) bad("element params ring dimension");
+        c.get<uint8_t>();
+        c.need(4ull * cp.bigint_bytes);
+        c.p += 4ull * cp.bigint_bytes;
+        if (c.u64() != A.L) bad("element params tower count");
+        for (uint32_t t = 0; t < A.L; ++t) {
+          c.expect32(kPoly, "element params tower pointer");
+          if (c.u32() != tower_ids[t]) bad("element params tower reference");
+        }
+        c.need(cp.bigint_bytes);
+        c.p += cp.bigint_bytes;
+      }
       if (k == 0 && e == 0) elem_id = eid;
       else if (eid != elem_id) bad("element params reference");
     }
@@ -233,11 +582,23 @@ PalisadeArchive palisade_parse_archive(const uint8_t* b, size_t len) {
 std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::string& keytag,
                                     uint32_t N, uint32_t L, const uint64_t* q, uint64_t K,
                                     uint64_t depth, uint64_t level, double scale, uint32_t encoding,
-                                    bool vector_archive, uint8_t* buf, size_t* total) {
+                                    bool vector_archive, bool key_params, uint8_t* buf,
+                                    size_t* total) {
   if (!vector_archive && K != 1) bad("a single-ciphertext archive holds exactly one ciphertext");
   const std::vector<uint32_t> ids = context_ids(ctx_obj, 3);
   if (ids.size() < 2 + (size_t)L) bad("context has fewer tower parameter sets than towers");
   const uint32_t nctx = (uint32_t)ids.size(), elem_id = ids[1];
+  PalisadeCtxParams kp;
+  if (key_params) {
+    uint32_t id0 = 0;
+    kp = palisade_parse_context_object(ctx_obj, &id0);
+    if (id0 != 3 || kp.N != N || kp.L != L) bad("context does not match the ciphertext parameters");
+    for (uint32_t t = 0; t < L; ++t)
+      if (kp.q[t] != q[t]) bad("context moduli do not match the ciphertext parameters");
+  }
+  // ids after the context: [the key's tower params x L, its ILDCRTParams], then per
+  // ciphertext its metadata map (first) or pointer + metadata map (later ones)
+  const uint32_t kid0 = 3 + nctx, extra = key_params ? L + 1 : 0;
   size_t pos = 0;
   auto put = [&](const void* v, size_t n) {
     if (buf) std::memcpy(buf + pos, v, n);
@@ -246,6 +607,17 @@ std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::strin
   auto p8 = [&](uint8_t v) { put(&v, 1); };
   auto p32 = [&](uint32_t v) { put(&v, 4); };
   auto p64 = [&](uint64_t v) { put(&v, 8); };
+  std::string tower_obj[kMaxTowers], elem_obj;
+  if (key_params) {
+    for (uint32_t t = 0; t < L; ++t) {
+      Out o;
+      put_tower_params(o, N, kp.q[t], kp.psi[t]);
+      tower_obj[t] = std::move(o.s);
+    }
+    Out o;
+    put_dcrt_params_refs(o, kp, kid0);
+    elem_obj = std::move(o.s);
+  }
   std::vector<size_t> off;
   off.reserve(K * 2 * L);
   p8(0x01);
@@ -253,7 +625,7 @@ std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::strin
   for (uint64_t k = 0; k < K; ++k) {
     const bool first = (k == 0);
     p32(kPoly);
-    p32(kNew | (first ? 1u : (uint32_t)(2 + nctx + 2 * k)));
+    p32(kNew | (first ? 1u : (uint32_t)(2 + nctx + 2 * k + extra)));
     if (first) {
       p32(1);  // CiphertextImpl version (CT1.txt)
       p32(0);  // CryptoObject version
@@ -269,6 +641,7 @@ std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::strin
     put(keytag.data(), keytag.size());
     p64(2);
     for (int e = 0; e < 2; ++e) {
+      const bool embed = key_params && first && e == 0;
       if (first && e == 0) p32(1);  // DCRTPoly version
       p64(L);
       for (uint32_t t = 0; t < L; ++t) {
@@ -282,17 +655,27 @@ std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::strin
         p64(q[t]);
         p32(0);  // EVALUATION
         p32(kPoly);
-        p32(ids[2 + t]);
+        if (embed) {
+          p32(kNew | (kid0 + t));
+          put(tower_obj[t].data(), tower_obj[t].size());
+        } else {
+          p32(key_params ? kid0 + t : ids[2 + t]);
+        }
       }
       p32(0);
       p32(kPoly);
-      p32(elem_id);
+      if (embed) {
+        p32(kNew | (kid0 + L));
+        put(elem_obj.data(), elem_obj.size());
+      } else {
+        p32(key_params ? kid0 + L : elem_id);
+      }
     }
     p64(depth);
     p64(level);
     put(&scale, 8);
     p32(encoding);
-    p32(kNew | (uint32_t)(3 + nctx + 2 * k));  // metadata map, empty
+    p32(kNew | (uint32_t)(3 + nctx + 2 * k + extra));  // metadata map, empty
     p64(0);
   }
   *total = pos;

@@ -45,10 +45,57 @@ bool palisade_looks_like_archive(const uint8_t* b, size_t len);
 // buf (nullptr: only sizes it), sets *total and returns the [K][2][L] tower offsets
 // where the N residues of each tower go.  ctx_obj: an embedded context object whose
 // shared-ptr ids start at 3 (from a public key archive or a parsed ciphertext archive).
+// key_params: the ciphertexts' polynomials carry their own element-parameter objects
+// (embedded at the first ciphertext's c0), as every archive the reference's
+// encrypt / computeWeightedAverage writes does: there the key is loaded from
+// key-public.txt (ckks.cpp:16), so Encrypt's c0 = b*v + e0 + m and c1 = a*v + e1 inherit
+// the key file's ILDCRTParams, a different object from the context's (pinned by
+// code/params_results.csv:12-16, tests/test_palisade_codec.py).  false: they reference
+// the context's parameters (CT1.txt, written where the keys were generated in-process).
 std::vector<size_t> palisade_layout(const std::string& ctx_obj, const std::string& keytag,
                                     uint32_t N, uint32_t L, const uint64_t* q, uint64_t K,
                                     uint64_t depth, uint64_t level, double scale, uint32_t encoding,
-                                    bool vector_archive, uint8_t* buf, size_t* total);
+                                    bool vector_archive, bool key_params, uint8_t* buf,
+                                    size_t* total);
+
+// The CryptoContext object: LPCryptoParametersCKKS (ILDCRTParams with one ILNativeParams
+// per tower, EncodingParams, the RLWE fields) + LPPublicKeyEncryptionSchemeCKKS + "CKKS".
+//   ctx      := u32 1  0x80000001 str(ParamsName)  new(id) u32 0 x3
+//               elem   enc  f32 sigma  f32 assurance  f32 rootHermite  u32 field*
+//               0x80000002 str(SchemeName)  new(id+3+L) u32 0 x2  u32 enabled  str("CKKS")
+//   elem     := 0x40000000 new(id+1) [u32 1 u32 1] u32 2N u32 N u8 1 [u32 1]
+//               big(Q) big(0) big(0) big(0)  u64 L  tower^L  big(0)
+//   tower_t  := 0x40000000 new(id+2+t) [u32 1 u32 1] u32 2N u32 N u8 1 [u32 1] u64 q
+//               u64 psi u64 0 u64 0
+//   enc      := 0x40000000 new(id+2+L) [u32 1] u64 scaleBits u64 0 x3 u32 0 u32 batch
+//   big(x)   := BigIntegerFixedT<u32, 3500>: 110 u32 limbs, most significant first,
+//               then u16 bit length (442 bytes)
+// [..] = class versions at a type's first occurrence; str = u64 length + chars.
+struct PalisadeCtxParams {
+  uint32_t N = 0, L = 0;
+  std::vector<uint64_t> q, psi;
+  uint64_t plaintext_modulus = 0;  // CKKS stores the scaling-factor bits here
+  uint32_t batch = 0;
+  float sigma = 3.19f, assurance = 9.0f, root_hermite = 1.006f;
+  // u32 block after the floats: 9 fields in the benchmark's cryptoparams (1.11.7), 8 in
+  // palisade_pybind's (an older 1.11 writer)
+  std::vector<uint32_t> fields = {0, 1, 2, 0, 1, 0, 2, 1, 2};
+  uint32_t enabled = 5;         // ENCRYPTION | SHE (ckks.cpp:34-35)
+  uint32_t bigint_bytes = 442;  // BigIntegerFixedT<uint32_t, 3500>
+  std::string elem_bigints;     // root, bigQ, bigRoot of the ILDCRTParams (parsed; else 0)
+};
+
+// Structured parse of a context object whose first shared-ptr id is *first_id
+// (2: standalone cryptocontext.txt body, 3: embedded in a key or ciphertext archive).
+PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id);
+std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t first_id);
+// Structured parse of a standalone cryptocontext.txt (throws on other layouts)
+PalisadeCtxParams palisade_parse_context_file(const std::string& file);
+// cryptocontext.txt as ckks.cpp:41 writes it (Serial::SerializeToFile of the context)
+std::string palisade_context_file(const PalisadeCtxParams& p);
+// key-public.txt (polys = [2][L][N]: b, a) or key-private.txt ([L][N]: s), ckks.cpp:48,53
+std::string palisade_key_file(const PalisadeCtxParams& p, const std::string& keytag,
+                              const uint64_t* polys, bool is_public);
 
 // key-public.txt (ckks.cpp:48): the embedded context object and the key tag.
 void palisade_key_context(const std::string& pub, std::string& ctx_obj, std::string& keytag);

@@ -146,7 +146,7 @@ struct shelfi_ctx {
   uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
   uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
                                  // [2] max decode logError (noise flooding)
-  int decode_noise = 0;          // shelfi_set_decode_noise
+  int decode_noise = 1;          // shelfi_set_decode_noise (PALISADE floods every decode)
   double decode_m_factor = 1.0;
   int last_log_error = -1;       // of the last flooded decrypt, -1 if none
   std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)

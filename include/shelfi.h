@@ -84,10 +84,13 @@ int shelfi_set_seed(shelfi_ctx* ctx, uint64_t seed);
 
 /* ---- keys ----------------------------------------------------------------- */
 /* ckks.cpp:25-59 genCryptoContextAndKeyGen: generates keys on the device and writes
- * cryptodir/{cryptocontext,key-public,key-private}.txt (this library's format). */
+ * cryptodir/{cryptocontext,key-public,key-private}.txt in PALISADE 1.11's cereal
+ * PortableBinary format (ckks.cpp:41-55; byte-identical to what the reference writes for
+ * the same parameters, keys and key tag).  cryptodir = "" or NULL: keys stay in memory. */
 int shelfi_keygen(shelfi_ctx* ctx, const char* cryptodir);
-/* ckks.cpp:11-23 loadCryptoParams: reads either this library's key files or the
- * reference's PALISADE 1.11 cereal-binary files (code/resources/cryptoparams/). */
+/* ckks.cpp:11-23 loadCryptoParams: reads PALISADE 1.11 cereal-binary files (the
+ * reference's code/resources/cryptoparams/, or shelfi_keygen's) and this library's
+ * round-1 key files ("SHCC"/"SHPK"/"SHSK"). */
 int shelfi_load(shelfi_ctx* ctx, const char* cryptodir);
 /* Raw key import/export ([2][L][N] public (b, a), [L][N] secret, EVALUATION). */
 int shelfi_set_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk);
@@ -115,8 +118,9 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
 /* Decode noise flooding, PALISADE 1.11 CKKSPackedEncoding::Decode:
  * symmetrize, estimate sigma from the anti-symmetric part, add Gaussian noise of
  * stddev sqrt(m_factor + 1) * max(sigma, sqrt(N)/8) (m_factor = CKKS_M_FACTOR, 1 in
- * PALISADE), fail with SHELFI_ERR_PRECISION when log2 sigma > scale_bits - 5.  Off by
- * default (exact, deterministic decode); applies to shelfi_decrypt and
+ * PALISADE), fail with SHELFI_ERR_PRECISION when log2 sigma > scale_bits - 5.  ON by
+ * default with m_factor 1, like the Decrypt it replaces (ckks.cpp:189); enabled = 0 gives
+ * the exact, deterministic decode (parity mode).  Applies to shelfi_decrypt and
  * shelfi_dev_decrypt.  Randomness: the ctx's seeded / OS-random ChaCha20 stream. */
 int shelfi_set_decode_noise(shelfi_ctx* ctx, int enabled, double m_factor);
 /* logError of the last flooded decrypt (max over its ciphertexts; PALISADE
@@ -154,11 +158,26 @@ int shelfi_set_wire_format(shelfi_ctx* ctx, int format); /* 0 blob (default), 1 
 int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
                           uint64_t* residues);
 /* Host-only: write an archive (free with shelfi_free) from residues [K][2][L][N] and an
- * embedded context object (shared-pointer ids from 3: shelfi_palisade_key_context). */
+ * embedded context object (shared-pointer ids from 3: shelfi_palisade_key_context).
+ * flags: SHELFI_PAL_VECTOR = vector<Ciphertext> (else a single Ciphertext, K = 1);
+ * SHELFI_PAL_KEY_PARAMS = the polynomials carry the key's own parameter objects, as in
+ * every archive the reference's encrypt / computeWeightedAverage writes (its keys are
+ * loaded from files); without it they reference the context's (CT1.txt). */
+#define SHELFI_PAL_VECTOR 1
+#define SHELFI_PAL_KEY_PARAMS 2
 int shelfi_palisade_write(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
                           uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
                           uint64_t num_cts, const uint64_t* residues, uint64_t depth, uint64_t level,
-                          double scale, int vector_archive, uint8_t** out, size_t* out_len);
+                          double scale, int flags, uint8_t** out, size_t* out_len);
+/* Host-only: cryptocontext.txt as ckks.cpp:41 serializes the context of
+ * genCryptoContextCKKS(multDepth = L - 1, scale_bits, batch) with these towers. */
+int shelfi_palisade_context_file(uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli,
+                                 const uint64_t* roots, uint32_t scale_bits, uint32_t batch,
+                                 uint8_t** out, size_t* out_len);
+/* Host-only: key-public.txt (is_public = 1, polys [2][L][N]: b, a) or key-private.txt
+ * (polys [L][N]: s) around an embedded context object (ids from 3), ckks.cpp:48,53. */
+int shelfi_palisade_key_file(const uint8_t* ctx_obj, size_t ctx_len, const char* keytag,
+                             const uint64_t* polys, int is_public, uint8_t** out, size_t* out_len);
 /* Host-only: the embedded context object (free with shelfi_free) and key tag of a
  * PALISADE key-public.txt (ckks.cpp:48). */
 int shelfi_palisade_key_context(const uint8_t* pub, size_t len, uint8_t** ctx_obj, size_t* ctx_len,

@@ -1,0 +1,89 @@
+"""API guards on the HIP path: scaling factors the reference's EvalMult cannot represent
+are refused (NaN, +-inf, |w * Delta| >= 2^63: the int64 cast of ckks.cpp:287-288 is
+undefined there), forged blob headers are refused by every consumer, and decrypt floods
+by default as the reference's Decrypt does (ckks.cpp:189)."""
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import PALISADE_DIR
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ck():
+    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=21, decodeNoise=False)
+    c.loadCryptoParams()
+    return c
+
+
+BAD_WEIGHTS = [float("nan"), float("inf"), -float("inf"), 4096.0, -4096.0, 3.0e38]
+
+
+@pytest.mark.parametrize("bad", BAD_WEIGHTS)
+def test_bytes_api_rejects_unrepresentable_weights(ck, bad):
+    x = np.linspace(-1, 1, 5000)
+    a, b = ck.encrypt(x), ck.encrypt(-x)
+    with pytest.raises(ValueError, match="scaling factor"):
+        ck.computeWeightedAverage([a, b], [0.5, bad])
+    # the context stays usable and a representable weight still works
+    assert np.abs(ck.decrypt(ck.computeWeightedAverage([a, b], [0.5, 0.25]), 5000) - 0.25 * x).max() < 1e-7
+
+
+@pytest.mark.parametrize("bad", BAD_WEIGHTS[:4])
+@pytest.mark.parametrize("C", [2, 20])
+def test_device_api_rejects_unrepresentable_weights(ck, bad, C):
+    K = 2
+    cts = [D.empty_ct(ck, K).zero_() for _ in range(C)]
+    w = [0.1] * C
+    w[-1] = bad
+    with pytest.raises(ValueError, match="scaling factor"):
+        D.wavg(ck, cts, w)
+    ar = D.Arena(ck, C, K)
+    for i in range(C):
+        ar.put(i, cts[i])
+    with pytest.raises(ValueError, match="scaling factor"):
+        ar.wavg(w)
+    torch.cuda.synchronize()
+
+
+def test_largest_representable_weight_is_accepted(ck):
+    """|w| * Delta just below 2^63 (Delta = q_last ~ 2^52): w = 2047 is representable."""
+    x = np.full(100, 1e-3)
+    a = ck.encrypt(x)
+    out = ck.decrypt(ck.computeWeightedAverage([a], [2047.0]), 100)
+    assert np.abs(out - 2.047).max() < 1e-6
+
+
+def test_forged_blob_count_is_refused(ck):
+    x = np.linspace(-1, 1, 100)
+    blob = bytearray(ck.encrypt(x))
+    ct_bytes = 2 * 2 * 8192 * 8
+    # K * ct_bytes = 2^64 + ct_bytes wraps to this 1-ciphertext blob's payload length
+    for K in (2 ** 64 // ct_bytes + 1, 2 ** 46, 2 ** 63 + 1):
+        forged = bytes(blob[:16]) + struct.pack("<Q", K) + bytes(blob[24:])
+        with pytest.raises(RuntimeError, match="length"):
+            ck.decrypt(forged, 100)
+        with pytest.raises(RuntimeError, match="length"):
+            ck.computeWeightedAverage([forged], [1.0])
+
+
+def test_decrypt_floods_by_default():
+    """CKKS() without decodeNoise=False adds PALISADE's decode noise: two decryptions of
+    one ciphertext differ, both within the noise's scale of the exact decode."""
+    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR)
+    c.loadCryptoParams()
+    x = np.random.default_rng(3).uniform(-1, 1, 4096)
+    a = c.encrypt(x)
+    d1, d2 = c.decrypt(a, 4096), c.decrypt(a, 4096)
+    assert not np.array_equal(d1, d2)
+    assert np.abs(d1 - x).max() < 1e-7 and np.abs(d2 - x).max() < 1e-7
+    assert c.last_log_precision() is not None
+    c.set_decode_noise(False)
+    e1, e2 = c.decrypt(a, 4096), c.decrypt(a, 4096)
+    assert np.array_equal(e1, e2)

@@ -22,7 +22,7 @@ from SHELFI_FHE import dist as X  # noqa: E402
 @pytest.fixture(scope="module")
 def ck(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("keys_comm")) + os.sep
-    c = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7)
+    c = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
     assert c.genCryptoContextAndKeyGen() == 1
     return c
 

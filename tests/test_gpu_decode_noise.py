@@ -24,7 +24,7 @@ def _arrays(ck):
 
 @pytest.fixture(scope="module")
 def ck1():
-    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR)
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, decodeNoise=False)
     ck.loadCryptoParams()
     return ck
 
@@ -32,7 +32,7 @@ def ck1():
 @pytest.fixture(scope="module")
 def ck2(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("keys_noise")) + os.sep
-    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7)
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 

@@ -14,7 +14,7 @@ from SHELFI_FHE import fedavg as F  # noqa: E402
 
 @pytest.fixture(scope="module")
 def ck():
-    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=5)
+    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=5, decodeNoise=False)
     c.loadCryptoParams()
     return c
 

@@ -20,10 +20,10 @@ def test_product_reproduces_golden(name, tmp_path):
     rec, arrays = load(name)
     slots, depth, kseed, n = G.CASES[name]
     if kseed is None:
-        ck = m.CKKS("ckks", slots, 52, PALISADE_DIR)
+        ck = m.CKKS("ckks", slots, 52, PALISADE_DIR, decodeNoise=False)
         ck.loadCryptoParams()
     else:
-        ck = m.CKKS("ckks", slots, 52, str(tmp_path) + os.sep, multDepth=depth, seed=kseed)
+        ck = m.CKKS("ckks", slots, 52, str(tmp_path) + os.sep, multDepth=depth, seed=kseed, decodeNoise=False)
         assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
     N, L = inf["ring_dim"], inf["num_towers"]

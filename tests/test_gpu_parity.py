@@ -30,7 +30,7 @@ def _ctx_arrays(ck):
 @pytest.fixture(scope="module")
 def cfg1():
     """BASELINE config 1: the reference's own PALISADE keys (N=2^13, L=2, batch 4096)."""
-    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42)
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42, decodeNoise=False)
     ck.loadCryptoParams()
     assert ck.info()["keys_loaded"]
     return ck
@@ -40,7 +40,7 @@ def cfg1():
 def cfg2(tmp_path_factory):
     """BASELINE config 2/3/5 parameters: N=2^15, L=4 (multDepth 3), batch 16384."""
     d = str(tmp_path_factory.mktemp("keys_c2")) + os.sep
-    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7)
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 
@@ -49,7 +49,7 @@ def cfg2(tmp_path_factory):
 def cfg4(tmp_path_factory):
     """BASELINE config 4 parameters: N=2^16, L=6 (multDepth 5), batch 32768."""
     d = str(tmp_path_factory.mktemp("keys_c4")) + os.sep
-    ck = m.CKKS("ckks", 32768, 52, d, multDepth=5, seed=9)
+    ck = m.CKKS("ckks", 32768, 52, d, multDepth=5, seed=9, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 
@@ -82,7 +82,7 @@ def test_params_and_keygen_match_oracle(cfg, request):
 
 
 def test_keyfiles_roundtrip(cfg2):
-    ck2 = m.CKKS("ckks", 16384, 52, cfg2.cryptodir, multDepth=3)
+    ck2 = m.CKKS("ckks", 16384, 52, cfg2.cryptodir, multDepth=3, decodeNoise=False)
     ck2.loadCryptoParams()
     a, b = ck2.get_keys(), cfg2.get_keys()
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

@@ -39,7 +39,7 @@ SHAPES = [
 @pytest.mark.parametrize("batch,ring,depth,sb,fb", SHAPES)
 def test_encrypt_decrypt_ntt_bitexact(batch, ring, depth, sb, fb, tmp_path):
     ck = m.CKKS("ckks", batch, sb, str(tmp_path) + os.sep, multDepth=depth, firstModBits=fb, ringDim=ring,
-                seed=5)
+                seed=5, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
     q = np.array(inf["moduli"], np.uint64)

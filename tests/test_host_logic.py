@@ -111,6 +111,19 @@ def test_blob_info_validation():
         m.blob_info(b"XXXX" + blob[4:])
 
 
+@pytest.mark.parametrize("K", [2 ** 46, 2 ** 46 + 1, 2 ** 63 + 1, 2 ** 64 - 1])
+def test_blob_header_with_wrapping_K_is_rejected(K):
+    """A forged K whose K * ct_bytes wraps mod 2^64 (2^46 * 2^18 = 2^64 at 2^13/L2) must
+    not pass the length check: every consumer of the header (blob_info, decrypt,
+    weighted_average) goes through the same parse."""
+    hdr = bytearray(64)
+    hdr[0:4] = b"SHCT"
+    struct.pack_into("<HHIIQIIdQQII", hdr, 4, 1, 64, 13, 2, K, 1, 0, 2.0 ** 52, 1, 2, 4096, 4)
+    for payload in (b"", bytes(2 * 2 * 8192 * 8)):
+        with pytest.raises(RuntimeError, match="length"):
+            m.blob_info(bytes(hdr) + payload)
+
+
 def test_no_gpu_fails_loudly():
     torch = pytest.importorskip("torch")
     if torch.cuda.is_available():

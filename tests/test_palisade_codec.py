@@ -6,10 +6,20 @@ Pins (reference artifacts, tests/golden/palisade*):
     encoding, and re-writing it from the parsed parts reproduces the file byte for byte;
   * each key dir's cryptocontext.txt, re-embedded one shared-pointer id later, equals
     the context object inside its key-public.txt (both dirs).
-The vector<Ciphertext> framing (ckks.cpp:98-100) is cereal's standard size tag +
-elements; no vector archive of the reference is committed, so that part is checked by
-round trips only."""
+  * the context writer (genCryptoContextAndKeyGen's cryptocontext.txt) reproduces the
+    committed file byte for byte from (N, q, psi, scale bits, batch), and the key-file
+    writer reproduces both dirs' key-public.txt / key-private.txt from their parsed
+    residues and key tag;
+  * the vector<Ciphertext> framing of what the reference's encrypt() returns: the pickled
+    per-key archives of CNN_OriginalFedAvg have exactly the byte counts the reference
+    recorded (code/params_results.csv:2-16, written by benchmark_crypto.py:183-191).
+    That count pins the key-parameter objects PALISADE embeds at the first ciphertext
+    (palisade_codec.h, key_params)."""
+import collections
+import ctypes as C
+import math
 import os
+import pickle
 
 import numpy as np
 import pytest
@@ -92,3 +102,84 @@ def test_malformed_archives_are_rejected():
     flipped[2680] = ord("Z")  # key tag must be lowercase hex
     with pytest.raises(RuntimeError):
         m.palisade_parse(bytes(flipped))
+
+
+def _read_keys(d):
+    lib = m._lib.load()
+    N, L = C.c_uint32(), C.c_uint32()
+    check_rc = m._lib.check
+    check_rc(lib.shelfi_read_palisade((d + os.sep).encode(), C.byref(N), C.byref(L), None, None, None, None))
+    N, L = N.value, L.value
+    q, psi = (C.c_uint64 * 16)(), (C.c_uint64 * 16)()
+    pk = np.zeros((2, L, N), np.uint64)
+    sk = np.zeros((L, N), np.uint64)
+    check_rc(lib.shelfi_read_palisade((d + os.sep).encode(), None, None, q, psi,
+                                      pk.ctypes.data_as(m._lib.u64p), sk.ctypes.data_as(m._lib.u64p)))
+    return N, [int(q[i]) for i in range(L)], [int(psi[i]) for i in range(L)], pk, sk
+
+
+def test_context_writer_reproduces_the_reference_file():
+    """ckks.cpp:28,41: genCryptoContextCKKS(1, 52, 4096) serialized; the towers come from
+    this library's prime rule (params_generate), everything else from the writer."""
+    N, q, psi = m.params_generate(4096, 52, 1)
+    ref = open(os.path.join(PALISADE_DIR, "cryptocontext.txt"), "rb").read()
+    assert m.palisade_context_file(N, q, psi, 52, 4096) == ref
+    # and its embedded form is what key files and ciphertext archives carry
+    pub = open(os.path.join(PALISADE_DIR, "key-public.txt"), "rb").read()
+    assert m.palisade_embed_context(ref) == m.palisade_key_context(pub)[0]
+
+
+@pytest.mark.parametrize("d", [PALISADE_DIR, PALISADE_PYBIND_DIR])
+def test_key_writer_reproduces_the_reference_files(d):
+    N, q, psi, pk, sk = _read_keys(d)
+    pub = open(os.path.join(d, "key-public.txt"), "rb").read()
+    priv = open(os.path.join(d, "key-private.txt"), "rb").read()
+    ctx_obj, tag = m.palisade_key_context(pub)
+    assert m.palisade_key_file(ctx_obj, tag, pk, True) == pub
+    assert m.palisade_key_file(ctx_obj, tag, sk, False) == priv
+
+
+# code/benchmark_crypto.py:85-96 (CNN_OriginalFedAvg state_dict, 1,663,370 params)
+CNN_KEYS = [("conv2d_1.weight", 800), ("conv2d_1.bias", 32), ("conv2d_2.weight", 51200),
+            ("conv2d_2.bias", 64), ("linear_1.weight", 1605632), ("linear_1.bias", 512),
+            ("linear_2.weight", 5120), ("linear_2.bias", 10)]
+# code/params_results.csv:2-16, "Communication" column per batch size (same for every
+# scale-bit setting: the ring stays 2^13 with 2 towers)
+PICKLED_BYTES = {1024: 427260022, 2048: 214437402, 4096: 108157302}
+
+
+@pytest.mark.parametrize("batch", sorted(PICKLED_BYTES))
+def test_pickled_encrypt_archives_match_params_results(batch):
+    """benchmark_crypto.py:183-191: enc_learner_layer[0] (an OrderedDict key ->
+    encrypt() bytes) pickled with HIGHEST_PROTOCOL.  Residue values do not change sizes."""
+    N, q, psi, _, _ = _read_keys(PALISADE_DIR)
+    pub = open(os.path.join(PALISADE_DIR, "key-public.txt"), "rb").read()
+    ctx_obj, tag = m.palisade_key_context(pub)
+    L, delta = len(q), float(q[-1])
+    od = collections.OrderedDict()
+    for k, n in CNN_KEYS:
+        K = math.ceil(n / batch)
+        r = np.zeros((K, 2, L, N), np.uint64)
+        od[k] = m.palisade_write(ctx_obj, tag, q, r, depth=1, level=0, scale=delta, key_params=True)
+    assert sum(math.ceil(n / batch) for _, n in CNN_KEYS) == {4096: 412, 2048: 817, 1024: 1628}[batch]
+    assert len(pickle.dumps(od, protocol=pickle.HIGHEST_PROTOCOL)) == PICKLED_BYTES[batch]
+
+
+@pytest.mark.parametrize("K", [1, 3])
+def test_key_params_archive_round_trip(K):
+    N, q, psi, _, _ = _read_keys(PALISADE_DIR)
+    pub = open(os.path.join(PALISADE_DIR, "key-public.txt"), "rb").read()
+    ctx_obj, tag = m.palisade_key_context(pub)
+    L = len(q)
+    rng = np.random.default_rng(K)
+    r = np.empty((K, 2, L, N), np.uint64)
+    for t in range(L):
+        r[:, :, t, :] = rng.integers(0, q[t], (K, 2, N), dtype=np.uint64)
+    a = m.palisade_write(ctx_obj, tag, q, r, depth=2, scale=float(q[-1]) ** 2, key_params=True)
+    b = m.palisade_write(ctx_obj, tag, q, r, depth=2, scale=float(q[-1]) ** 2)
+    assert len(a) - len(b) == 2325  # one ILDCRTParams (4 BigIntegers) + 2 tower objects
+    info, r2 = m.palisade_parse(a)
+    assert info["num_cts"] == K and info["depth"] == 2 and np.array_equal(r, r2)
+    # a truncated key-params object is refused
+    with pytest.raises(RuntimeError):
+        m.palisade_parse(a[:len(ctx_obj) + 3000])
