@@ -4,13 +4,18 @@ bit-for-bit, on small inputs (1-2 ciphertexts):
   - rings 2^12, 2^14: compile-time block passes with 1- and 3-stage columns passes;
   - sparse packing (gap = N / 2 batch of 2 and 4): the fused INTT + CRT decode with
     coefficients that are not slots;
-  - ring 2^16, L = 2: 11-stage blocks, 5-stage columns, fused CRT at 32 KiB of LDS
-    (cfg4, 2^16 with L = 6, takes the unfused CRT: tests/test_gpu_parity.py);
+  - ring 2^16, L = 2: 11-stage blocks, 5-stage columns, fused CRT at 32 KiB of LDS;
+  - ring 2^16, L = 4 and L = 6 (cfg4): the fused CRT needs 64 / 96 KiB of LDS, over its
+    limit -> unfused 5-stage columns pass + CRT kernel;
   - ring 2^17, L = 2: 12-stage blocks, 5-stage columns, fused CRT at 32 KiB of LDS;
   - ring 2^17, L = 4: fused CRT over its LDS limit -> unfused columns pass + CRT kernel;
   - 30-bit scaling primes (q < 2^40): the generic block kernels (no one-step reduction).
-The parameter sets follow PALISADE's chain rule, keys from keygen(seed)."""
+The parameter sets follow PALISADE's chain rule, keys from keygen(seed).
+SHELFI_NTT_BLOCK_LOG_BIG=12 (2^12 blocks at 2^16, read once per process) selects another
+kernel set: the large rings are re-run under it in a child process."""
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -30,6 +35,8 @@ SHAPES = [
     (8192, 32768, 3, 52, 60),  # N = 2^15, gap 2
     (4096, 32768, 3, 52, 60),  # N = 2^15, gap 4
     (32768, 0, 1, 52, 60),     # N = 2^16, L = 2: 2^11 blocks, 5-stage columns, fused CRT
+    (32768, 0, 3, 52, 60),     # N = 2^16, L = 4: unfused columns + CRT kernel
+    (32768, 0, 5, 52, 60),     # N = 2^16, L = 6 (cfg4)
     (65536, 0, 1, 52, 60),     # N = 2^17, L = 2
     (65536, 0, 3, 52, 60),     # N = 2^17, L = 4
     (4096, 0, 1, 30, 40),      # 30-bit scaling prime
@@ -64,3 +71,13 @@ def test_encrypt_decrypt_ntt_bitexact(batch, ring, depth, sb, fb, tmp_path):
     agg_res = m.blob_residues(agg, N, len(q))
     assert np.array_equal(agg_res, O.wavg([ref, ref], [0.25, 0.5], q, delta))
     assert np.array_equal(dec2, O.decrypt_vector(agg_res, sk, q, psi, S, delta * delta, n))
+
+
+@pytest.mark.skipif(os.environ.get("SHELFI_NTT_BLOCK_LOG_BIG") is not None, reason="already the child")
+def test_large_rings_with_2p12_blocks():
+    env = dict(os.environ, SHELFI_NTT_BLOCK_LOG_BIG="12")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        os.path.abspath(__file__), "-k", "bitexact and (32768-0 or 65536-0)"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert " passed" in r.stdout and " failed" not in r.stdout
