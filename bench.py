@@ -4,13 +4,14 @@
 A *step* is one encrypted FedAvg aggregation over one batch of synthetic input: every
 learner's ciphertexts (already resident in HBM) are scaled by its float32 weight and
 summed (ckks.cpp:264-320, EvalMult + EvalAdd) by the wavg kernel.  At N > 1 GPUs
-(weak scaling, 16 learners' worth of work per GPU) the default partitioning is by
-ciphertext index: rank r aggregates every learner's ciphertexts [k0, k1) with no
-collective (the aggregator routes each upload's ciphertext ranges to their GPU).  The
-learner-sharded alternative (BASELINE config 3's wording: each rank aggregates its own
-learners, one RCCL reduce_scatter over xGMI + modq combines the partial sums,
-SHELFI_FHE/dist.py) is measured in the same run and reported beside it
-(`alternative_partitioning`; --shard learners makes it the headline).
+(weak scaling, 16 learners' worth of work per GPU) the headline partitioning is
+BASELINE.json's north_star: client ciphertexts sharded by learner, each rank aggregates
+its own learners into a partial sum and an RCCL reduce_scatter over xGMI (uint64 SUM,
+then the modq kernel) combines them, overlapped piece by piece with the local wavg
+(SHELFI_FHE/dist.py PipelinedCombine; --combine shelfi runs the same combine through
+the library's own C-ABI communicator).  Sharding by ciphertext index instead (every
+rank aggregates all learners' ciphertexts [k0, k1), no collective) is measured in the
+same run and reported as `alternative_partitioning` (--shard cts makes it the headline).
 
 Workload (default): BASELINE config 3's per-GPU shard — 16 learners x ResNet-18
 (11,689,512 params -> 714 ciphertexts of 16384 slots), ring 2^15, L = 4 towers;
@@ -60,7 +61,7 @@ def parse():
     ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
     ap.add_argument("--pieces", type=int, default=8,
                     help="N>1: ciphertext pieces whose RCCL reduce_scatter overlaps the next piece's wavg")
-    ap.add_argument("--shard", choices=["learners", "cts"], default="cts",
+    ap.add_argument("--shard", choices=["learners", "cts"], default="learners",
                     help="N>1: learners = each rank aggregates its own learners, one RCCL reduce_scatter "
                          "combines the partial sums (BASELINE config 3); cts = each rank aggregates every "
                          "learner's slice of the ciphertexts (no collective; the host routes each upload's "
@@ -259,7 +260,7 @@ def main():
     Cl = args.learners_per_gpu or Cl_default
     # one key pair shared by every rank (seeded keygen, no key files written), then a
     # per-rank encryption stream
-    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, device=local, seed=7)
+    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, device=local, seed=7, decodeNoise=False)
     if ck.genCryptoContextAndKeyGen() != 1:
         raise SystemExit("keygen failed")
     ck.set_seed(1000 + rank)
@@ -324,11 +325,14 @@ def main():
         elif shard == "learners":
             comb = ShelfiCombine(ck, K, (2, L, N), dev)
 
-        def kernel():
+        def kernel_into(dst):
             if args.layout == "arena":
-                arena.wavg(weights, out=out)
+                arena.wavg(weights, out=dst)
             else:
-                D.wavg(ck, cts, weights, out=out)
+                D.wavg(ck, cts, weights, out=dst)
+
+        def kernel():
+            kernel_into(out)
 
         def piece(k0, k1, view):
             if args.layout == "arena":
@@ -343,7 +347,7 @@ def main():
             return comb.run(piece, lambda s_: D.modq(ck, s_))
 
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
-                "enc_times": enc_times, "kernel": kernel, "step": step, "comb": comb, "weights": weights,
+                "enc_times": enc_times, "kernel": kernel, "kernel_into": kernel_into, "step": step, "piece": piece, "comb": comb, "weights": weights,
                 "cts": cts, "placement": placement}
 
     def timed(mode):
@@ -404,6 +408,45 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = units / (elapsed / args.steps)
     check = None if args.no_check else checked(main_mode)
+    # the library's own C-ABI communicator (comm.cpp: RCCL uint64 SUM + mod-q fold inside
+    # libshelfi) on the same partial sums, outside the timed region: its all-reduced
+    # aggregate must equal the torch path's owned shares bit for bit on every rank
+    comm_check = None
+    if distributed and main_mode["shard"] == "learners" and args.combine == "torch":
+        try:
+            t0 = time.perf_counter()
+            comm = SD.Comm(ck, rank, world)
+            full = torch.empty((K, 2, L, N), dtype=torch.int64, device=dev)
+            main_mode["piece"](0, K, full)
+            comm.allreduce(full)
+            owned = main_mode["step"]()
+            torch.cuda.synchronize()
+            ok = all(torch.equal(sv, full[a:b]) for a, b, sv in owned)
+            comm.close()
+            okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+            comm_check = {"ok": bool(okt.item()), "seconds": round(time.perf_counter() - t0, 3),
+                          "what": "shelfi_dev_allreduce (C ABI, world %d) == torch reduce_scatter shares" % world}
+            del full
+        except Exception as e:  # reported, never fatal to the headline
+            comm_check = {"ok": False, "error": repr(e)[:300]}
+    # the same launches into a plain torch.empty output (no placement tuning): the
+    # kernel's placement-independent rate
+    untuned = None
+    if main_mode["placement"] is not None:
+        plain = torch.empty_like(main_mode["out"])
+        stream = torch.cuda.current_stream(dev)
+        evu = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        main_mode["kernel_into"](plain)
+        for a_, b_ in evu:
+            a_.record(stream)
+            main_mode["kernel_into"](plain)
+            b_.record(stream)
+        torch.cuda.synchronize()
+        um = [a_.elapsed_time(b_) for a_, b_ in evu]
+        untuned = sum(um) / len(um)
+        del plain
     # the other N > 1 partitioning, measured in the same run on the same inputs
     alt = None
     if distributed and not args.no_alt:
@@ -424,20 +467,26 @@ def main():
     cts_mode = main_mode["shard"] == "cts"
     local_wavg = main_mode["kernel"]
 
-    # device-resident decrypt+decode timing over the K aggregated ciphertexts
+    # device-resident decrypt+decode timing over the K aggregated ciphertexts: the exact
+    # decode (parity mode) and the default, PALISADE's noise-flooded decode (ckks.cpp:189)
     local_wavg()
     torch.cuda.synchronize()
-    dec = D.decrypt(ck, out, K_loc * batch, delta * delta)  # warm: sizes the scratch arena
-    torch.cuda.synchronize()
-    dts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
+
+    def time_decrypt(flood):
+        ck.set_decode_noise(flood)
+        dec = D.decrypt(ck, out, K_loc * batch, delta * delta)  # warm: sizes the scratch arena
         torch.cuda.synchronize()
-        dts.append(time.perf_counter() - t0)
-    dec_ms_per_ct = sorted(dts)[1] * 1e3 / K_loc
-    assert torch.isfinite(dec).all().item()
-    del dec
+        dts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
+            torch.cuda.synchronize()
+            dts.append(time.perf_counter() - t0)
+        assert torch.isfinite(dec).all().item()
+        return sorted(dts)[1] * 1e3 / K_loc
+
+    dec_ms_per_ct = time_decrypt(False)
+    dec_flood_ms_per_ct = time_decrypt(True)
 
     # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`
     api = None
@@ -477,6 +526,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "wavg_kernel", "bytes_per_launch": bytes_per_launch,
                 "launch_ms_avg": round(kern_avg_ms, 4), "launch_ms_min": round(kern_ms[0], 4)}
+    if untuned is not None:
+        roofline["untuned_output"] = {"launch_ms_avg": round(untuned, 4),
+                                      "frac": round(bytes_per_launch / (untuned * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "what": "same launches into a plain torch.empty output buffer"}
     # encrypt / decrypt per ciphertext: SURVEY §8(d) algorithmic bytes (f64 slots + ct,
     # keys amortized) over the measured time; these are VALU-bound (NTT), the HBM
     # fraction says how far from the memory bound they run
@@ -505,11 +558,14 @@ def main():
                                                    if args.combine == "torch" else
                                                    ", RCCL reduce_scatter through shelfi_dev_reduce_scatter")),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
-                   "parallelism": ("ciphertext-sharded dp%d" if cts_mode else "learner-sharded dp%d") % world,
+                   "parallelism": ("dp1 (one GPU, no collective)" if not distributed else
+                                   "ciphertext-sharded dp%d (no collective)" % world if cts_mode else
+                                   "learner-sharded dp%d + RCCL reduce_scatter over xGMI + modq" % world),
                    "layout": args.layout, "output_placement": main_mode["placement"]},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(enc_ms, 5),
         "decrypt_decode_ms_per_ct": round(dec_ms_per_ct, 5),
+        "decrypt_decode_flooded_ms_per_ct": round(dec_flood_ms_per_ct, 5),
         "encrypt_hbm_frac": frac(enc_bytes, enc_ms),
         "decrypt_hbm_frac": frac(dec_bytes, dec_ms_per_ct),
     }
@@ -517,6 +573,8 @@ def main():
         res["check"] = check
     if alt:
         res["alternative_partitioning"] = alt
+    if comm_check:
+        res["c_abi_comm_check"] = comm_check
     if api:
         res["api_bytes_path"] = api
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -41,15 +41,18 @@ def test_bench_single_gpu_line():
     assert r["n_gpus"] == 1 and r["steps"] == 3 and r["value"] > 0
     assert r["roofline"]["bound"] == "hbm" and 0 < r["roofline"]["frac"] < 1
     assert r["check"]["max_abs_err"] < 1e-8
+    assert r["decrypt_decode_flooded_ms_per_ct"] > 0
 
 
 def test_bench_distributed_path_one_rank():
-    """--shard learners headline (NCCL group, pipelined reduce_scatter, modq) with the
-    ciphertext-sharded alternative measured beside it."""
+    """The default N > 1 headline, learner-sharded (NCCL group, pipelined reduce_scatter,
+    modq), with the ciphertext-sharded alternative measured beside it and the C-ABI
+    communicator cross-checked on the same partial sums."""
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist", "--shard", "learners", "--pieces", "3"] + COMMON)
-    assert "reduce_scatter" in r["config"]["workload"]
+              "--force-dist", "--pieces", "3"] + COMMON)
+    assert "reduce_scatter" in r["config"]["workload"] and "RCCL" in r["config"]["parallelism"]
+    assert r["c_abi_comm_check"]["ok"], r["c_abi_comm_check"]
     assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
     alt = r["alternative_partitioning"]
     assert alt["parallelism"].startswith("ciphertext-sharded") and alt["value"] > 0
@@ -57,11 +60,11 @@ def test_bench_distributed_path_one_rank():
 
 
 def test_bench_ciphertext_sharded_path_one_rank():
-    """The default N > 1 layout, with the RCCL learner-sharded alternative beside it."""
+    """--shard cts (no collective), with the RCCL learner-sharded alternative beside it."""
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist"] + COMMON)
-    assert r["config"]["parallelism"] == "ciphertext-sharded dp1"
+              "--force-dist", "--shard", "cts"] + COMMON)
+    assert r["config"]["parallelism"] == "ciphertext-sharded dp1 (no collective)"
     assert r["check"]["max_abs_err"] < 1e-8
     alt = r["alternative_partitioning"]
     assert "RCCL" in alt["parallelism"] and alt["check"]["max_abs_err"] < 1e-8
