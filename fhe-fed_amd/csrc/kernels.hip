@@ -1091,40 +1091,8 @@ __global__ __launch_bounds__(256) void fft_inv_blocks(const double* __restrict__
 // stages len = 2..S with twiddle ffwd[len/2 + (x mod len)].  Small len in LDS
 // blocks, the top LOGR stages on register columns; the last pass writes the real
 // parts of the first `n` slots straight into the caller's output vector.
-__global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf, uint32_t logS,
-                                                      uint32_t blkLog, const double2* __restrict__ tw,
-                                                      double* __restrict__ out, uint64_t n,
-                                                      int final_pass) {
-  extern __shared__ __attribute__((aligned(16))) double2 smc[];
-  const uint32_t S = 1u << logS, blk = 1u << blkLog;
-  const uint32_t sh = logS - blkLog;
-  const uint64_t k = blockIdx.x >> sh;
-  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
-  const uint64_t off = k * S + ((uint64_t)b << blkLog);
-  for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];
-  __syncthreads();
-  for (uint32_t len = 2; len <= blk; len <<= 1) {
-    const uint32_t lenh = len >> 1;
-    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
-      const uint32_t j = p & (lenh - 1);
-      const uint32_t i0 = (p - j) * 2 + j;
-      const double2 W = tw[lenh + j];
-      const double2 u = smc[i0];
-      const double2 v = cmul(smc[i0 + lenh], W);
-      smc[i0] = cadd(u, v);
-      smc[i0 + lenh] = csub(u, v);
-    }
-    __syncthreads();
-  }
-  if (final_pass) {
-    for (uint32_t i = threadIdx.x; i < blk; i += 256) {
-      const uint64_t gi = off + i;
-      if (gi < n) out[gi] = smc[i].x;
-    }
-  } else {
-    for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
-  }
-}
+// fft_fwd_blocks (the first FFTSpecial pass) is defined with the decode-noise flooding
+// below, which it can fuse into its load.
 
 template <int LOGR>
 __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ buf, uint32_t logS,
@@ -1626,15 +1594,18 @@ __device__ __forceinline__ double block_sum_1024(double v, double* red) {
   return s;
 }
 
-// Box-Muller pair from two 64-bit words: u1 in (0, 1], u2 in [0, 1).
+// Box-Muller pair from two 64-bit words: u1 in (0, 1] (53 bits), u2 in [0, 1).  The
+// transcendental functions run in binary32 (one instruction each): the normals scale
+// noise ~1e-13 of the decoded values, so their 2^-24 relative error moves an output by
+// < 1e-20 (the oracle evaluates them in binary64).
 __device__ __forceinline__ void box_muller(uint64_t a, uint64_t b, double& z0, double& z1) {
-  const double u1 = (double)((a >> 11) + 1) * 0x1.0p-53;
-  const double u2 = (double)(b >> 11) * 0x1.0p-53;
-  const double r = sqrt(-2.0 * log(u1));
-  double sn, cs;
-  sincospi(2.0 * u2, &sn, &cs);
-  z0 = r * cs;
-  z1 = r * sn;
+  const float u1 = (float)((double)((a >> 11) + 1) * 0x1.0p-53);
+  const float u2 = (float)(b >> 40) * 0x1.0p-24f;  // revolutions
+  const float r = __fsqrt_rn(-2.0f * __logf(u1));
+  float sn, cs;
+  __sincosf(6.2831853071795864f * u2, &sn, &cs);
+  z0 = (double)(r * cs);
+  z1 = (double)(r * sn);
 }
 
 __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict__ fbuf, uint32_t logS,
@@ -1695,31 +1666,182 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
   }
   const double nsd = stddev_p / two_p;  // noise stddev in output units
   const uint64_t nonce = (3ull << 56) | (g0 + blockIdx.x);
+  // the normals of the slot at FFT-input position P: block P >> 1, pair P & 1
+  auto noise = [&](uint32_t P, double& za, double& zb) {
+    uint64_t w[8];
+    chacha20_block(key, P >> 1, nonce, w);
+    if (P & 1) box_muller(w[2], w[3], za, zb);
+    else box_muller(w[0], w[1], za, zb);
+  };
   __syncthreads();  // every thread has read its pairs before any is overwritten
   for (uint32_t i = threadIdx.x; i <= half; i += blockDim.x) {
-    uint64_t w[8];
-    chacha20_block(key, i, nonce, w);
-    double z[4];
-    box_muller(w[0], w[1], z[0], z[1]);
-    box_muller(w[2], w[3], z[2], z[3]);
     const uint32_t pi = bitrev_dev(i, logS);
     const double2 x = f[pi];
+    double z0, z1;
+    noise(pi, z0, z1);
     if (i == 0) {
-      f[pi] = make_double2(x.x + nsd * z[0], nsd * z[1]);
+      f[pi] = make_double2(x.x + nsd * z0, nsd * z1);
       if (S == 1) continue;
     } else if (i == half) {
-      f[pi] = make_double2(0.5 * (x.x - x.y) + nsd * z[0], 0.5 * (x.y - x.x) + nsd * z[1]);
+      f[pi] = make_double2(0.5 * (x.x - x.y) + nsd * z0, 0.5 * (x.y - x.x) + nsd * z1);
     } else {
       const uint32_t pj = bitrev_dev(S - i, logS);
       const double2 y = f[pj];
-      f[pi] = make_double2(0.5 * (x.x - y.y) + nsd * z[0], 0.5 * (x.y - y.x) + nsd * z[1]);
-      f[pj] = make_double2(0.5 * (y.x - x.y) + nsd * z[2], 0.5 * (y.y - x.x) + nsd * z[3]);
+      double z2, z3;
+      noise(pj, z2, z3);
+      f[pi] = make_double2(0.5 * (x.x - y.y) + nsd * z0, 0.5 * (x.y - y.x) + nsd * z1);
+      f[pj] = make_double2(0.5 * (y.x - x.y) + nsd * z2, 0.5 * (y.y - x.x) + nsd * z3);
     }
   }
 }
 
+// Flooding at 2^11 slots and more, in two steps that stream the slots once each:
+//  1. decode_stats_kernel: per ciphertext G = S/2048 workgroups sum the anti-symmetric
+//     components u (decode_flood_kernel's, over pairs (i, S - i)) and their squares;
+//  2. fft_fwd_blocks adds the noise while it loads its block (FloodArgs): sigma from
+//     the G partial sums (one-pass variance (sum u^2 - (sum u)^2 / S) / (S - 1)), the
+//     normals of position P from ChaCha20 block P >> 1 (a thread loads positions 2m,
+//     2m + 1: one block, two Box-Muller pairs).
+// The symmetrization (v + conj)/2 is left out: conj contributes only the imaginary part
+// of each decoded slot (m(1/zeta) = conj m(zeta) for real coefficients) and decrypt
+// keeps real parts, so the output is the same up to rounding (oracle tolerance 1e-14).
+// Slot i sits at FFT-input position P = bitrev(i); its conjugate partner S - i sits at
+// P ^ (2^h - 1), h = the index of P's leading bit (complementing i's bits above its
+// lowest set bit complements P's bits below its highest): the octave [2^h, 2^(h+1))
+// mirrored.  Pair m (0 <= m < S/2 - 1) is P = 2^h + o with m + 1 = 2^(h-1) + o, partner
+// 2^(h+1) - 1 - o: consecutive m read two contiguous runs (one backwards).  Positions 0
+// (slot 0) and 1 (slot S/2) are their own partners.
+constexpr uint32_t kFloodPairsPerWg = 1024;
+__global__ __launch_bounds__(256) void decode_stats_kernel(const double2* __restrict__ fbuf, uint32_t logS,
+                                                           uint32_t G, double2* __restrict__ part) {
+  __shared__ double red[2][4];
+  const uint32_t S = 1u << logS, half = S >> 1;
+  const uint64_t k = blockIdx.x / G;
+  const uint32_t wg = blockIdx.x % G;
+  const double2* __restrict__ f = fbuf + k * S;
+  double s1 = 0.0, s2 = 0.0;
+  const uint32_t m1 = min(half - 1, (wg + 1) * kFloodPairsPerWg);
+  for (uint32_t m = wg * kFloodPairsPerWg + threadIdx.x; m < m1; m += 256) {
+    const uint32_t hb = 31 - __clz(m + 1);  // h - 1
+    const uint32_t o = m + 1 - (1u << hb);
+    const double2 x = f[(2u << hb) + o], y = f[(4u << hb) - 1 - o];
+    const double a = x.x + y.y, b = x.y + y.x;
+    s1 += a + b;
+    s2 += a * a + b * b;
+  }
+  if (wg == 0 && threadIdx.x == 0) {
+    const double2 x0 = f[0], xh = f[1];  // slot 0: 2 im; slot S/2: re + im
+    const double a = 2.0 * x0.y, c = xh.x + xh.y;
+    s1 += a + c;
+    s2 += a * a + c * c;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_down(s1, o, 64);
+    s2 += __shfl_down(s2, o, 64);
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s1;
+    red[1][wave] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = make_double2((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]),
+                                    (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+}
+
+struct FloodArgs {
+  const double2* part;  // [K][G] (sum u, sum u^2) of decode_stats_kernel
+  uint32_t G, logN;
+  double two_p, p_bits, m_factor;
+  Key8 key;
+  uint64_t g0;
+  uint32_t* flags;  // [1] |= precision failure, [2] = max logError
+};
+
+// FFTSpecial first pass (decode): input already bit-reversed by the CRT's scatter; DIT
+// stages len = 2..blk with twiddle ffwd[len/2 + (x mod len)] in LDS blocks; the top LOGR
+// stages follow on register columns (fft_fwd_cols).  A single pass writes the real parts
+// of the first `n` slots straight into the caller's output vector.  FLOOD: the decode
+// noise is added while loading (see decode_stats_kernel).
+template <bool FLOOD>
+__global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf, uint32_t logS,
+                                                      uint32_t blkLog, const double2* __restrict__ tw,
+                                                      double* __restrict__ out, uint64_t n,
+                                                      int final_pass, FloodArgs fa) {
+  extern __shared__ __attribute__((aligned(16))) double2 smc[];
+  const uint32_t S = 1u << logS, blk = 1u << blkLog;
+  const uint32_t sh = logS - blkLog;
+  const uint64_t k = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint64_t off = k * S + ((uint64_t)b << blkLog);
+  if (FLOOD) {
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t g = 0; g < fa.G; ++g) {
+      const double2 v = fa.part[k * fa.G + g];
+      s1 += v.x;
+      s2 += v.y;
+    }
+    const double var = (s2 - s1 * (s1 / (double)S)) / (double)(S - 1);
+    double sigma_p = 0.5 * sqrt(var > 0.0 ? var : 0.0) * fa.two_p;
+    const bool fail = !(log2(sigma_p) <= fa.p_bits - 5.0);
+    const double floor_sd = 0.125 * sqrt((double)(1u << fa.logN));
+    if (sigma_p < floor_sd) sigma_p = floor_sd;
+    const double stddev_p = sqrt(fa.m_factor + 1.0) * sigma_p;
+    if (b == 0 && threadIdx.x == 0) {
+      if (fail) atomicOr(&fa.flags[1], 1u);
+      atomicMax((int*)&fa.flags[2], (int)rint(log2(stddev_p * sqrt(2.0 * (double)S))));
+    }
+    const double nsd = stddev_p / fa.two_p;
+    const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
+    const double4* src = reinterpret_cast<const double4*>(buf + off);
+    for (uint32_t m = threadIdx.x; m < blk / 2; m += 256) {  // positions 2m, 2m + 1
+      uint64_t w[8];
+      chacha20_block(fa.key, (((uint64_t)b << blkLog) >> 1) + m, nonce, w);
+      double z0, z1, z2, z3;
+      box_muller(w[0], w[1], z0, z1);
+      box_muller(w[2], w[3], z2, z3);
+      const double4 v = src[m];
+      smc[2 * m] = make_double2(v.x + nsd * z0, v.y + nsd * z1);
+      smc[2 * m + 1] = make_double2(v.z + nsd * z2, v.w + nsd * z3);
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];
+  }
+  __syncthreads();
+  for (uint32_t len = 2; len <= blk; len <<= 1) {
+    const uint32_t lenh = len >> 1;
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const uint32_t j = p & (lenh - 1);
+      const uint32_t i0 = (p - j) * 2 + j;
+      const double2 W = tw[lenh + j];
+      const double2 u = smc[i0];
+      const double2 v = cmul(smc[i0 + lenh], W);
+      smc[i0] = cadd(u, v);
+      smc[i0 + lenh] = csub(u, v);
+    }
+    __syncthreads();
+  }
+  if (final_pass) {
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) {
+      const uint64_t gi = off + i;
+      if (gi < n) out[gi] = smc[i].x;
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
+  }
+}
+
+static uint32_t flood_groups(uint32_t S) {
+  const uint32_t half = S / 2;
+  return half >= kFloodPairsPerWg ? half / kFloodPairsPerWg : 1;
+}
+
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
-  return K * (uint64_t)p.L * p.N * sizeof(uint64_t) + K * (uint64_t)p.batch * sizeof(double2);
+  // dbuf [K][L][N] | fbuf [K][S] | flooding partial sums [K][G]
+  return K * (uint64_t)p.L * p.N * sizeof(uint64_t) + K * (uint64_t)p.batch * sizeof(double2) +
+         K * (uint64_t)flood_groups(p.batch) * sizeof(double2) + 64;
 }
 
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
@@ -1765,19 +1887,39 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
                        fbuf);
   SHELFI_HIP(hipGetLastError());
-  if (dn && dn->enabled) {
-    Key8 k8;
-    for (int i = 0; i < 8; ++i) k8.k[i] = dn->key[i];
-    hipLaunchKernelGGL(decode_flood_kernel, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, logS, p.logN,
-                       ldexp(1.0, (int)dn->p_bits), (double)dn->p_bits, dn->m_factor, k8, dn->g0,
-                       dn->flags);
-    SHELFI_HIP(hipGetLastError());
-  }
   const uint32_t fblkLog = fft_block_log(logS);
   const int flogR = (int)(logS - fblkLog);
   const size_t lds = sizeof(double2) << fblkLog;
-  hipLaunchKernelGGL(fft_fwd_blocks, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
-                     fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0);
+  FloodArgs fa{};
+  bool fused_flood = false;
+  if (dn && dn->enabled) {
+    for (int i = 0; i < 8; ++i) fa.key.k[i] = dn->key[i];
+    fa.two_p = ldexp(1.0, (int)dn->p_bits);
+    fa.p_bits = (double)dn->p_bits;
+    fa.m_factor = dn->m_factor;
+    fa.g0 = dn->g0;
+    fa.flags = dn->flags;
+    fa.logN = p.logN;
+    const char* env = getenv("SHELFI_FLOOD_OLD");  // A/B probe switch (read per launch)
+    fused_flood = p.batch >= 64 && !(env && *env == '1');
+    if (fused_flood) {
+      fa.G = flood_groups(p.batch);
+      double2* part = fbuf + K * (uint64_t)p.batch;
+      fa.part = part;
+      hipLaunchKernelGGL(decode_stats_kernel, dim3((uint32_t)(K * fa.G)), dim3(256), 0, s, fbuf, logS, fa.G,
+                         part);
+    } else {
+      hipLaunchKernelGGL(decode_flood_kernel, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, logS, p.logN,
+                         fa.two_p, fa.p_bits, fa.m_factor, fa.key, fa.g0, fa.flags);
+    }
+    SHELFI_HIP(hipGetLastError());
+  }
+  if (fused_flood)
+    hipLaunchKernelGGL(fft_fwd_blocks<true>, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
+                       fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
+  else
+    hipLaunchKernelGGL(fft_fwd_blocks<false>, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
+                       fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
   SHELFI_HIP(hipGetLastError());
   if (flogR > 0) {
     const uint64_t nb = K * ((p.batch >> flogR) / 256);

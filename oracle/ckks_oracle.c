@@ -900,34 +900,29 @@ void or_sample_keygen(uint64_t seed, uint32_t N, uint32_t L, const uint64_t* q, 
   free(w);
 }
 
-/* Decode-flooding normals of ciphertext g (product spec): pair index i in [0, S/2]
- * draws ChaCha20 block (counter i, nonce (3 << 56) | g); words w0..w3 give two
+/* Decode-flooding normals of ciphertext g (product spec): the slot at FFT-input
+ * position P (slot i sits at P = bitrev(i), the order decrypt's CRT writes them) draws
+ * ChaCha20 block (counter P >> 1, nonce (3 << 56) | g); its words w0..w3 give two
  * Box-Muller pairs (u1 = ((w >> 11) + 1) 2^-53, u2 = (w' >> 11) 2^-53,
- * r = sqrt(-2 ln u1), (r cos 2 pi u2, r sin 2 pi u2)): slot i takes the first pair,
- * slot S - i (0 < i < S/2) the second.  z[2i], z[2i+1] = (re, im) of slot i. */
+ * r = sqrt(-2 ln u1), (r cos 2 pi u2, r sin 2 pi u2)): even P takes the first pair,
+ * odd P the second.  z[2i], z[2i+1] = (re, im) normals of slot i. */
 void or_flood_normals(uint64_t seed, uint64_t g, uint32_t S, double* z) {
   uint32_t key[8], blk[16];
   or_seed_to_key(seed, key);
-  uint32_t half = S / 2;
-  for (uint32_t i = 0; i <= half; ++i) {
-    or_chacha20_block(key, i, (3ull << 56) | g, blk);
-    double zz[4];
-    for (int pr = 0; pr < 2; ++pr) {
+  int logS = 0;
+  while ((1u << logS) < S) ++logS;
+  for (uint32_t P = 0; P < S; P += 2) {
+    or_chacha20_block(key, P >> 1, (3ull << 56) | g, blk);
+    for (int pr = 0; pr < 2 && P + pr < S; ++pr) {
       uint64_t a = (uint64_t)blk[4 * pr] | ((uint64_t)blk[4 * pr + 1] << 32);
       uint64_t b = (uint64_t)blk[4 * pr + 2] | ((uint64_t)blk[4 * pr + 3] << 32);
       double u1 = (double)((a >> 11) + 1) * 0x1.0p-53;
       double u2 = (double)(b >> 11) * 0x1.0p-53;
       double r = sqrt(-2.0 * log(u1));
-      zz[2 * pr] = r * cos(2.0 * M_PI * u2);
-      zz[2 * pr + 1] = r * sin(2.0 * M_PI * u2);
+      uint32_t i = bitrev(P + pr, logS);
+      z[2 * i] = r * cos(2.0 * M_PI * u2);
+      z[2 * i + 1] = r * sin(2.0 * M_PI * u2);
     }
-    z[2 * i] = zz[0];
-    z[2 * i + 1] = zz[1];
-    if (i > 0 && i < half) {
-      z[2 * (S - i)] = zz[2];
-      z[2 * (S - i) + 1] = zz[3];
-    }
-    if (S == 1) break;
   }
 }
 
