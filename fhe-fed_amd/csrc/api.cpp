@@ -288,21 +288,26 @@ static void build_tables(shelfi_ctx* ctx) {
   ctx->dt.ipsi_rev = upload(ipr.data(), ipr.size());
   ctx->dt.ipsi_rev_sh = upload(iprs.data(), iprs.size());
   {
-    const uint32_t BL = ntt_block_log(p.logN), sstart = p.logN - BL;
-    std::vector<ulonglong2> fb((size_t)L * N), ib((size_t)L * N);
-    for (uint32_t t = 0; t < L; ++t)
-      for (uint32_t b = 0; b < (1u << sstart); ++b) {
-        const size_t base = (size_t)t * N + ((size_t)b << BL);
-        fb[base] = ib[base] = make_ulonglong2(0, 0);
-        for (uint32_t l = 0; l < BL; ++l)
-          for (uint32_t i = 0; i < (1u << l); ++i) {
-            const size_t src = (size_t)t * N + (1ull << (sstart + l)) + ((size_t)b << l) + i;
-            fb[base + (1u << l) + i] = make_ulonglong2(pr[src], prs[src]);
-            ib[base + (1u << l) + i] = make_ulonglong2(ipr[src], iprs[src]);
-          }
-      }
-    ctx->dt.tw_fwd_blk = upload(fb.data(), fb.size());
-    ctx->dt.tw_inv_blk = upload(ib.data(), ib.size());
+    // per-block twiddle slices: entry 2^l + i of block b = psi table index
+    // 2^(sstart + l) + b 2^l + i (local stage l of a 2^BL-element block)
+    auto slices = [&](uint32_t BL, const std::vector<uint64_t>& w, const std::vector<uint64_t>& ws) {
+      const uint32_t sstart = p.logN - BL;
+      std::vector<ulonglong2> out((size_t)L * N);
+      for (uint32_t t = 0; t < L; ++t)
+        for (uint32_t b = 0; b < (1u << sstart); ++b) {
+          const size_t base = (size_t)t * N + ((size_t)b << BL);
+          out[base] = make_ulonglong2(0, 0);
+          for (uint32_t l = 0; l < BL; ++l)
+            for (uint32_t i = 0; i < (1u << l); ++i) {
+              const size_t src = (size_t)t * N + (1ull << (sstart + l)) + ((size_t)b << l) + i;
+              out[base + (1u << l) + i] = make_ulonglong2(w[src], ws[src]);
+            }
+        }
+      return out;
+    };
+    const uint32_t BL = ntt_block_log(p.logN);
+    ctx->dt.tw_fwd_blk = upload(slices(BL, pr, prs).data(), (size_t)L * N);
+    ctx->dt.tw_inv_blk = upload(slices(BL, ipr, iprs).data(), (size_t)L * N);
   }
   const uint32_t S = p.batch;
   std::vector<double> ir(S), ii(S), fr(S), fi(S);

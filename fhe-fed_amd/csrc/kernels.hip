@@ -660,6 +660,19 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
   }
 }
 
+// Padded LDS blocks of the compile-time passes: 4 spare u64 after every 32, so that the
+// set patterns of the chunk plans (element distance 1, 4 or 8 inside a run of 32, or a
+// multiple of 32) fall on distinct banks for ds_read_b64 / ds_write_b64 (unpadded, the
+// distance-4 sets were 8-way conflicts: 9.3 extra LDS cycles per instruction measured).
+// A set's elements are j0 + m D with D = 2^dLog, j0 mod D < D and the group aligned to
+// D M, so element m sits at lpad(j0) + lofs<D>(m): the run crossings depend on m only.
+__device__ __forceinline__ uint32_t lpad(uint32_t i) { return i + ((i >> 5) << 2); }
+template <int D>
+__device__ constexpr uint32_t lofs(int m) {
+  return (uint32_t)(m * D + (((m * D) >> 5) << 2));
+}
+constexpr uint32_t lpad_size(int BL) { return (1u << BL) + (1u << (BL - 3)); }
+
 // ---- compile-time block passes over per-block twiddle tables ---------------
 // For blocks of 2^BL elements (BL = ntt_block_log), block b owns the twiddle slice
 // tb = tw_*_blk[t][b << BL]: local stage l (the l-th of the block's stages, in the
@@ -708,11 +721,12 @@ __device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, 
     const uint32_t s = threadIdx.x + 256u * r;
     const uint32_t g = (H0 == BL - 1) ? 0u : s >> dLog;  // first chunk: one group
     const uint32_t j0 = (g << (H0 + 1)) + (s & ((1u << dLog) - 1));
+    const uint32_t pj0 = lpad(j0);
     uint64_t x[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << dLog));
+    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << dLog), pj0 + lofs<(1 << dLog)>(m));
     fwd_set_ct<BL, H0, KC>(x, g, tb, q, n8q);
-    st(r, j0, x);
+    st(r, j0, pj0, x);
   }
 }
 // Inverse (GS) chunk of KC stages starting at local half-size 2^T0: set s -> g = s >> T0,
@@ -728,9 +742,10 @@ __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, 
     const uint32_t s = threadIdx.x + 256u * r;
     const uint32_t g = s >> T0;
     const uint32_t j0 = (g << (T0 + KC)) + (s & ((1u << T0) - 1));
+    const uint32_t pj0 = lpad(j0);
     uint64_t x[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << T0));
+    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << T0), pj0 + lofs<(1 << T0)>(m));
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       const int hm = 1 << i;
@@ -742,7 +757,7 @@ __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, 
         for (int mm = 0; mm < hm; ++mm) gs_bfly_s(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n4q);
       }
     }
-    st(r, j0, x);
+    st(r, j0, pj0, x);
   }
 }
 
@@ -758,7 +773,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
   constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
-  __shared__ __attribute__((aligned(16))) uint64_t sm[1 << BL];
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
   const uint32_t sstart = logN - BL;
   const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
   const uint32_t rest = blockIdx.x >> sstart;
@@ -768,7 +783,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
   const ulonglong2* tb0 = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
-  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
   uint64_t V[NSL][ML];  // NTT(v) at this thread's last-chunk positions
 #pragma unroll 1
   for (int poly = 0; poly < 3; ++poly) {
@@ -782,28 +797,29 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
 #pragma unroll
       for (int m = 0; m < M1; ++m) x[m] = src[threadIdx.x + 256u * r + (m << D1)];
       fwd_set_ct<BL, BL - 1, K1>(x, 0u, tb, q, n8q);
+      const uint32_t p0 = lpad(threadIdx.x + 256u * r);
 #pragma unroll
-      for (int m = 0; m < M1; ++m) sm[threadIdx.x + 256u * r + (m << D1)] = x[m];
+      for (int m = 0; m < M1; ++m) sm[p0 + lofs<(1 << D1)>(m)] = x[m];
     }
     __syncthreads();
-    fwd_chunk_ct<BL, BL - 1 - K1, K2>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
+    fwd_chunk_ct<BL, BL - 1 - K1, K2>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << (BL - K1 - K2))] = x[m];
+      for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2))>(m)] = x[m];
     });
     __syncthreads();
-    fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, auto& x) {
+    fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
-      for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (BL - K1 - K2 - K3))] = x[m];
+      for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2 - K3))>(m)] = x[m];
     });
     __syncthreads();
     // last chunk (contiguous sets of ML, written inline: V captured by a lambda would
     // live in scratch)
 #pragma unroll
     for (int r = 0; r < NSL; ++r) {
-      const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4;
+      const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4, pj0 = lpad(j0);
       uint64_t x[ML];
 #pragma unroll
-      for (int m = 0; m < ML; ++m) x[m] = sm[j0 + m];
+      for (int m = 0; m < ML; ++m) x[m] = sm[pj0 + m];
       fwd_set_ct<BL, K4 - 1, K4>(x, g, tb, q, n8q);
       if (poly == 0) {  // NTT(v), lazy (< 12q): only ever a Shoup multiplicand
 #pragma unroll
@@ -841,7 +857,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
                                                              const uint64_t* __restrict__ sk,
                                                              const uint64_t* __restrict__ sksh) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
-  __shared__ __attribute__((aligned(16))) uint64_t sm[1 << BL];
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
   const uint32_t sstart = logN - BL;
   const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
   const uint32_t poly = blockIdx.x >> sstart;  // k * L + t
@@ -854,27 +870,29 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint64_t* __restrict__ c1 = c0 + LN;
   const uint64_t* __restrict__ s = sk + off;
   const uint64_t* __restrict__ ss = sksh + off;
-  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
   // first chunk: contiguous sets of 2^K1 (T0 = 0)
   inv_chunk_ct<BL, 0, K1>(tb, q, n4q,
-                          [&](uint32_t j) { return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q); },
-                          [&](int, uint32_t j0, auto& x) {
+                          [&](uint32_t j, uint32_t) {
+                            return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q);
+                          },
+                          [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
-                            for (int m = 0; m < (1 << K1); ++m) sm[j0 + m] = x[m];
+                            for (int m = 0; m < (1 << K1); ++m) sm[pj0 + lofs<1>(m)] = x[m];
                           });
   __syncthreads();
-  inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+  inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K2); ++m) sm[j0 + (m << K1)] = x[m];
+    for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << K1)>(m)] = x[m];
   });
   __syncthreads();
-  inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+  inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
-    for (int m = 0; m < (1 << K3); ++m) sm[j0 + (m << (K1 + K2))] = x[m];
+    for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (K1 + K2))>(m)] = x[m];
   });
   __syncthreads();
   uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
-  inv_chunk_ct<BL, BL - K4, K4>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, auto& x) {
+  inv_chunk_ct<BL, BL - K4, K4>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, uint32_t, auto& x) {
 #pragma unroll
     for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = x[m];
   });
@@ -1315,6 +1333,130 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
   }
 }
 
+// Encode + sampling + the columns pass in one kernel (enc_prep_kernel followed by the three
+// ntt_fwd_cols_enc launches, without the 10-byte-per-coefficient record in between):
+// thread = column c of ciphertext k, coefficients j = c + BLK r (r < R = 2^LOGR).  With
+// E8 = N/8 = BLK 2^(LOGR-3) (LOGR >= 3), ChaCha20 block bb feeds coefficients bb + E8 w
+// (w < 8), so the blocks bb = c + BLK u (u < 2^(LOGR-3)) of each stream hold exactly this
+// column: row r = u + 2^(LOGR-3) w.  Same stream words, same samples, same rounding as
+// enc_prep_kernel, then for every tower the columns stages of v, m + e0 and e1 and the
+// lazy stores into pbuf that ntt_fwd_blocks_enc_ct reads.
+template <int LOGR>
+__global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
+                                                      uint32_t logN, uint32_t logS, uint32_t L,
+                                                      double delta, const uint64_t* __restrict__ cdt,
+                                                      int T, Key8 key, uint64_t g0,
+                                                      const TowerConst* __restrict__ tcs,
+                                                      const uint64_t* __restrict__ tw,
+                                                      const uint64_t* __restrict__ twp,
+                                                      uint64_t* __restrict__ out,
+                                                      uint32_t* __restrict__ flag) {
+  constexpr int R = 1 << LOGR, NB = 1 << (LOGR - 3);
+  static_assert(LOGR >= 3, "a column must own whole ChaCha20 blocks");
+  __shared__ uint64_t tab[64];
+  if (threadIdx.x < 64) tab[threadIdx.x] = (int)threadIdx.x < T ? cdt[threadIdx.x] : ~0ull;
+  __syncthreads();
+  const uint32_t N = 1u << logN, BLK = N >> LOGR, E8 = N >> 3, half = N >> 1;
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = gid >> (logN - LOGR);
+  if (k >= K) return;
+  const uint32_t c = (uint32_t)(gid & (BLK - 1));
+  const uint64_t nonce = (1ull << 56) | (g0 + k);
+  const uint32_t S = 1u << logS, gapLog = logN - 1 - logS;
+  const double invS = 1.0 / (double)S;  // a power of two: x * (1/S) == x / S exactly
+  const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
+  const uint64_t LN = (uint64_t)L << logN;
+  // columns stages of one polynomial of tower t (values x[r] < q) and its lazy store
+  auto cols = [&](uint64_t (&x)[R], uint32_t t, const TowerConst& cst, int poly) {
+    const uint64_t q = cst.q;
+    const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
+    const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
+#pragma unroll
+    for (int s = 0; s < LOGR; ++s) {
+      const int m = 1 << s, tr = R >> (s + 1);
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        const uint64_t W = w[m + i], Wp = wp[m + i];
+#pragma unroll
+        for (int jj = 0; jj < tr; ++jj) {
+          const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+          if (fwd_red_at(s))
+            ct_bfly_s<true>(x[r0], x[r1], W, Wp, q, cst.n8q);
+          else
+            ct_bfly_s<false>(x[r0], x[r1], W, Wp, q, cst.n8q);
+        }
+      }
+    }
+    uint64_t* __restrict__ o = out + (k * 3 + poly) * LN + ((uint64_t)t << logN) + c;
+#pragma unroll
+    for (int r = 0; r < R; ++r) o[(uint64_t)r * BLK] = fwd_bound(LOGR) > 8 ? csub_neg(x[r], cst.n8q) : x[r];
+  };
+  // phase 1: v (stream blocks [0, E8)) and e1 ([2 E8, 3 E8)), packed (e1 << 8) | (uint8) v
+  {
+    int32_t sv[R];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      uint64_t w[8];
+      chacha20_block(key, c + BLK * u, nonce, w);
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) sv[u + NB * ww] = (int32_t)ternary_sample(w[ww]) & 0xFF;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      uint64_t w[8];
+      chacha20_block(key, 2 * E8 + c + BLK * u, nonce, w);
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) sv[u + NB * ww] |= (int32_t)gauss_sample_lds(w[ww], tab) << 8;
+    }
+#pragma unroll 1
+    for (uint32_t t = 0; t < L; ++t) {
+      const TowerConst cst = tcs[t];
+#pragma unroll 1
+      for (int poly = 0; poly < 3; poly += 2) {
+        uint64_t x[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = small_mod(poly == 0 ? (int32_t)(int8_t)(sv[r] & 0xFF) : (sv[r] >> 8), cst.q);
+        cols(x, t, cst, poly);
+      }
+    }
+  }
+  // phase 2: m + e0 (blocks [E8, 2 E8)); rows r and r + R/2 read one slot
+  int64_t me[R];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    uint64_t w[8];
+    chacha20_block(key, E8 + c + BLK * u, nonce, w);
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const int r = u + NB * ww;
+      const uint32_t jj = c + BLK * r;  // < N/2
+      int64_t mre = 0, mim = 0;
+      if ((jj & ((1u << gapLog) - 1)) == 0) {
+        const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
+        const double vr = __dmul_rn(__dmul_rn(cv.x, invS), delta);
+        const double vi = __dmul_rn(__dmul_rn(cv.y, invS), delta);
+        if (!(fabs(vr) <= lim) || !(fabs(vi) <= lim)) atomicOr(flag, 1u);  // also NaN / inf
+        mre = round_half_away(vr);
+        mim = round_half_away(vi);
+      }
+      me[r] = mre + gauss_sample_lds(w[ww], tab);
+      me[r + R / 2] = mim + gauss_sample_lds(w[ww + 4], tab);
+    }
+  }
+#pragma unroll 1
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst cst = tcs[t];
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      x[r] = mod_signed_dev(me[r], cst);
+      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+    }
+    cols(x, t, cst, 1);
+  }
+  (void)half;
+}
+
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
   // FFT buffer | pbuf [K][3][L][N] | me0 [K][N] int64 | ve [K][N] int16
   return K * (uint64_t)p.batch * sizeof(double2) + K * 3ull * p.L * p.N * sizeof(uint64_t) +
@@ -1343,20 +1485,34 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        blkLog, 1, dt.fft_inv);
   }
   SHELFI_HIP(hipGetLastError());
-  // 2. encode (scale/round) + sampling -> compact record
   Key8 k8;
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
-  int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
-  int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
-  const uint64_t threads = K * (p.N / 8);
-  hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, fbuf,
-                     K, p.logN, logS, p.delta, dt.cdt, dt.cdt_len, k8, g0, me0, ve, flag);
-  SHELFI_HIP(hipGetLastError());
-  // 3. NTT of v, m + e0, e1 per tower (columns pass expands the record), then the
-  // blocks pass fused with the public-key combine writes the ciphertexts
   const uint32_t nblkLog = ntt_block_log(p.logN);
   const int nlogR = (int)(p.logN - nblkLog);
-  if (nlogR > 0) {
+  const char* env = getenv("SHELFI_ENC_FUSED_COLS");  // A/B probe switch (read per launch)
+  const bool fused = (nlogR == 3 || nlogR == 4) && !(env && *env == '0');
+  int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
+  int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
+  if (fused) {
+    // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
+    const uint64_t nb = (K << (p.logN - nlogR)) / 256;
+    if (nlogR == 3)
+      hipLaunchKernelGGL((enc_cols_fused<3>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
+                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag);
+    else
+      hipLaunchKernelGGL((enc_cols_fused<4>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
+                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag);
+    SHELFI_HIP(hipGetLastError());
+  } else {
+    // 2. encode (scale/round) + sampling -> compact record
+    const uint64_t threads = K * (p.N / 8);
+    hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, fbuf,
+                       K, p.logN, logS, p.delta, dt.cdt, dt.cdt_len, k8, g0, me0, ve, flag);
+    SHELFI_HIP(hipGetLastError());
+  }
+  // 3. NTT of v, m + e0, e1 per tower (columns pass expands the record), then the
+  // blocks pass fused with the public-key combine writes the ciphertexts
+  if (nlogR > 0 && !fused) {
     const uint64_t nb = K * ((p.N >> nlogR) / 256);
 #define COLS_ENC(LR)                                                                          \
   hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 0>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
@@ -1481,6 +1637,7 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
 // CRT-reconstructed exactly as crt_decode_kernel does (same operation order) and stored
 // at bitrev(slot).  Needs L R 512 B of LDS <= kCrtFuseLds and gap = N / 2S <= 64.
 constexpr size_t kCrtFuseLds = 48 << 10;
+constexpr int kCrtRowStride = 68;  // u64 per LDS row of ntt_inv_cols_crt (64 columns + 4)
 template <int LOGR>
 __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restrict__ dbuf, uint32_t L,
                                                         uint32_t logN, uint32_t logS,
@@ -1489,9 +1646,11 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
                                                         const TowerConst* __restrict__ tcs, uint64_t Qlo,
                                                         uint64_t Qhi, double inv_scale,
                                                         double2* __restrict__ fbuf) {
-  constexpr int R = 1 << LOGR, CW = 64;
-  extern __shared__ uint64_t ys_flat[];  // [L][R][CW]
-  uint64_t(*ys)[R][CW] = reinterpret_cast<uint64_t(*)[R][CW]>(ys_flat);
+  // rows padded to 68 u64: the CRT loop reads ys[t][r][u] with r fastest (8 consecutive
+  // lanes = 8 rows), at 64 those were 8-way bank conflicts; 68 puts rows 8 banks apart
+  constexpr int R = 1 << LOGR, CW = 64, CWP = kCrtRowStride;
+  extern __shared__ uint64_t ys_flat[];  // [L][R][CWP]
+  uint64_t(*ys)[R][CWP] = reinterpret_cast<uint64_t(*)[R][CWP]>(ys_flat);
   const uint32_t N = 1u << logN, BLK = N >> LOGR, S = 1u << logS;
   const uint32_t cpb = BLK / CW;
   const uint64_t k = blockIdx.x / cpb;
@@ -1855,7 +2014,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   // last pass fused with the CRT decode where its shape allows
   const uint32_t blkLog = ntt_block_log(p.logN);
   const int logR = (int)(p.logN - blkLog);
-  const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
+  const size_t fuse_lds = (size_t)p.L * kCrtRowStride * sizeof(uint64_t) << (logR > 0 ? logR : 0);
   const bool fuse = logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
                     ((p.N >> logR) % 64) == 0;
   {
