@@ -72,9 +72,10 @@ def parse():
                          "(shelfi_dev_reduce_scatter, one collective after the local wavg)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
-    ap.add_argument("--place-output", type=int, default=8,
+    ap.add_argument("--place-output", type=int, default=0,
                     help="arena layout, no collective: time this many candidate output buffers before "
-                         "the timed region and keep the fastest placement (0 = one plain buffer)")
+                         "the timed region and keep the fastest placement (default 0 = one plain "
+                         "torch.empty buffer, the headline since round 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
@@ -87,6 +88,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
                     help="PMC-derived HBM bytes per wavg launch (from tools/pmc_traffic.py)")
+    ap.add_argument("--encdec-traffic-json", default=os.path.join(ROOT, "profiles", "encdec_traffic.json"),
+                    help="PMC-derived HBM bytes per ciphertext of the encrypt / decrypt chains "
+                         "(tools/encdec_traffic.py over tools/encdec_prof.py, cfg3 parameters)")
     return ap.parse_args()
 
 
@@ -569,6 +573,18 @@ def main():
         "encrypt_hbm_frac": frac(enc_bytes, enc_ms),
         "decrypt_hbm_frac": frac(dec_bytes, dec_ms_per_ct),
     }
+    try:
+        with open(args.encdec_traffic_json) as f:
+            et = json.load(f)
+        if args.workload in ("cfg3", "cfg2", "cfg5"):  # 2^15 / L4: the parameters it was measured at
+            for name in ("encrypt", "decrypt"):
+                res[name + "_traffic"] = {
+                    "hbm_bytes_per_ct": round(et[name]["hbm_bytes_per_ct"]),
+                    "algorithmic_bytes_per_ct": et["algorithmic_bytes_per_ct"],
+                    "over_algorithmic": round(et[name]["traffic_over_algorithmic"], 3),
+                    "source": os.path.relpath(args.encdec_traffic_json, ROOT)}
+    except (OSError, ValueError, KeyError):
+        pass
     if check:
         res["check"] = check
     if alt:
