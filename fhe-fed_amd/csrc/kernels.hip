@@ -1753,18 +1753,24 @@ __device__ __forceinline__ double block_sum_1024(double v, double* red) {
   return s;
 }
 
-// Box-Muller pair from two 64-bit words: u1 in (0, 1] (53 bits), u2 in [0, 1).  The
-// transcendental functions run in binary32 (one instruction each): the normals scale
-// noise ~1e-13 of the decoded values, so their 2^-24 relative error moves an output by
-// < 1e-20 (the oracle evaluates them in binary64).
-__device__ __forceinline__ void box_muller(uint64_t a, uint64_t b, double& z0, double& z1) {
-  const float u1 = (float)((double)((a >> 11) + 1) * 0x1.0p-53);
-  const float u2 = (float)(b >> 40) * 0x1.0p-24f;  // revolutions
+// Box-Muller pair from two 32-bit stream words: u1 = (a + 1) 2^-32 in (0, 1], u2 = b 2^-32
+// in [0, 1) (revolutions; the top 24 bits are used).  The transcendental functions run
+// in binary32 (one instruction each): the normals scale noise ~1e-13 of the decoded
+// values, so their 2^-24 relative error moves an output by < 1e-20 (the oracle
+// evaluates them in binary64).
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& z0, double& z1) {
+  const float u1 = (float)fma((double)a, 0x1.0p-32, 0x1.0p-32);
+  const float u2 = (float)(b >> 8) * 0x1.0p-24f;
   const float r = __fsqrt_rn(-2.0f * __logf(u1));
   float sn, cs;
   __sincosf(6.2831853071795864f * u2, &sn, &cs);
   z0 = (double)(r * cs);
   z1 = (double)(r * sn);
+}
+// (re, im) normals of FFT-input position P: ChaCha20 block P >> 3 (nonce (3 << 56) | g),
+// stream words 2 (P mod 8) and 2 (P mod 8) + 1 (one u64 of chacha20_block's output).
+__device__ __forceinline__ void flood_pair(uint64_t w, double& z0, double& z1) {
+  box_muller((uint32_t)w, (uint32_t)(w >> 32), z0, z1);
 }
 
 __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict__ fbuf, uint32_t logS,
@@ -1828,9 +1834,8 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
   // the normals of the slot at FFT-input position P: block P >> 1, pair P & 1
   auto noise = [&](uint32_t P, double& za, double& zb) {
     uint64_t w[8];
-    chacha20_block(key, P >> 1, nonce, w);
-    if (P & 1) box_muller(w[2], w[3], za, zb);
-    else box_muller(w[0], w[1], za, zb);
+    chacha20_block(key, P >> 3, nonce, w);
+    flood_pair(w[P & 7], za, zb);
   };
   __syncthreads();  // every thread has read its pairs before any is overwritten
   for (uint32_t i = threadIdx.x; i <= half; i += blockDim.x) {
@@ -1859,8 +1864,8 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
 //     components u (decode_flood_kernel's, over pairs (i, S - i)) and their squares;
 //  2. fft_fwd_blocks adds the noise while it loads its block (FloodArgs): sigma from
 //     the G partial sums (one-pass variance (sum u^2 - (sum u)^2 / S) / (S - 1)), the
-//     normals of position P from ChaCha20 block P >> 1 (a thread loads positions 2m,
-//     2m + 1: one block, two Box-Muller pairs).
+//     normals of position P from ChaCha20 block P >> 3 (a thread loads positions 8m ..
+//     8m + 7: one block, eight Box-Muller pairs).
 // The symmetrization (v + conj)/2 is left out: conj contributes only the imaginary part
 // of each decoded slot (m(1/zeta) = conj m(zeta) for real coefficients) and decrypt
 // keeps real parts, so the output is the same up to rounding (oracle tolerance 1e-14).
@@ -1955,15 +1960,18 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
     const double nsd = stddev_p / fa.two_p;
     const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
     const double4* src = reinterpret_cast<const double4*>(buf + off);
-    for (uint32_t m = threadIdx.x; m < blk / 2; m += 256) {  // positions 2m, 2m + 1
+    for (uint32_t m = threadIdx.x; m < blk / 8; m += 256) {  // positions 8m .. 8m + 7
       uint64_t w[8];
-      chacha20_block(fa.key, (((uint64_t)b << blkLog) >> 1) + m, nonce, w);
-      double z0, z1, z2, z3;
-      box_muller(w[0], w[1], z0, z1);
-      box_muller(w[2], w[3], z2, z3);
-      const double4 v = src[m];
-      smc[2 * m] = make_double2(v.x + nsd * z0, v.y + nsd * z1);
-      smc[2 * m + 1] = make_double2(v.z + nsd * z2, v.w + nsd * z3);
+      chacha20_block(fa.key, (((uint64_t)b << blkLog) >> 3) + m, nonce, w);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        double z0, z1, z2, z3;
+        flood_pair(w[2 * h], z0, z1);
+        flood_pair(w[2 * h + 1], z2, z3);
+        const double4 v = src[4 * m + h];
+        smc[8 * m + 2 * h] = make_double2(v.x + nsd * z0, v.y + nsd * z1);
+        smc[8 * m + 2 * h + 1] = make_double2(v.z + nsd * z2, v.w + nsd * z3);
+      }
     }
   } else {
     for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];

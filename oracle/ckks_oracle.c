@@ -902,22 +902,20 @@ void or_sample_keygen(uint64_t seed, uint32_t N, uint32_t L, const uint64_t* q, 
 
 /* Decode-flooding normals of ciphertext g (product spec): the slot at FFT-input
  * position P (slot i sits at P = bitrev(i), the order decrypt's CRT writes them) draws
- * ChaCha20 block (counter P >> 1, nonce (3 << 56) | g); its words w0..w3 give two
- * Box-Muller pairs (u1 = ((w >> 11) + 1) 2^-53, u2 = (w' >> 11) 2^-53,
- * r = sqrt(-2 ln u1), (r cos 2 pi u2, r sin 2 pi u2)): even P takes the first pair,
- * odd P the second.  z[2i], z[2i+1] = (re, im) normals of slot i. */
+ * ChaCha20 block (counter P >> 3, nonce (3 << 56) | g); its 32-bit words 2 (P mod 8) and
+ * 2 (P mod 8) + 1 give one Box-Muller pair (u1 = (w + 1) 2^-32, u2 = w' 2^-32,
+ * r = sqrt(-2 ln u1), (r cos 2 pi u2, r sin 2 pi u2)).  z[2i], z[2i+1] = (re, im)
+ * normals of slot i. */
 void or_flood_normals(uint64_t seed, uint64_t g, uint32_t S, double* z) {
   uint32_t key[8], blk[16];
   or_seed_to_key(seed, key);
   int logS = 0;
   while ((1u << logS) < S) ++logS;
-  for (uint32_t P = 0; P < S; P += 2) {
-    or_chacha20_block(key, P >> 1, (3ull << 56) | g, blk);
-    for (int pr = 0; pr < 2 && P + pr < S; ++pr) {
-      uint64_t a = (uint64_t)blk[4 * pr] | ((uint64_t)blk[4 * pr + 1] << 32);
-      uint64_t b = (uint64_t)blk[4 * pr + 2] | ((uint64_t)blk[4 * pr + 3] << 32);
-      double u1 = (double)((a >> 11) + 1) * 0x1.0p-53;
-      double u2 = (double)(b >> 11) * 0x1.0p-53;
+  for (uint32_t P = 0; P < S; P += 8) {
+    or_chacha20_block(key, P >> 3, (3ull << 56) | g, blk);
+    for (uint32_t pr = 0; pr < 8 && P + pr < S; ++pr) {
+      double u1 = ((double)blk[2 * pr] + 1.0) * 0x1.0p-32;
+      double u2 = (double)blk[2 * pr + 1] * 0x1.0p-32;
       double r = sqrt(-2.0 * log(u1));
       uint32_t i = bitrev(P + pr, logS);
       z[2 * i] = r * cos(2.0 * M_PI * u2);
