@@ -42,6 +42,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fhe-fed_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_CLOCK_GHZ = 2.4  # MI355X peak engine clock
+VALU_CYCLES_PER_INST = 4.0  # one wave64 VOP3 instruction per SIMD (tools/valu_rates.hip, profiles/r02_valu_rates.txt)
 # name -> (slots, multDepth, params per learner, learners per GPU, description)
 WORKLOADS = {
     "cfg2": (16384, 3, 61_706, 16, "LeNet-5"),
@@ -91,6 +93,9 @@ def parse():
     ap.add_argument("--encdec-traffic-json", default=os.path.join(ROOT, "profiles", "encdec_traffic.json"),
                     help="PMC-derived HBM bytes per ciphertext of the encrypt / decrypt chains "
                          "(tools/encdec_traffic.py over tools/encdec_prof.py, cfg3 parameters)")
+    ap.add_argument("--encdec-valu-json", default=os.path.join(ROOT, "profiles", "encdec_valu.json"),
+                    help="SQ_INSTS_VALU wave-instructions per ciphertext of the encrypt / decrypt chains "
+                         "(tools/encdec_valu.py over tools/encdec_prof.py, cfg3 parameters)")
     return ap.parse_args()
 
 
@@ -583,6 +588,26 @@ def main():
                     "algorithmic_bytes_per_ct": et["algorithmic_bytes_per_ct"],
                     "over_algorithmic": round(et[name]["traffic_over_algorithmic"], 3),
                     "source": os.path.relpath(args.encdec_traffic_json, ROOT)}
+    except (OSError, ValueError, KeyError):
+        pass
+    # VALU roofline of the encrypt / decrypt chains (their bound): PMC
+    # wave-instructions per ciphertext over the issue peak of one wave64 VALU instruction per
+    # 4 cycles per SIMD (VOP3 integer ops incl. v_mad_u64_u32, tools/valu_rates.hip) at the
+    # 2.4 GHz peak engine clock
+    try:
+        with open(args.encdec_valu_json) as f:
+            ev = json.load(f)
+        if args.workload in ("cfg3", "cfg2", "cfg5"):
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            peak = simds * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST  # G wave-instructions / s
+            for name, ms in (("encrypt", enc_ms), ("decrypt", dec_ms_per_ct),
+                             ("decrypt_flooded", dec_flood_ms_per_ct)):
+                wi = ev[name]["wave_instr_per_ct"]
+                ach = wi / (ms * 1e-3) / 1e9
+                res[name + "_valu"] = {"bound": "valu", "wave_instr_per_ct": wi,
+                                       "achieved": round(ach, 1), "peak": round(peak, 1),
+                                       "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
+                                       "source": os.path.relpath(args.encdec_valu_json, ROOT)}
     except (OSError, ValueError, KeyError):
         pass
     if check:

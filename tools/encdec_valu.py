@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""VALU wave-instructions per ciphertext of the device encrypt / decrypt / flooded-decrypt
+chains, from one rocprofv3 --pmc pass carrying SQ_INSTS_VALU over tools/encdec_prof.py
+(median per dispatch of each kernel, divided by the ciphertexts per call).  These chains
+are bound by VALU issue, not HBM: bench.py turns the counts into a VALU
+roofline with the issue rate tools/valu_rates.hip measures (one VOP3 wave64 instruction,
+v_mad_u64_u32 included, per ~4 cycles per SIMD).
+usage: encdec_valu.py sq_counter_collection.csv --cts 714 -o profiles/encdec_valu.json"""
+import argparse
+import collections
+import csv
+import json
+import statistics
+
+CHAINS = {
+    "encrypt": ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
+                "ntt_fwd_blocks_enc"),
+    "decrypt": ("ntt_inv_blocks_dec_ct", "ntt_inv_cols_crt", "fft_fwd_blocks<false>", "fft_fwd_cols"),
+    "decrypt_flooded": ("ntt_inv_blocks_dec_ct", "ntt_inv_cols_crt", "decode_stats_kernel",
+                        "fft_fwd_blocks<true>", "fft_fwd_cols"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("sq_csv")
+    ap.add_argument("--cts", type=int, default=714)
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(a.sq_csv)):
+        if r.get("Counter_Name") != "SQ_INSTS_VALU":
+            continue
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("shelfi::", "")
+        vals[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    per = {k: statistics.median(v.values()) / a.cts for k, v in vals.items()}
+    res = {"cts_per_call": a.cts, "counter": "SQ_INSTS_VALU (wave-level), median per dispatch / cts per call"}
+    for name, ks in CHAINS.items():
+        part = {k: round(v) for k, v in per.items() if any(k.startswith(n) for n in ks)}
+        res[name] = {"kernels_wave_instr_per_ct": part, "wave_instr_per_ct": sum(part.values())}
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
