@@ -1,6 +1,7 @@
 // Pinned staging rings + parallel memcpy for the bytes API (see host_stage.h).
 #include "host_stage.h"
 
+#include <immintrin.h>
 #include <sched.h>
 #include <sys/mman.h>
 
@@ -39,8 +40,41 @@ void advise_huge(void* p, size_t n) {
   if (b > a) (void)madvise((void*)a, b - a, MADV_HUGEPAGE);  // advice only; failure is harmless
 }
 
+// Copy with non-temporal (streaming) stores: the destination of a staging copy is read
+// next by a DMA engine or by the caller much later, so the stores skip the read-for-
+// ownership of every destination line and do not evict the source from the cache.
+__attribute__((target("avx512f"))) static void copy_nt512(uint8_t* d, const uint8_t* s, size_t n) {
+  const size_t head = std::min(n, (size_t)((64 - ((uintptr_t)d & 63)) & 63));
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  const size_t body = n & ~(size_t)255;
+  for (size_t i = 0; i < body; i += 256) {
+    const __m512i a = _mm512_loadu_si512(s + i), b = _mm512_loadu_si512(s + i + 64),
+                  c = _mm512_loadu_si512(s + i + 128), e = _mm512_loadu_si512(s + i + 192);
+    _mm512_stream_si512((__m512i*)(d + i), a);
+    _mm512_stream_si512((__m512i*)(d + i + 64), b);
+    _mm512_stream_si512((__m512i*)(d + i + 128), c);
+    _mm512_stream_si512((__m512i*)(d + i + 192), e);
+  }
+  _mm_sfence();
+  std::memcpy(d + body, s + body, n - body);
+}
+
+static bool use_nt_copy() {
+  if (const char* e = std::getenv("SHELFI_NT_COPY")) return std::atoi(e) != 0;
+  return true;
+}
+
+void copy_bytes(uint8_t* d, const uint8_t* s, size_t n, bool nt) {
+  static const bool has512 = __builtin_cpu_supports("avx512f");
+  if (nt && has512 && n >= (64u << 10)) copy_nt512(d, s, n);
+  else std::memcpy(d, s, n);
+}
+
 // ------------------------------------------------------------- CopyPool ----
-CopyPool::CopyPool(int threads) : parts_(std::max(1, threads)) {
+CopyPool::CopyPool(int threads) : parts_(std::max(1, threads)), nt_(use_nt_copy()) {
   workers_.reserve(parts_ - 1);
   for (int i = 1; i < parts_; ++i) workers_.emplace_back([this, i] { run(i); });
 }
@@ -65,7 +99,7 @@ void CopyPool::share(int id) {
   for (size_t j = 0; j < njobs_ && base < b; ++j) {
     const CopyJob& J = jobs_[j];
     const size_t lo = std::max(a, base), hi = std::min(b, base + J.n);
-    if (hi > lo) std::memcpy(J.dst + (lo - base), J.src + (lo - base), hi - lo);
+    if (hi > lo) copy_bytes(J.dst + (lo - base), J.src + (lo - base), hi - lo, nt_);
     base += J.n;
   }
 }
@@ -96,7 +130,7 @@ void CopyPool::copy_many(const CopyJob* jobs, size_t njobs, int parts) {
   if (total == 0) return;
   const int active = (parts >= 1 && parts < parts_) ? parts : parts_;
   if (workers_.empty() || active == 1 || total < (512u << 10)) {
-    for (size_t j = 0; j < njobs; ++j) std::memcpy(jobs[j].dst, jobs[j].src, jobs[j].n);
+    for (size_t j = 0; j < njobs; ++j) copy_bytes(jobs[j].dst, jobs[j].src, jobs[j].n, nt_);
     return;
   }
   jobs_ = jobs;

@@ -23,6 +23,9 @@
 
 namespace shelfi {
 
+// memcpy, with non-temporal stores when `nt` and the CPU has AVX-512 (n >= 64 KiB).
+void copy_bytes(uint8_t* d, const uint8_t* s, size_t n, bool nt);
+
 // One memcpy of a scatter/gather list.
 struct CopyJob {
   uint8_t* dst;
@@ -58,6 +61,7 @@ class CopyPool {
   const CopyJob* jobs_ = nullptr;
   size_t njobs_ = 0, total_ = 0;
   int active_ = 1;  // threads sharing the current list
+  bool nt_ = true;  // streaming stores (SHELFI_NT_COPY=0: plain memcpy)
 };
 
 // A host range of a scatter/gather transfer.
