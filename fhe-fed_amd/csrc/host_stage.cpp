@@ -6,6 +6,8 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -156,6 +158,7 @@ void CopyPool::copy(void* dst, const void* src, size_t n) {
 Stager::Stager(size_t slot_bytes, int n_in, int n_out, int threads)
     : slot_bytes_(slot_bytes), in_(n_in), out_(n_out), pool_(threads),
       h2d_parts_(std::min(pool_.threads(), default_h2d_copy_threads())) {
+  if (const char* e = std::getenv("SHELFI_STAGE_TRACE")) trace_ = std::atoi(e) != 0;
   try {
     for (auto* ring : {&in_, &out_})
       for (Slot& s : *ring) {
@@ -193,7 +196,9 @@ bool Stager::drain_front(bool block) {
     if (e != hipSuccess)
       throw Error{SHELFI_ERR_DEVICE, std::string("staged copy: ") + hipGetErrorString(e)};
   }
+  const auto t0 = std::chrono::steady_clock::now();
   pool_.copy_many(s.out_jobs.data(), s.out_jobs.size());
+  if (trace_) t_drain_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   s.out_jobs.clear();
   s.pending = false;
   pending_.pop_front();
@@ -208,6 +213,15 @@ void Stager::poll() {
 // Wait until an input slot's previous DMA has read it, draining outputs meanwhile.
 void Stager::wait_in_slot(Slot& sl) {
   if (!sl.used) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Acc {
+    bool on;
+    double& t;
+    std::chrono::steady_clock::time_point t0;
+    ~Acc() {
+      if (on) t += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+  } acc{trace_, t_wait_, t0};
   for (;;) {
     const hipError_t e = hipEventQuery(sl.ev);
     if (e == hipSuccess) return;
@@ -237,7 +251,12 @@ void Stager::h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s) 
       }
     }
     if (!fill) break;
+    const auto t0 = std::chrono::steady_clock::now();
     pool_.copy_many(jobs.data(), jobs.size(), h2d_parts_);
+    if (trace_) {
+      t_fill_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      b_in_ += fill;
+    }
     SHELFI_HIP(hipMemcpyAsync(dst, sl.host, fill, hipMemcpyHostToDevice, s));
     SHELFI_HIP(hipEventRecord(sl.ev, s));
     sl.used = true;
@@ -289,6 +308,13 @@ void Stager::finish() {
   }
   for (Slot& sl : in_)
     if (sl.used) SHELFI_HIP(hipEventSynchronize(sl.ev));
+  if (trace_ && (b_in_ || t_drain_ > 0)) {
+    std::fprintf(stderr, "[stage] in %.1f MB: fill %.2f ms (%.1f GB/s), wait in-slot %.2f ms, drain %.2f ms\n",
+                 b_in_ / 1e6, t_fill_ * 1e3, t_fill_ > 0 ? b_in_ / t_fill_ / 1e9 : 0.0, t_wait_ * 1e3,
+                 t_drain_ * 1e3);
+    t_fill_ = t_wait_ = t_drain_ = 0;
+    b_in_ = 0;
+  }
 }
 
 void Stager::abort() noexcept {

@@ -116,6 +116,11 @@ class Stager {
   size_t in_next_ = 0, out_next_ = 0;
   std::deque<size_t> pending_;  // out slot indices in enqueue order
   CopyPool pool_;
+  // SHELFI_STAGE_TRACE=1: seconds the calling thread spent filling input slots, waiting
+  // for an input slot's DMA, and draining outputs (printed to stderr by finish())
+  bool trace_ = false;
+  double t_fill_ = 0, t_wait_ = 0, t_drain_ = 0;
+  size_t b_in_ = 0;
   // Threads that fill an upload slot: fewer than the pool (pageable -> pinned copies
   // compete with the DMA engine reading pinned memory; 4 of 8 measured +8-16% H2D,
   // DESIGN.md §5.3).  Drains into fresh output pages keep the whole pool (page faults).
