@@ -1079,6 +1079,8 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
   std::vector<HostPiece> pcs;
+  uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
+  SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
@@ -1103,6 +1105,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       a.L = p.L;
       a.logN = p.logN;
       a.accumulate = c0 ? 1 : 0;
+      a.bad = bad;
       launch_wavg(a, ctx->dt.tc, pp.b);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       if (c0 + gc >= C) {
@@ -1116,6 +1119,9 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   }
   sr.finish();
   pp.sync();
+  uint32_t flag = 0;
+  SHELFI_HIP(hipMemcpy(&flag, bad, 4, hipMemcpyDeviceToHost));
+  if (flag) throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed learner data)"};
 }
 
 int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,

@@ -235,7 +235,9 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
 //    [chunk][learner][512 residues]; a block then reads one contiguous C x 4 KiB
 //    region instead of C separate streams — measured 6.35 vs 5.80 TB/s at C = 16
 //    (tools/wavg_variants.py), the gap being DRAM row locality across 16 streams.
-template <bool INTERLEAVED>
+// CHECK (the bytes API, whose inputs are untrusted learner uploads): also flag any input
+// residue >= q_t in *a.bad (the carry-free limb sums assume canonical residues).
+template <bool INTERLEAVED, bool CHECK = false>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
   const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
@@ -251,11 +253,14 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
 
   uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
   uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
+  bool bad = false;
 #pragma unroll 8
   for (uint32_t k = 0; k < a.C; ++k) {
     const uint64_t* __restrict__ p = INTERLEAVED ? src + (uint64_t)k * kWavgPerBlock : a.ptrs[k] + e;
     const uint32_t w0 = a.wl[k][t][0], w1 = a.wl[k][t][1];
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    if (CHECK)
+      bad |= (((uint64_t)v.y << 32) | v.x) >= c.q || (((uint64_t)v.w << 32) | v.z) >= c.q;
     // element a: (v.x, v.y), element b: (v.z, v.w); 30-bit limbs
     const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
     const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
@@ -268,6 +273,7 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
     s10b += (uint64_t)xb1 * w0;
     s11b += (uint64_t)xb1 * w1;
   }
+  if (CHECK && bad) atomicOr(a.bad, 1u);
   uint64_t r0 = wavg_fold(s00a, s01a, s10a, s11a, c);
   uint64_t r1 = wavg_fold(s00b, s01b, s10b, s11b, c);
   if (a.accumulate) {  // learners beyond the first 16: fold into the running sum
@@ -348,6 +354,8 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   if (a.arena)
     hipLaunchKernelGGL(wavg_kernel<true>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+  else if (a.bad)
+    hipLaunchKernelGGL((wavg_kernel<false, true>), dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
   else
     hipLaunchKernelGGL(wavg_kernel<false>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());

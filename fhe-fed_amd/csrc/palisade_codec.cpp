@@ -229,7 +229,7 @@ PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t
   c.u32();
   const uint32_t M = c.u32();
   p.N = c.u32();
-  if (p.N < 2 || (p.N & (p.N - 1)) || M != 2 * p.N) bad("context ring dimension");
+  if (p.N < 2 || p.N > (1u << 17) || (p.N & (p.N - 1)) || M != 2 * p.N) bad("context ring dimension");
   c.get<uint8_t>();
   c.u32();  // BigInteger version
   // BigInteger width: the four element BigIntegers are followed by u64 L and the
@@ -251,8 +251,8 @@ PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t
   if (!B) bad("context BigInteger layout");
   p.bigint_bytes = B;
   const std::vector<uint32_t> Q = read_bigint(c, B);
-  p.elem_bigints.assign(obj.data() + c.p, 3ull * B);
   c.need(3ull * B);
+  p.elem_bigints.assign(obj.data() + c.p, 3ull * B);
   c.p += 3ull * B;
   const uint64_t L = c.u64();
   if (L < 1 || L > (uint64_t)kMaxTowers) bad("context tower count");
@@ -575,7 +575,8 @@ PalisadeArchive palisade_parse_archive(const uint8_t* b, size_t len) {
     }
   }
   if (c.p != len) bad("trailing bytes");
-  // every residue below its modulus is checked by the caller on the data it uses
+  // residues >= q are refused by the aggregation (wavg_kernel<false, true>); decrypt of a
+  // malformed archive only yields a meaningless decode
   return A;
 }
 

@@ -182,6 +182,7 @@ struct WavgArgs {
   uint64_t rows;  // K * 2 * L
   uint32_t C, L, logN, accumulate;
   uint32_t arena_learners, first_learner;          // arena width, first learner of this pass
+  uint32_t* bad;  // SEPARATE layout: device flag set when an input residue is >= q (or null)
 };
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
 void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,

@@ -87,3 +87,26 @@ def test_decrypt_floods_by_default():
     c.set_decode_noise(False)
     e1, e2 = c.decrypt(a, 4096), c.decrypt(a, 4096)
     assert np.array_equal(e1, e2)
+
+
+@pytest.mark.parametrize("C", [3, 20])  # one launch; two launches (accumulating past 16 learners)
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_bytes_api_rejects_residues_not_below_q(ck, C, where):
+    """An upload whose residue is >= its tower modulus is malformed (the carry-free limb
+    sums of the aggregation assume canonical residues): refused, in either wire format."""
+    x = np.linspace(-1, 1, 5000)
+    good = ck.encrypt(x)
+    hdr = m._lib.load().shelfi_blob_header_bytes()
+    res = np.frombuffer(good, np.uint64, offset=hdr).copy()
+    inf = ck.info()
+    if where == "first":
+        res[0] = inf["moduli"][0]  # exactly q_0
+    else:
+        res[-1] = np.uint64(2**64 - 1)
+    bad = good[:hdr] + res.tobytes()
+    blobs = [good] * (C - 1) + [bad]
+    with pytest.raises(RuntimeError, match="residue >= its tower modulus"):
+        ck.computeWeightedAverage(blobs, [1.0 / C] * C)
+    # the context stays usable
+    out = ck.decrypt(ck.computeWeightedAverage([good] * C, [1.0 / C] * C), 5000)
+    assert np.abs(out - x).max() < 1e-7
