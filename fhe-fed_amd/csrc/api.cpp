@@ -253,6 +253,11 @@ static void build_tables(shelfi_ctx* ctx) {
     c.ninv_qhat_shoup = shoup(c.ninv_qhat, q);
     c.qhat_lo = (uint64_t)qhat128;
     c.qhat_hi = (uint64_t)(qhat128 >> 64);
+    const u128 nQ = (u128)0 - Q128;  // 2^128 - Q mod 2^128
+    for (int j = 0; j < 5; ++j) {
+      c.crt30[j] = (uint32_t)((qhat128 >> (30 * j)) & ((1u << 30) - 1));
+      c.nq30[j] = (uint32_t)((nQ >> (30 * j)) & ((1u << 30) - 1));
+    }
     c.inv_q = 1.0 / (double)q;
     c.nq = (uint64_t)0 - q;
     c.n4q = (uint64_t)0 - (q << 2);

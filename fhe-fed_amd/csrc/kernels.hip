@@ -1562,6 +1562,72 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   SHELFI_HIP(hipGetLastError());
 }
 
+// One coefficient of the exact centered CRT: y(t) in [0, q_t) are b_t (Q/q_t)^-1 mod q_t
+// for the L towers; X = sum_t y_t (Q/q_t) - k Q with k = round(sum_t y_t / q_t), read as a
+// signed 128-bit integer, then (double)X * (1/scale) (PALISADE Decode: ConvertToDouble *
+// scalingFactorPre * 2^-p).  For L <= 7 the 128-bit sum runs in 30-bit limb columns
+// (y_t = a + b 2^30; every column is a sum of <= 2L products below 2^60 plus k times a
+// 30-bit limb, below 2^64 without carries: one v_mad_u64_u32 per product), then one carry
+// pass; X is exact either way, so the two paths give the same bits.
+template <class YF>
+__device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst* __restrict__ tcs,
+                                            uint64_t Qlo, uint64_t Qhi, double inv_scale) {
+  double frac = 0.0;
+  uint64_t xlo = 0, xhi = 0;
+  if (L <= 7) {
+    constexpr uint32_t M30 = (1u << 30) - 1;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+#pragma unroll 1
+    for (uint32_t t = 0; t < L; ++t) {
+      const TowerConst& c = tcs[t];
+      const uint64_t y = yf(t);
+      frac += (double)y * c.inv_q;
+      const uint32_t a = (uint32_t)y & M30, b = (uint32_t)(y >> 30);
+      s0 += (uint64_t)a * c.crt30[0];
+      s1 += (uint64_t)a * c.crt30[1] + (uint64_t)b * c.crt30[0];
+      s2 += (uint64_t)a * c.crt30[2] + (uint64_t)b * c.crt30[1];
+      s3 += (uint64_t)a * c.crt30[3] + (uint64_t)b * c.crt30[2];
+      s4 += (uint64_t)a * c.crt30[4] + (uint64_t)b * c.crt30[3];
+    }
+    const uint64_t kk = (uint64_t)(frac + 0.5);  // <= L
+    const uint32_t* nq = tcs[0].nq30;
+    s0 += kk * nq[0];
+    s1 += kk * nq[1] + (s0 >> 30);
+    s2 += kk * nq[2] + (s1 >> 30);
+    s3 += kk * nq[3] + (s2 >> 30);
+    s4 += kk * nq[4] + (s3 >> 30);
+    xlo = (s0 & M30) | ((s1 & M30) << 30) | (s2 << 60);
+    xhi = ((s2 & M30) >> 4) | ((s3 & M30) << 26) | (s4 << 56);
+  } else {
+#pragma unroll 1
+    for (uint32_t t = 0; t < L; ++t) {
+      const TowerConst& c = tcs[t];
+      const uint64_t y = yf(t);
+      frac += (double)y * c.inv_q;
+      const uint64_t plo = y * c.qhat_lo;
+      const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
+      xlo += plo;
+      xhi += phi + (xlo < plo ? 1 : 0);
+    }
+    const uint64_t kk = (uint64_t)(frac + 0.5);
+    const uint64_t slo = kk * Qlo;
+    const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
+    const uint64_t borrow = xlo < slo ? 1 : 0;
+    xlo -= slo;
+    xhi = xhi - shi - borrow;
+  }
+  // sign-magnitude -> double (the oracle's or_i128_to_double)
+  const bool neg = (int64_t)xhi < 0;
+  if (neg) {
+    xlo = ~xlo + 1;
+    xhi = ~xhi + (xlo == 0 ? 1 : 0);
+  }
+  double v = __dadd_rn(__dmul_rn((double)xhi, 18446744073709551616.0), (double)xlo);
+  if (neg) v = -v;
+  return __dmul_rn(v, inv_scale);
+}
+
+
 // -------------------------------------------------------------- decrypt ----
 // Exact centered CRT: y_t = b_t (Q/q_t)^-1 mod q_t; X = sum y_t (Q/q_t) - k Q with
 // k = round(sum y_t / q_t) (exact while |X| << Q/2), evaluated mod 2^128 and read
@@ -1597,32 +1663,12 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const uint32_t j = (part ? (N >> 1) : 0) + (i << gapLog);
-    double frac = 0.0;
-    uint64_t xlo = 0, xhi = 0;
-    for (uint32_t t = 0; t < L; ++t) {
-      const TowerConst& c = tcs[t];
-      const uint64_t y = shoup_mul(d[((uint64_t)t << logN) + j], c.qhat_inv, c.qhat_inv_shoup, c.q);
-      frac += (double)y * c.inv_q;
-      const uint64_t plo = y * c.qhat_lo;
-      const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
-      xlo += plo;
-      xhi += phi + (xlo < plo ? 1 : 0);
-    }
-    const uint64_t kk = (uint64_t)(frac + 0.5);
-    const uint64_t slo = kk * Qlo;
-    const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
-    const uint64_t borrow = xlo < slo ? 1 : 0;
-    xlo -= slo;
-    xhi = xhi - shi - borrow;
-    // sign-magnitude -> double (the oracle's or_i128_to_double)
-    const bool neg = (int64_t)xhi < 0;
-    if (neg) {
-      xlo = ~xlo + 1;
-      xhi = ~xhi + (xlo == 0 ? 1 : 0);
-    }
-    double v = __dadd_rn(__dmul_rn((double)xhi, 18446744073709551616.0), (double)xlo);
-    if (neg) v = -v;
-    res[part] = __dmul_rn(v, inv_scale);
+    res[part] = crt_value(
+        [&](uint32_t t) {
+          const TowerConst& c = tcs[t];
+          return shoup_mul(d[((uint64_t)t << logN) + j], c.qhat_inv, c.qhat_inv_shoup, c.q);
+        },
+        L, tcs, Qlo, Qhi, inv_scale);
   }
   if (!tiled) {
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
@@ -1700,32 +1746,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
       const uint32_t rr = r + part * (R / 2);
-      double frac = 0.0;
-      uint64_t xlo = 0, xhi = 0;
-#pragma unroll 1
-      for (uint32_t t = 0; t < L; ++t) {
-        const TowerConst& c = tcs[t];
-        const uint64_t y = ys[t][rr][u];
-        frac += (double)y * c.inv_q;
-        const uint64_t plo = y * c.qhat_lo;
-        const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
-        xlo += plo;
-        xhi += phi + (xlo < plo ? 1 : 0);
-      }
-      const uint64_t kk = (uint64_t)(frac + 0.5);
-      const uint64_t slo = kk * Qlo;
-      const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
-      const uint64_t borrow = xlo < slo ? 1 : 0;
-      xlo -= slo;
-      xhi = xhi - shi - borrow;
-      const bool neg = (int64_t)xhi < 0;
-      if (neg) {
-        xlo = ~xlo + 1;
-        xhi = ~xhi + (xlo == 0 ? 1 : 0);
-      }
-      double v = __dadd_rn(__dmul_rn((double)xhi, 18446744073709551616.0), (double)xlo);
-      if (neg) v = -v;
-      res[part] = __dmul_rn(v, inv_scale);
+      res[part] = crt_value([&](uint32_t t) { return ys[t][rr][u]; }, L, tcs, Qlo, Qhi, inv_scale);
     }
     const uint32_t i = (col + BLK * r) >> gapLog;
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);

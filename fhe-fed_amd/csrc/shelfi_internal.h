@@ -93,6 +93,9 @@ struct TowerConst {
   // q >= 2^40, red_ok): red_r = floor(2^(32 + E) / q) < 2^32, E = bitlength(q) - 1
   uint32_t red_r, red_sh, red_ok, pad32;
   uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
+  // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^128 and (2^128 - Q) mod 2^128
+  // (the same in every tower), limbs 0..3 of 30 bits and limb 4 of 8 bits
+  uint32_t crt30[5], nq30[5], pad30[2];
 };
 
 struct DeviceTables {
