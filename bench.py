@@ -484,15 +484,16 @@ def main():
     def time_decrypt(flood):
         ck.set_decode_noise(flood)
         dec = D.decrypt(ck, out, K_loc * batch, delta * delta)  # warm: sizes the scratch arena
+        D.decrypt(ck, out, K_loc * batch, delta * delta, out=dec)  # and the clocks
         torch.cuda.synchronize()
         dts = []
-        for _ in range(3):
+        for _ in range(5):
             t0 = time.perf_counter()
-            dec = D.decrypt(ck, out, K_loc * batch, delta * delta)
+            D.decrypt(ck, out, K_loc * batch, delta * delta, out=dec)
             torch.cuda.synchronize()
             dts.append(time.perf_counter() - t0)
         assert torch.isfinite(dec).all().item()
-        return sorted(dts)[1] * 1e3 / K_loc
+        return sorted(dts)[2] * 1e3 / K_loc
 
     dec_ms_per_ct = time_decrypt(False)
     dec_flood_ms_per_ct = time_decrypt(True)
