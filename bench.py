@@ -361,7 +361,11 @@ def main():
 
     def timed(mode):
         """warmup, then exactly `steps` steps between barrier + sync; max over ranks.
-        Per-launch wavg events on the launch stream (torch's current stream)."""
+        Two HIP events on the launch stream (torch's current stream) bracket the timed
+        steps: without a collective their span / steps is the average wavg launch over the
+        timed region (back-to-back launches, boundaries included).  Per-launch events
+        (min, spread) come from a second pass outside the timed region: recorded around
+        every launch inside it, they cost more host time than a cfg2 launch takes."""
         for _ in range(args.warmup):
             mode["step"]()
         torch.cuda.synchronize()
@@ -369,32 +373,34 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+        region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         t0 = time.perf_counter()
+        region[0].record(stream)
         for i in range(args.steps):
             if mode["comb"] is None:
-                ev[i][0].record(stream)
                 mode["kernel"]()
-                ev[i][1].record(stream)
             else:
                 mode["step"]()
+        region[1].record(stream)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        if mode["comb"] is not None:  # the local kernel alone, outside the timed region
-            for i in range(args.steps):
-                ev[i][0].record(stream)
-                mode["kernel"]()
-                ev[i][1].record(stream)
-            torch.cuda.synchronize()
+        region_avg = region[0].elapsed_time(region[1]) / args.steps if mode["comb"] is None else None
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        for i in range(args.steps):  # the local kernel alone, outside the timed region
+            ev[i][0].record(stream)
+            mode["kernel"]()
+            ev[i][1].record(stream)
+        torch.cuda.synchronize()
         if distributed:
             tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = tt.item()
-        return elapsed, sorted(a.elapsed_time(b) for a, b in ev)
+        per = sorted(a.elapsed_time(b) for a, b in ev)
+        return elapsed, (region_avg if region_avg is not None else sum(per) / len(per)), per
 
     def checked(mode):
         """End to end: this rank's owned aggregate cts (after the collective + modq in
@@ -412,8 +418,7 @@ def main():
 
     units = Cl * world * K  # client ciphertexts folded per step, whole job (any shard)
     main_mode = build(args.shard if distributed else "local")
-    elapsed, kern_ms = timed(main_mode)
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    elapsed, kern_avg_ms, kern_ms = timed(main_mode)
     ms_per_step = elapsed * 1e3 / args.steps
     value = units / (elapsed / args.steps)
     check = None if args.no_check else checked(main_mode)
@@ -460,7 +465,7 @@ def main():
     alt = None
     if distributed and not args.no_alt:
         alt_mode = build("learners" if args.shard == "cts" else "cts")
-        a_el, a_k = timed(alt_mode)
+        a_el, _, a_k = timed(alt_mode)
         alt = {"parallelism": ("ciphertext-sharded dp%d (no collective)" if alt_mode["shard"] == "cts"
                                else "learner-sharded dp%%d + RCCL reduce_scatter in %d pieces" % args.pieces)
                               % world,

@@ -38,13 +38,22 @@ def empty_ct(ckks, K: int, device=None):
     return torch.empty(ct_shape(ckks, K), dtype=torch.int64, device=device)
 
 
+def _ln(ckks):
+    """(L, N) of a context: fixed at construction, cached (info() is a library call and a
+    dict build, too slow for the per-launch path of small aggregations)."""
+    ln = getattr(ckks, "_dev_ln", None)
+    if ln is None:
+        inf = ckks.info()
+        ln = ckks._dev_ln = (inf["num_towers"], inf["ring_dim"])
+    return ln
+
+
 def _check_ct(t, ckks, K=None):
-    inf = ckks.info()
+    L, N = _ln(ckks)
     if not t.is_cuda or not t.is_contiguous() or t.element_size() != 8:
         raise ValueError("ciphertext tensors must be contiguous 64-bit CUDA tensors")
-    if t.dim() != 4 or t.shape[1] != 2 or t.shape[2] != inf["num_towers"] or t.shape[3] != inf["ring_dim"]:
-        raise ValueError("ciphertext tensor must have shape [K][2][L][N] = [K][2][%d][%d]"
-                         % (inf["num_towers"], inf["ring_dim"]))
+    if t.dim() != 4 or t.shape[1] != 2 or t.shape[2] != L or t.shape[3] != N:
+        raise ValueError("ciphertext tensor must have shape [K][2][L][N] = [K][2][%d][%d]" % (L, N))
     if K is not None and t.shape[0] != K:
         raise ValueError("ciphertext tensors hold different numbers of ciphertexts")
 

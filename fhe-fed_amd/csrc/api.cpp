@@ -83,6 +83,10 @@ struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev == dev) {  // the common case: nothing to switch (and nothing to restore)
+      prev = -1;
+      return;
+    }
     SHELFI_HIP(hipSetDevice(dev));
   }
   ~DeviceGuard() {
