@@ -184,7 +184,7 @@ def _gloo_worker(rank, world, port, mode, result_q):
         dist_.destroy_process_group()
 
 
-def _gloo_pipelined_worker(rank, world, port, pieces, result_q):
+def _gloo_pipelined_worker(rank, world, port, pieces, result_q, K=7, C_=5):
     import torch
     import torch.distributed as dist_
 
@@ -195,7 +195,7 @@ def _gloo_pipelined_worker(rank, world, port, pieces, result_q):
     os.environ["MASTER_PORT"] = str(port)
     dist_.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        N, L, K, C_ = 1024, 2, 7, 5
+        N, L = 1024, 2
         q, psi = O_.params_generate(N, L, 40, 50)
         delta = float(int(q[-1]))
         rng = np.random.default_rng(5)
@@ -232,7 +232,7 @@ def _gloo_pipelined_worker(rank, world, port, pieces, result_q):
         dist_.destroy_process_group()
 
 
-def _spawn_world2(target, *args):
+def _spawn_world(world, target, *args, **kw):
     import multiprocessing as mp
     import socket
 
@@ -241,13 +241,18 @@ def _spawn_world2(target, *args):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q_ = ctx.Queue()
-    procs = [ctx.Process(target=target, args=(r, 2, port) + args + (q_,)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q_,), kwargs=kw)
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = [q_.get(timeout=120) for _ in procs]
+    res = [q_.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     return sorted(res)
+
+
+def _spawn_world2(target, *args):
+    return _spawn_world(2, target, *args)
 
 
 @pytest.mark.parametrize("pieces", [1, 3, 4])
@@ -257,6 +262,15 @@ def test_pipelined_combine_gloo_world2(pieces):
     the ranks' shares tile [0, K)."""
     pytest.importorskip("torch")
     assert _spawn_world2(_gloo_pipelined_worker, pieces) == [(0, True), (1, True)]
+
+
+def test_pipelined_combine_gloo_world8_rehearsal():
+    """The driver's N = 8 learner-sharded step in miniature (bench.py --gpus 8's combine):
+    8 gloo ranks, 11 learners (3 ranks hold two), K = 13 in 3 pieces (every piece's
+    reduce_scatter padded; some ranks own nothing of a piece): bit-exact vs one process."""
+    pytest.importorskip("torch")
+    res = _spawn_world(8, _gloo_pipelined_worker, 3, K=13, C_=11)
+    assert res == [(r, True) for r in range(8)]
 
 
 @pytest.mark.parametrize("mode", ["reduce_scatter", "reduce", "all_reduce"])
