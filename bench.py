@@ -544,6 +544,23 @@ def main():
                "ms_per_call": round(dt_api * 1e3, 2),
                "input_GB_per_s": round(Cl * Ka * 2 * L * N * 8 / dt_api / 1e9, 2)}
         del blobs, res_blob
+        # the same in the reference's own wire format (PALISADE cereal archives, §8 f1):
+        # the learners' uploads encrypted with set_wire_format("palisade")
+        try:
+            ck.set_wire_format("palisade")
+            xa = np.random.default_rng(7).uniform(-1, 1, Ka * batch)
+            pblobs = [ck.encrypt(xa) for _ in range(Cl)]
+            ck.computeWeightedAverage(pblobs, weights)  # warm
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                res_p = ck.computeWeightedAverage(pblobs, weights)
+            dt_p = (time.perf_counter() - t0) / reps
+            api["palisade_wire"] = {"value": round(Cl * Ka / dt_p, 1), "ms_per_call": round(dt_p * 1e3, 2),
+                                    "archive_bytes_per_learner": len(pblobs[0]),
+                                    "aggregate_bytes": len(res_p)}
+            del pblobs, res_p
+        finally:
+            ck.set_wire_format("shelfi")
 
     # roofline of the dominant kernel: algorithmic bytes = (C + 1) * K * 2 * L * N * 8
     bytes_per_launch = (C_loc + 1) * K_loc * 2 * L * N * 8
