@@ -195,6 +195,36 @@ class CKKS(Scheme):
                                         sk.ctypes.data_as(_lib.u64p)))
         return pk, sk
 
+    # ------------------------------------- f4: EvalMult / ModReduce (§8 f4) --
+    def evalMultKeyGen(self) -> None:
+        """cc->EvalMultKeyGen(sk): the HYBRID relinearization key (s^2 -> s), generated on
+        the device from the loaded secret key (seeded like the keys under set_seed)."""
+        check(self._lib.shelfi_eval_mult_keygen(self._ctx), "evalMultKeyGen")
+
+    def eval_key_info(self) -> dict:
+        """HYBRID key-switching parameters: dnum digits of alpha towers, special primes."""
+        dn, al, kp = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        sp = (C.c_uint64 * 16)()
+        has = C.c_int()
+        check(self._lib.shelfi_eval_key_info(self._ctx, C.byref(dn), C.byref(al), C.byref(kp), sp,
+                                             C.byref(has)), "eval_key_info")
+        return {"dnum": dn.value, "alpha": al.value, "special_moduli": [int(sp[i]) for i in range(kp.value)],
+                "has_key": bool(has.value)}
+
+    def get_eval_key(self) -> np.ndarray:
+        """[2][dnum][L + kP][N] (b-vector, a-vector), EVALUATION."""
+        inf, ek = self.info(), self.eval_key_info()
+        out = np.zeros((2, ek["dnum"], inf["num_towers"] + len(ek["special_moduli"]), inf["ring_dim"]),
+                       np.uint64)
+        check(self._lib.shelfi_get_eval_key(self._ctx, out.ctypes.data_as(_lib.u64p)), "get_eval_key")
+        return out
+
+    def set_eval_key(self, evk: np.ndarray) -> None:
+        evk = np.ascontiguousarray(evk, dtype=np.uint64)
+        if evk.size != self._lib.shelfi_eval_key_words(self._ctx):
+            raise ValueError("evaluation key must be [2][dnum][L + kP][N]")
+        check(self._lib.shelfi_set_eval_key(self._ctx, evk.ctypes.data_as(_lib.u64p)), "set_eval_key")
+
     # ------------------------------------------------------------ hot path --
     def _take(self, ptr: "_lib.u8p", n: int) -> bytes:
         try:
@@ -268,6 +298,20 @@ def params_generate(batchSize: int = 4096, scaleFactorBits: int = 52, multDepth:
     check(lib.shelfi_params_generate(ringDim, L, scaleFactorBits, firstModBits, batchSize,
                                      C.byref(N), q, psi), "params_generate")
     return int(N.value), [int(x) for x in q], [int(x) for x in psi]
+
+
+def special_primes(ringDim: int, moduli) -> dict:
+    """Host-only: PALISADE's HYBRID key-switching parameters for a Q chain (dnum, alpha,
+    special primes and their minimal roots)."""
+    lib = _lib.load()
+    q = np.ascontiguousarray(moduli, dtype=np.uint64)
+    dn, al, kp = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    sp, sr = (C.c_uint64 * 16)(), (C.c_uint64 * 16)()
+    check(lib.shelfi_special_primes(int(ringDim), q.size, q.ctypes.data_as(_lib.u64p), C.byref(dn), C.byref(al),
+                                    C.byref(kp), sp, sr), "special_primes")
+    k = kp.value
+    return {"dnum": dn.value, "alpha": al.value, "special_moduli": [int(sp[i]) for i in range(k)],
+            "special_roots": [int(sr[i]) for i in range(k)]}
 
 
 def blob_info(blob: bytes) -> dict:

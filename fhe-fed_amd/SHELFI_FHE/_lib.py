@@ -130,6 +130,20 @@ SIGNATURES = {
     "shelfi_dev_decrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_size_t,
                                      C.c_void_p, C.c_void_p]),
     "shelfi_dev_ntt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
+    # EvalMult / relinearization / ModReduce (eval.cpp, keyswitch.hip)
+    "shelfi_special_primes": (C.c_int, [C.c_uint32, C.c_uint32, u64p, C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), u64p, u64p]),
+    "shelfi_eval_key_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                       C.POINTER(C.c_uint32), u64p, C.POINTER(C.c_int)]),
+    "shelfi_eval_mult_keygen": (C.c_int, [C.c_void_p]),
+    "shelfi_eval_key_words": (C.c_size_t, [C.c_void_p]),
+    "shelfi_get_eval_key": (C.c_int, [C.c_void_p, u64p]),
+    "shelfi_set_eval_key": (C.c_int, [C.c_void_p, u64p]),
+    "shelfi_dev_mult": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p,
+                                  C.c_void_p]),
+    "shelfi_dev_rescale": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "shelfi_dev_decrypt_level": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_double,
+                                           C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_fft_twiddles": (C.c_int, [C.c_uint32, f64p, f64p, f64p, f64p]),
     "shelfi_gauss_cdt": (C.c_int, [C.c_double, u64p, C.c_int]),
 }

@@ -48,11 +48,12 @@ def _ln(ckks):
     return ln
 
 
-def _check_ct(t, ckks, K=None):
+def _check_ct(t, ckks, K=None, any_level=False):
     L, N = _ln(ckks)
     if not t.is_cuda or not t.is_contiguous() or t.element_size() != 8:
         raise ValueError("ciphertext tensors must be contiguous 64-bit CUDA tensors")
-    if t.dim() != 4 or t.shape[1] != 2 or t.shape[2] != L or t.shape[3] != N:
+    towers_ok = (1 <= t.shape[2] <= L) if (any_level and t.dim() == 4) else (t.dim() == 4 and t.shape[2] == L)
+    if t.dim() != 4 or t.shape[1] != 2 or not towers_ok or t.shape[3] != N:
         raise ValueError("ciphertext tensor must have shape [K][2][L][N] = [K][2][%d][%d]" % (L, N))
     if K is not None and t.shape[0] != K:
         raise ValueError("ciphertext tensors hold different numbers of ciphertexts")
@@ -182,14 +183,51 @@ def encrypt(ckks, x, out=None):
 
 
 def decrypt(ckks, ct, n: int, scale: float, out=None):
-    """decrypt + decode K ciphertexts of scaling factor `scale` into n float64 values."""
+    """decrypt + decode K ciphertexts of scaling factor `scale` into n float64 values
+    (any number of towers <= L: ciphertexts after rescale() decrypt at their level)."""
     torch = _torch()
-    _check_ct(ct, ckks)
+    _check_ct(ct, ckks, any_level=True)
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=ct.device)
-    check(_lib.load().shelfi_dev_decrypt(ckks._ctx, C.c_void_p(ct.data_ptr()), ct.shape[0],
-                                         float(scale), int(n), C.c_void_p(out.data_ptr()),
-                                         C.c_void_p(_stream_ptr(ct))), "dev_decrypt")
+    check(_lib.load().shelfi_dev_decrypt_level(ckks._ctx, C.c_void_p(ct.data_ptr()), ct.shape[0],
+                                               int(ct.shape[2]), float(scale), int(n),
+                                               C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(ct))),
+          "dev_decrypt")
+    return out
+
+
+def mult(ckks, a, b, out=None):
+    """cc->EvalMult(a, b) for K ciphertext pairs of the same level: tensor product +
+    HYBRID relinearization (needs ckks.evalMultKeyGen()).  Scale: scale_a * scale_b."""
+    torch = _torch()
+    _check_ct(a, ckks, any_level=True)
+    _check_ct(b, ckks, a.shape[0], any_level=True)
+    if a.shape != b.shape:
+        raise ValueError("EvalMult operands must have the same shape (same level)")
+    if out is None:
+        out = torch.empty_like(a)
+    if out.shape != a.shape or not out.is_contiguous():
+        raise ValueError("out must be a contiguous tensor shaped like a")
+    check(_lib.load().shelfi_dev_mult(ckks._ctx, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.shape[0],
+                                      int(a.shape[2]), C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(a))),
+          "dev_mult")
+    return out
+
+
+def rescale(ckks, ct, out=None):
+    """cc->ModReduce(ct): drop the last tower, dividing by it with rounding
+    ([K][2][l][N] -> [K][2][l-1][N]); scale / q_{l-1}."""
+    torch = _torch()
+    _check_ct(ct, ckks, any_level=True)
+    K, _, l, N = ct.shape
+    if l < 2:
+        raise ValueError("ModReduce needs at least 2 towers")
+    if out is None:
+        out = torch.empty((K, 2, l - 1, N), dtype=ct.dtype, device=ct.device)
+    if tuple(out.shape) != (K, 2, l - 1, N) or not out.is_contiguous() or out.element_size() != 8:
+        raise ValueError("out must be a contiguous [K][2][l-1][N] 64-bit tensor")
+    check(_lib.load().shelfi_dev_rescale(ckks._ctx, C.c_void_p(ct.data_ptr()), K, int(l),
+                                         C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(ct))), "dev_rescale")
     return out
 
 

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <new>
 
+#include "api_util.h"
 #include "host_stage.h"
 #include "palisade_codec.h"
 #include "palisade_io.h"
@@ -78,64 +79,11 @@ static BlobHeader parse_blob(const uint8_t* blob, size_t len, const shelfi_ctx* 
   return h;
 }
 
-// -------------------------------------------------------------- helpers ----
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev == dev) {  // the common case: nothing to switch (and nothing to restore)
-      prev = -1;
-      return;
-    }
-    SHELFI_HIP(hipSetDevice(dev));
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
 // Calls on one context are serialized (as the reference's GIL serializes its object).
 static std::mutex& ctx_mutex(const shelfi_ctx* ctx) { return ctx->mu; }
 
-template <class F>
-static int guarded(F&& f) {
-  try {
-    f();
-    return SHELFI_OK;
-  } catch (const Error& e) {
-    set_error(e.msg);
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    set_error("host out of memory");
-    return SHELFI_ERR_DEVICE;
-  } catch (const std::exception& e) {
-    set_error(e.what());
-    return SHELFI_ERR_DEVICE;
-  }
-}
 
-static void dfree(void*& p) {
-  if (p) (void)hipFree(p);
-  p = nullptr;
-}
-template <class T>
-static void dfree_t(T*& p) {
-  void* v = p;
-  dfree(v);
-  p = nullptr;
-}
-
-static void* ensure(void*& buf, size_t& cap, size_t bytes) {
-  if (bytes <= cap && buf) return buf;
-  dfree(buf);
-  cap = 0;
-  size_t want = bytes < 64 ? 64 : bytes;
-  SHELFI_HIP(hipMalloc(&buf, want));
-  cap = want;
-  return buf;
-}
-
-static void seed_to_key(uint64_t seed, uint32_t key[8]) {
+void seed_to_key(uint64_t seed, uint32_t key[8]) {
   uint64_t st = seed;
   for (int i = 0; i < 4; ++i) {
     uint64_t z = (st += 0x9E3779B97F4A7C15ull);
@@ -147,7 +95,7 @@ static void seed_to_key(uint64_t seed, uint32_t key[8]) {
   }
 }
 
-static void os_random(void* buf, size_t n) {
+void os_random(void* buf, size_t n) {
   uint8_t* p = (uint8_t*)buf;
   while (n) {
     ssize_t r = getrandom(p, n, 0);
@@ -183,20 +131,26 @@ static void validate_params(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_
     throw Error{SHELFI_ERR_ARG, "firstModBits must be in [scaleFactorBits, 60]"};
 }
 
+void free_ntt_tables(DeviceTables& dt) {
+  dfree_t(dt.tc);
+  dfree_t(dt.psi_rev);
+  dfree_t(dt.psi_rev_sh);
+  dfree_t(dt.ipsi_rev);
+  dfree_t(dt.ipsi_rev_sh);
+  dfree_t(dt.tw_fwd_blk);
+  dfree_t(dt.tw_inv_blk);
+}
+
 static void free_tables(shelfi_ctx* ctx) {
-  dfree_t(ctx->dt.tc);
-  dfree_t(ctx->dt.psi_rev);
-  dfree_t(ctx->dt.psi_rev_sh);
-  dfree_t(ctx->dt.ipsi_rev);
-  dfree_t(ctx->dt.ipsi_rev_sh);
-  dfree_t(ctx->dt.tw_fwd_blk);
-  dfree_t(ctx->dt.tw_inv_blk);
+  eval_release(ctx, false);  // level / extended-basis tables belong to these parameters
+  free_ntt_tables(ctx->dt);
   dfree_t(ctx->dt.fft_inv);
   dfree_t(ctx->dt.fft_fwd);
   dfree_t(ctx->dt.cdt);
 }
 
 static void free_keys(shelfi_ctx* ctx) {
+  eval_release(ctx, true);  // the relinearization key belongs to the secret key
   dfree_t(ctx->dk.pk);
   dfree_t(ctx->dk.pk_sh);
   dfree_t(ctx->dk.sk);
@@ -207,13 +161,6 @@ static void free_keys(shelfi_ctx* ctx) {
   ctx->sk_host.clear();
 }
 
-template <class T>
-static T* upload(const T* host, size_t count) {
-  void* d = nullptr;
-  SHELFI_HIP(hipMalloc(&d, sizeof(T) * (count ? count : 1)));
-  SHELFI_HIP(hipMemcpy(d, host, sizeof(T) * count, hipMemcpyHostToDevice));
-  return (T*)d;
-}
 
 static uint32_t bitrev_host(uint32_t x, uint32_t bits) {
   uint32_t r = 0;
@@ -221,10 +168,10 @@ static uint32_t bitrev_host(uint32_t x, uint32_t bits) {
   return r;
 }
 
-// (Re)build every device table for ctx->p.
-static void build_tables(shelfi_ctx* ctx) {
-  free_tables(ctx);
-  Params& p = ctx->p;
+// NTT / CRT tables of the towers p.q[0..L) (the context's chain, one of its levels, or an
+// extended basis Q_l u P of the key switching in eval.cpp).
+void build_ntt_tables(const Params& p, DeviceTables& dt) {
+  free_ntt_tables(dt);
   const uint32_t N = p.N, L = p.L;
   std::vector<TowerConst> tc(L);
   std::vector<uint64_t> pr((size_t)L * N), prs((size_t)L * N), ipr((size_t)L * N), iprs((size_t)L * N);
@@ -287,15 +234,15 @@ static void build_tables(shelfi_ctx* ctx) {
       iprs[(size_t)t * N + i] = shoup(ipr[(size_t)t * N + i], q);
     }
   }
-  ctx->dt.qmod128_lo = (uint64_t)Q128;
-  ctx->dt.qmod128_hi = (uint64_t)(Q128 >> 64);
-  ctx->dt.tc = upload(tc.data(), L);
-  ctx->dt.red_ok = true;
-  for (uint32_t t = 0; t < L; ++t) ctx->dt.red_ok = ctx->dt.red_ok && tc[t].red_ok;
-  ctx->dt.psi_rev = upload(pr.data(), pr.size());
-  ctx->dt.psi_rev_sh = upload(prs.data(), prs.size());
-  ctx->dt.ipsi_rev = upload(ipr.data(), ipr.size());
-  ctx->dt.ipsi_rev_sh = upload(iprs.data(), iprs.size());
+  dt.qmod128_lo = (uint64_t)Q128;
+  dt.qmod128_hi = (uint64_t)(Q128 >> 64);
+  dt.tc = upload(tc.data(), L);
+  dt.red_ok = true;
+  for (uint32_t t = 0; t < L; ++t) dt.red_ok = dt.red_ok && tc[t].red_ok;
+  dt.psi_rev = upload(pr.data(), pr.size());
+  dt.psi_rev_sh = upload(prs.data(), prs.size());
+  dt.ipsi_rev = upload(ipr.data(), ipr.size());
+  dt.ipsi_rev_sh = upload(iprs.data(), iprs.size());
   {
     // per-block twiddle slices: entry 2^l + i of block b = psi table index
     // 2^(sstart + l) + b 2^l + i (local stage l of a 2^BL-element block)
@@ -315,9 +262,16 @@ static void build_tables(shelfi_ctx* ctx) {
       return out;
     };
     const uint32_t BL = ntt_block_log(p.logN);
-    ctx->dt.tw_fwd_blk = upload(slices(BL, pr, prs).data(), (size_t)L * N);
-    ctx->dt.tw_inv_blk = upload(slices(BL, ipr, iprs).data(), (size_t)L * N);
+    dt.tw_fwd_blk = upload(slices(BL, pr, prs).data(), (size_t)L * N);
+    dt.tw_inv_blk = upload(slices(BL, ipr, iprs).data(), (size_t)L * N);
   }
+}
+
+// (Re)build every device table for ctx->p.
+static void build_tables(shelfi_ctx* ctx) {
+  free_tables(ctx);
+  Params& p = ctx->p;
+  build_ntt_tables(p, ctx->dt);
   const uint32_t S = p.batch;
   std::vector<double> ir(S), ii(S), fr(S), fi(S);
   fft_twiddles(S, ir.data(), ii.data(), fr.data(), fi.data());
@@ -390,7 +344,7 @@ static void install_keys(shelfi_ctx* ctx, const uint64_t* pk, const uint64_t* sk
   }
 }
 
-static void require_keys(const shelfi_ctx* ctx) {
+void require_keys(const shelfi_ctx* ctx) {
   if (!ctx->keys_loaded)
     throw Error{SHELFI_ERR_STATE,
                 "no keys: call loadCryptoParams() or genCryptoContextAndKeyGen() first"};
@@ -438,6 +392,12 @@ static PalisadeCtxParams palisade_params_of(const Params& p) {
   cp.plaintext_modulus = p.scale_bits;
   cp.batch = p.batch;
   cp.sigma = (float)p.sigma;
+  // the block ends (..., ks = HYBRID 2, rs = EXACTRESCALE 1, dnum): dnum follows multDepth
+  // (2 for the reference's multDepth 1 and for key-eval-mult.txt's multDepth 2; special_primes)
+  uint32_t dn, al, kp;
+  uint64_t sp[kMaxTowers];
+  special_primes(p.N, p.L, p.q, &dn, &al, &kp, sp, nullptr);
+  cp.fields.back() = dn;
   return cp;
 }
 
@@ -1497,14 +1457,18 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
   });
 }
 
-int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double scale, size_t n,
-                       double* out_dev, void* stream) {
+// decrypt K ciphertexts of `towers` RNS towers (the context's L, or fewer after ModReduce)
+static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
+                       size_t n, double* out_dev, void* stream) {
   if (!ctx || (n && (!ct_dev || !out_dev))) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     require_keys(ctx);
     DeviceGuard g(ctx->device);
-    const Params& p = ctx->p;
+    if (towers < 1 || towers > ctx->p.L) throw Error{SHELFI_ERR_ARG, "tower count out of range for this context"};
+    Params p = ctx->p;
+    p.L = towers;  // Q_l = q_0 .. q_{towers-1}; the secret key's first towers
+    const DeviceTables& dt = towers == ctx->p.L ? ctx->dt : level_tables(ctx, towers);
     if (n > (uint64_t)K * p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
     hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     const uint64_t Kn = (n + p.batch - 1) / p.batch;
@@ -1518,12 +1482,21 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
       const uint64_t kc = std::min(kc_max, Kn - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
       dn.g0 = g0 + k0;
-      launch_decrypt(p, ctx->dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0,
-                     scratch, s, &dn);
+      launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn);
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);
   });
+}
+
+int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double scale, size_t n,
+                       double* out_dev, void* stream) {
+  return dev_decrypt(ctx, ct_dev, K, ctx ? ctx->p.L : 0, scale, n, out_dev, stream);
+}
+
+int shelfi_dev_decrypt_level(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
+                             size_t n, double* out_dev, void* stream) {
+  return dev_decrypt(ctx, ct_dev, K, towers, scale, n, out_dev, stream);
 }
 
 int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, void* stream) {

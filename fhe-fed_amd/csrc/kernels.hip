@@ -25,185 +25,10 @@
 // multiplications use Shoup's precomputed quotient (w' = floor(w 2^64 / q)).
 #include <hip/hip_runtime.h>
 
+#include "dev_common.h"
 #include "shelfi_internal.h"
 
 namespace shelfi {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// ------------------------------------------------------------ modular ops ----
-__device__ __forceinline__ uint64_t addmod(uint64_t a, uint64_t b, uint64_t q) {
-  uint64_t s = a + b;
-  return s >= q ? s - q : s;
-}
-__device__ __forceinline__ uint64_t submod(uint64_t a, uint64_t b, uint64_t q) {
-  return a >= b ? a - b : a + q - b;
-}
-// x * w mod q, w < q, w' = floor(w 2^64 / q), any 64-bit x.
-__device__ __forceinline__ uint64_t shoup_mul(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
-  uint64_t hi = __umul64hi(x, wp);
-  uint64_t r = x * w - hi * q;
-  return r >= q ? r - q : r;
-}
-// x mod q for any 64-bit x (Shoup with w = 1).
-__device__ __forceinline__ uint64_t red64(uint64_t x, uint64_t q, uint64_t one_sh) {
-  uint64_t hi = __umul64hi(x, one_sh);
-  uint64_t r = x - hi * q;
-  return r >= q ? r - q : r;
-}
-// ---- lazy NTT arithmetic (bit-exact after the final canonicalisation) -----
-// High 64 bits of x*y from three 32x32 partial products, all carries out of the low
-// 64 bits dropped (x0*y0 and the sum of the middle low halves): the exact value minus
-// 0, 1 or 2.  Six VALU ops (three quarter-rate) instead of eight for the carried form.
-__device__ __forceinline__ uint64_t umulhi_approx(uint64_t x, uint64_t y) {
-  const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
-  return (uint64_t)x1 * y1 + (((uint64_t)x1 * y0) >> 32) + (((uint64_t)x0 * y1) >> 32);
-}
-// x * w mod q up to 3 extra q: result in [0, 4q) for any 64-bit x (Shoup with the
-// quotient short by at most 2).  x*w - h*q is formed as x*w + h*(2^64 - q) so the
-// second 64-bit product takes the first as its v_mad_u64_u32 addend (no borrow chain).
-__device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
-  const uint64_t h = umulhi_approx(x, wp), nq = (uint64_t)0 - q;
-  const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
-  const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
-  const uint64_t lo = (uint64_t)h0 * n0 + (uint64_t)x0 * w0;  // mod 2^64
-  // the cross terms only touch the high word: one v_add3_u32 there (left to itself the
-  // compiler zero-extends them and spends a v_mov + 64-bit add)
-  const uint32_t c1 = x1 * w0 + x0 * w1, c2 = h1 * n0 + h0 * n1;
-  uint32_t hi;
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(lo >> 32)), "v"(c1), "v"(c2));
-  return ((uint64_t)hi << 32) | (uint32_t)lo;
-}
-// Same bound, as x*w - h*q (the form the inverse butterflies schedule better).
-__device__ __forceinline__ uint64_t shoup_lazy_sub(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
-  return x * w - umulhi_approx(x, wp) * q;
-}
-// X >= 4q ? X - 4q : X, selected on the subtraction's own borrow.
-__device__ __forceinline__ uint64_t sub4q_if_ge(uint64_t X, uint64_t q) {
-  uint64_t d;
-  const bool borrow = __builtin_sub_overflow(X, q << 2, &d);
-  return borrow ? X : d;
-}
-// Forward (CT) butterfly keeping values in [0, 8q) (q < 2^60, so 8q < 2^63).
-__device__ __forceinline__ void ct_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                        uint64_t q) {
-  const uint64_t x = sub4q_if_ge(X, q);      // [0, 4q)
-  const uint64_t t = shoup_lazy(Y, W, Wp, q);  // [0, 4q)
-  X = x + t;                                 // [0, 8q)
-  Y = x + (q << 2) - t;                      // (0, 8q)
-}
-// Inverse (GS) butterfly keeping values in [0, 4q).
-__device__ __forceinline__ void gs_bfly(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                        uint64_t q) {
-  const uint64_t s = X + Y;                  // [0, 8q)
-  const uint64_t d = X + (q << 2) - Y;       // (0, 8q)
-  X = sub4q_if_ge(s, q);                     // [0, 4q)
-  Y = shoup_lazy_sub(d, W, Wp, q);           // [0, 4q)
-}
-// ---- borrow-free conditional subtraction and one-step reduction ------------
-// d = x - c as x + (2^64 - c) (v_lshl_add_u64, no VCC carry chain); when x < c < 2^63
-// d wraps to >= 2^63, so its sign selects x (v_bfi_b32 on the sign mask).
-// (v_bfi_b32 spelled out: left to itself the compiler rebuilds the select from a 64-bit
-// compare + v_cndmask and v_max_i32 + v_and_or_b32, 6 instructions instead of 4.)
-__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, bitwise
-  uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ uint64_t csub_neg(uint64_t x, uint64_t negc) {
-  const uint64_t d = x + negc;
-  const uint32_t m = (uint32_t)((int32_t)(uint32_t)(d >> 32) >> 31);
-  const uint32_t lo = bfi32(m, (uint32_t)x, (uint32_t)d);
-  const uint32_t hi = bfi32(m, (uint32_t)(x >> 32), (uint32_t)(d >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-// any u64 x -> [0, q) (TowerConst::red_ok, q >= 2^40): quotient estimate from x's high
-// word, short by at most 1, then one conditional subtraction.
-__device__ __forceinline__ uint64_t red_any(uint64_t x, const TowerConst& c) {
-  const uint32_t k = __umulhi((uint32_t)(x >> 32), c.red_r) >> c.red_sh;
-  const uint64_t r = x + (uint64_t)k * (uint32_t)c.nq + ((uint64_t)(k * (uint32_t)(c.nq >> 32)) << 32);
-  return csub_neg(r, c.nq);
-}
-// Reduction schedule for canonical inputs (bounds in units of q): stage s reduces its x
-// inputs only when its outputs could otherwise reach 16q; fwd_bound(S) bounds the
-// outputs after S stages.
-constexpr bool fwd_red_at(int s) {
-  int B = 1;
-  for (int i = 0; i < s; ++i) B = (B + 4 > 16 ? 8 : B) + 4;
-  return B + 4 > 16;
-}
-constexpr int fwd_bound(int S) {
-  int B = 1;
-  for (int i = 0; i < S; ++i) B = (B + 4 > 16 ? 8 : B) + 4;
-  return B;
-}
-// Forward (CT) butterfly with the input reduction scheduled by the caller: inputs
-// x < 16q (RED: x -= 8q when x >= 8q, so x < 8q) or x < 12q (no reduction), any y;
-// outputs X = x + t, Y = x + 4q - t with t = y w mod q in [0, 4q): below 16q (q < 2^60).
-template <bool RED>
-__device__ __forceinline__ void ct_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                          uint64_t q, uint64_t n8q) {
-  const uint64_t x = RED ? csub_neg(X, n8q) : X;
-  const uint64_t t = shoup_lazy(Y, W, Wp, q);
-  X = x + t;
-  Y = x + (q << 2) - t;
-}
-
-// Inverse (GS) butterfly, [0, 4q) in and out, borrow-free reduction of the sum.
-__device__ __forceinline__ void gs_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
-                                          uint64_t q, uint64_t n4q) {
-  const uint64_t x = X, y = Y;
-  X = csub_neg(x + y, n4q);
-  Y = shoup_lazy(x + (q << 2) - y, W, Wp, q);
-}
-// [0, 8q) -> [0, q)
-__device__ __forceinline__ uint64_t canon8(uint64_t x, uint64_t q) {
-  x = x >= 4 * q ? x - 4 * q : x;
-  x = x >= 2 * q ? x - 2 * q : x;
-  return x >= q ? x - q : x;
-}
-// [0, 4q) -> [0, q)
-__device__ __forceinline__ uint64_t canon4(uint64_t x, uint64_t q) {
-  x = x >= 2 * q ? x - 2 * q : x;
-  return x >= q ? x - q : x;
-}
-
-// a * b mod q for arbitrary a, b < q (no precomputed companion).
-__device__ __forceinline__ uint64_t mulmod_generic(uint64_t a, uint64_t b, const TowerConst& c) {
-  uint64_t hi = __umul64hi(a, b), lo = a * b;
-  return addmod(shoup_mul(hi, c.r64, c.r64_shoup, c.q), red64(lo, c.q, c.one_shoup), c.q);
-}
-__device__ __forceinline__ uint64_t mod_signed_dev(int64_t v, const TowerConst& c) {
-  // one reduction of |v| and a sign fix-up (two branch-free reductions cost registers)
-  const bool neg = v < 0;
-  const uint64_t r = red64(neg ? (uint64_t)0 - (uint64_t)v : (uint64_t)v, c.q, c.one_shoup);
-  return (neg && r) ? c.q - r : r;
-}
-__device__ __forceinline__ uint64_t small_mod(int64_t v, uint64_t q) {  // |v| < q
-  return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v;
-}
-__device__ __forceinline__ uint32_t bitrev_dev(uint32_t x, uint32_t bits) {
-  return bits ? (__brev(x) >> (32 - bits)) : 0;
-}
-// llround (ties away from zero), the oracle's or_round_half_away.
-__device__ __forceinline__ int64_t round_half_away(double x) {
-  double t = trunc(x);
-  double d = __dsub_rn(x, t);
-  if (d >= 0.5) t = __dadd_rn(t, 1.0);
-  else if (d <= -0.5) t = __dsub_rn(t, 1.0);
-  return (int64_t)t;
-}
-// complex helpers: (a+bi)(c+di) = (ac - bd, ad + bc), each op rounded (no FMA).
-__device__ __forceinline__ double2 cmul(double2 v, double2 w) {
-  return make_double2(__dsub_rn(__dmul_rn(v.x, w.x), __dmul_rn(v.y, w.y)),
-                      __dadd_rn(__dmul_rn(v.x, w.y), __dmul_rn(v.y, w.x)));
-}
-__device__ __forceinline__ double2 cadd(double2 a, double2 b) {
-  return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
-}
-__device__ __forceinline__ double2 csub(double2 a, double2 b) {
-  return make_double2(__dsub_rn(a.x, b.x), __dsub_rn(a.y, b.y));
-}
 
 // ------------------------------------------------------------------ wavg ----
 // One thread = 2 adjacent residues (one 16-byte load per learner); one block =
@@ -1167,61 +992,6 @@ __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ 
     default: throw Error{SHELFI_ERR_ARG, "unsupported batch size"};                      \
   }
 
-// ---------------------------------------------------------------- ChaCha20 ----
-struct Key8 {
-  uint32_t k[8];
-};
-#define CH_QR(a, b, c, d)                      \
-  a += b; d ^= a; d = __builtin_rotateleft32(d, 16); \
-  c += d; b ^= c; b = __builtin_rotateleft32(b, 12); \
-  a += b; d ^= a; d = __builtin_rotateleft32(d, 8);  \
-  c += d; b ^= c; b = __builtin_rotateleft32(b, 7);
-
-// RFC 8439 block function with a 64-bit counter (words 12-13) and 64-bit nonce
-// (words 14-15); out = 8 u64 words (2i, 2i+1).
-__device__ __forceinline__ void chacha20_block(const Key8& key, uint64_t counter, uint64_t nonce,
-                                               uint64_t out[8]) {
-  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                    key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
-                    (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce,
-                    (uint32_t)(nonce >> 32)};
-  uint32_t x[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] = s[i];
-#pragma unroll 2
-  for (int i = 0; i < 10; ++i) {
-    CH_QR(x[0], x[4], x[8], x[12]);
-    CH_QR(x[1], x[5], x[9], x[13]);
-    CH_QR(x[2], x[6], x[10], x[14]);
-    CH_QR(x[3], x[7], x[11], x[15]);
-    CH_QR(x[0], x[5], x[10], x[15]);
-    CH_QR(x[1], x[6], x[11], x[12]);
-    CH_QR(x[2], x[7], x[8], x[13]);
-    CH_QR(x[3], x[4], x[9], x[14]);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    out[i] = (uint64_t)(x[2 * i] + s[2 * i]) | ((uint64_t)(x[2 * i + 1] + s[2 * i + 1]) << 32);
-}
-
-__device__ __forceinline__ int64_t gauss_sample(uint64_t r, const uint64_t* __restrict__ cdt,
-                                                int T) {
-  const uint64_t u = r >> 1;
-  int64_t k = 0;
-  for (int i = 0; i < T; ++i) k += (u >= cdt[i]) ? 1 : 0;
-  return (r & 1) ? -k : k;
-}
-__device__ __forceinline__ int64_t ternary_sample(uint64_t r) { return (int64_t)(r % 3) - 1; }
-// The same count by branch-free binary search over the table padded to 64 entries with
-// 2^64 - 1 (never <= a 63-bit u) and staged in LDS: 6 steps instead of T = 43 64-bit
-// compares (the table is non-decreasing, so #{i : u >= cdt[i]} is an upper bound).
-__device__ __forceinline__ int64_t gauss_sample_lds(uint64_t r, const uint64_t* tab) {
-  const uint64_t u = r >> 1;
-  uint32_t k = 0;
-#pragma unroll
-  for (uint32_t step = 32; step; step >>= 1) k += (u >= tab[k + step - 1]) ? step : 0u;
-  return (r & 1) ? -(int64_t)k : (int64_t)k;
-}
 
 // -------------------------------------------------------------- encrypt ----
 // One thread = ChaCha20 block bb of each sampled polynomial, which feeds the 8

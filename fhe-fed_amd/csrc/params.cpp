@@ -5,8 +5,10 @@
 // modulus chain, minimal primitive 2N-th roots and the HE-standard ring dimension.
 // These are one-time setup computations on the host; every per-ciphertext
 // operation runs in kernels.hip.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "shelfi_internal.h"
 
@@ -117,6 +119,53 @@ void generate_chain(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_
     q[0] = (first_mod_bits == scale_bits) ? prev_prime(qp, m)
                                           : prev_prime(first_prime(first_mod_bits, m), m);
   for (uint32_t t = 0; t < L; ++t) psi[t] = min_root(m, q[t]);
+}
+
+// PALISADE 1.11 HYBRID key-switching parameters of a Q chain (ParamsGenCKKS):
+// dnum = ComputeNumLargeDigits(0, multDepth) (3 above multDepth 3, 2 from 1, else 1), digits
+// of alpha = ceil(L / dnum) towers, kP = ceil(maxBits / 60) special primes where maxBits is
+// the bit length of the largest digit product, taken below FirstPrime(60, 2N) with
+// PreviousPrime, skipping the moduli of Q.  Pinned by key-eval-mult.txt
+// (palisade_pybind/SHELFI_FHE/resources/cryptoparams/: N = 2^14, Q = 60/52/53-bit towers,
+// its key polynomials carry exactly the two special primes this returns).
+void special_primes(uint32_t N, uint32_t L, const uint64_t* q, uint32_t* dnum, uint32_t* alpha,
+                    uint32_t* kP, uint64_t* p, uint64_t* ppsi) {
+  const uint32_t depth = L - 1;
+  uint32_t dn = depth > 3 ? 3 : (depth > 0 ? 2 : 1);
+  if (dn > L) dn = L;
+  const uint32_t al = (L + dn - 1) / dn;
+  uint32_t max_bits = 0;
+  for (uint32_t j = 0; j < dn; ++j) {
+    std::vector<uint64_t> prod(1, 1);  // little-endian 64-bit limbs
+    for (uint32_t i = j * al; i < std::min(L, (j + 1) * al); ++i) {
+      u128 carry = 0;
+      for (auto& w : prod) {
+        const u128 v = (u128)w * q[i] + carry;
+        w = (uint64_t)v;
+        carry = v >> 64;
+      }
+      if (carry) prod.push_back((uint64_t)carry);
+    }
+    uint32_t bits = 64 * (uint32_t)(prod.size() - 1);
+    for (uint64_t top = prod.back(); top; top >>= 1) ++bits;
+    max_bits = std::max(max_bits, bits);
+  }
+  const uint32_t k = (max_bits + 59) / 60;
+  const uint64_t m = 2ull * N;
+  uint64_t c = first_prime(60, m);
+  for (uint32_t i = 0; i < k; ++i) {
+    bool in_q;
+    do {
+      c = prev_prime(c, m);
+      in_q = false;
+      for (uint32_t t = 0; t < L; ++t) in_q = in_q || c == q[t];
+    } while (in_q);
+    p[i] = c;
+    if (ppsi) ppsi[i] = min_root(m, c);
+  }
+  *dnum = dn;
+  *alpha = al;
+  *kP = k;
 }
 
 // CKKS special-FFT twiddles, flat index lenh + j, M = 4 * slots, ksi[k] =

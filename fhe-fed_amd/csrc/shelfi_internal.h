@@ -72,6 +72,8 @@ uint32_t default_ring_dim(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bi
 void generate_chain(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
                     uint64_t* q, uint64_t* psi);
 uint64_t min_root(uint64_t m, uint64_t q);
+void special_primes(uint32_t N, uint32_t L, const uint64_t* q, uint32_t* dnum, uint32_t* alpha,
+                    uint32_t* kP, uint64_t* p, uint64_t* ppsi);
 void fft_twiddles(uint32_t slots, double* inv_re, double* inv_im, double* fwd_re, double* fwd_im);
 int gauss_cdt(double sigma, uint64_t* cdt, int max_entries);
 uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull);
@@ -117,6 +119,24 @@ struct DeviceTables {
   uint64_t qmod128_lo = 0, qmod128_hi = 0;  // Q mod 2^128
 };
 
+// NTT / CRT tables of an arbitrary tower list p.q[0..p.L) (api.cpp); free_ntt_tables frees
+// only what build_ntt_tables allocates (not the FFT / Gaussian tables of a context).
+void build_ntt_tables(const Params& p, DeviceTables& dt);
+void free_ntt_tables(DeviceTables& dt);
+// A view of towers [t0, t0 + n) of dt for launch_ntt (pointers offset, nothing owned).
+inline DeviceTables tower_view(const DeviceTables& dt, uint32_t t0, uint32_t N) {
+  DeviceTables v;
+  v.tc = dt.tc + t0;
+  v.psi_rev = dt.psi_rev + (size_t)t0 * N;
+  v.psi_rev_sh = dt.psi_rev_sh + (size_t)t0 * N;
+  v.ipsi_rev = dt.ipsi_rev + (size_t)t0 * N;
+  v.ipsi_rev_sh = dt.ipsi_rev_sh + (size_t)t0 * N;
+  v.tw_fwd_blk = dt.tw_fwd_blk + (size_t)t0 * N;
+  v.tw_inv_blk = dt.tw_inv_blk + (size_t)t0 * N;
+  v.red_ok = dt.red_ok;
+  return v;
+}
+
 struct DeviceKeys {
   uint64_t* pk = nullptr;     // [2][L][N]
   uint64_t* pk_sh = nullptr;  // [2][L][N]
@@ -128,6 +148,7 @@ struct DeviceKeys {
 
 namespace shelfi {
 class Stager;
+struct EvalState;  // eval.cpp: relinearization key + per-level tables
 }
 
 struct shelfi_ctx {
@@ -167,6 +188,7 @@ struct shelfi_ctx {
   size_t scratch_bytes = 0;
   void* io = nullptr;            // bytes-API staging arena (inputs/outputs)
   size_t io_bytes = 0;
+  shelfi::EvalState* ev = nullptr;  // EvalMult / ModReduce state (eval.cpp), lazily created
   // RCCL communicator of the multi-GPU combine (comm.cpp; ncclComm_t, opaque here)
   void* comm = nullptr;
   int comm_rank = 0, comm_world = 0;
@@ -218,5 +240,54 @@ size_t keygen_scratch_bytes(const Params& p);
 
 // comm.cpp: drop the context's RCCL communicator (if any)
 void comm_release(shelfi_ctx* ctx);
+// eval.cpp: drop the relinearization key (keys_only) or all EvalMult / ModReduce state
+void eval_release(shelfi_ctx* ctx, bool keys_only);
+// eval.cpp: NTT / CRT tables of Q_l (towers q_0 .. q_{Ll-1}) for decrypt at a level
+const DeviceTables& level_tables(shelfi_ctx* ctx, uint32_t Ll);
+// api.cpp helpers shared with eval.cpp
+void seed_to_key(uint64_t seed, uint32_t key[8]);
+void os_random(void* buf, size_t n);
+void require_keys(const shelfi_ctx* ctx);
+
+// ---- EvalMult (ct x ct) + relinearization, ModReduce (keyswitch.hip) ----
+// PALISADE 1.11 HYBRID key switching: Q_l split into digits of alpha towers, special
+// primes P = p_0 .. p_{kP-1}; the key is [2][dnum][L + kP][N] (b-vector, a-vector).
+struct KsArgs {
+  uint32_t Ll, kP, T, dn, alpha, logN, Lfull, dnFull;
+  const uint64_t* mu_inv;     // [dn][alpha] ((Q_j / q_i) mod q_i)^-1 mod q_i
+  const uint64_t* mu_inv_sh;  // Shoup companions
+  const uint64_t* mu_hat;     // [dn][alpha][T] (Q_j / q_i) mod target tower t
+  const uint64_t* md_inv;     // [kP] ((P / p_m) mod p_m)^-1 mod p_m
+  const uint64_t* md_inv_sh;
+  const uint64_t* md_hat;     // [kP][Ll] (P / p_m) mod q_t
+  const uint64_t* pinv;       // [Ll] P^-1 mod q_t
+  const uint64_t* pinv_sh;
+  const TowerConst* tq;       // towers of Q_l (the context's, prefix)
+  const TowerConst* te;       // towers of Q_l u P (extended tables)
+};
+// out = relinearized (a x b): tensor, ModUp per digit, inner product with the key,
+// ModDown.  a, b, out [K][2][Ll][N]; scratch = ks_scratch_bytes(.., K).
+size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t N, uint64_t K);
+void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTables& dte,
+                      const uint64_t* evk, const uint64_t* evk_sh, const uint64_t* x, const uint64_t* y,
+                      uint64_t K, uint64_t* out, void* scratch, hipStream_t s);
+// ModReduce: in [K][2][Ll][N] -> out [K][2][Ll-1][N] (EVAL); qlinv[t] = q_{Ll-1}^-1 mod q_t
+struct RescaleConst {
+  uint64_t ql;  // the dropped modulus q_{Ll-1}
+  uint64_t qlinv[kMaxTowers], qlinv_sh[kMaxTowers];
+};
+size_t rescale_scratch_bytes(uint32_t Ll, uint32_t N, uint64_t K);
+void launch_rescale(const DeviceTables& dt, uint32_t Ll, uint32_t logN, const RescaleConst& rc,
+                    const uint64_t* in, uint64_t K, uint64_t* out, void* scratch, hipStream_t s);
+// EvalMultKeyGen on the device: dte = tables of Q u P (T0 = L + kP towers), sk [L][N] EVAL
+struct EvkGenConst {
+  uint64_t q0;                // s is read centred from tower 0
+  uint64_t pmod[kMaxTowers];  // P mod q_t
+  uint32_t L, kP, dnum, alpha, logN;
+};
+size_t evk_scratch_bytes(uint32_t L, uint32_t kP, uint32_t N);
+void launch_evk_keygen(const EvkGenConst& g, const DeviceTables& dtq, const DeviceTables& dte,
+                       const uint64_t* cdt, int cdt_len, const uint32_t key[8], const uint64_t* sk,
+                       uint64_t* evk, void* scratch, hipStream_t s);
 
 }  // namespace shelfi

@@ -255,6 +255,37 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
 /* negacyclic NTT of P polys [P][N] whose tower is (p % L) (PALISADE order). */
 int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, void* stream);
 
+/* ---- EvalMult (ct x ct), relinearization, ModReduce ---------- *
+ * The general-circuit part of the PALISADE 1.11 CKKS scheme behind the reference's
+ * contexts (ckks.cpp:28 genCryptoContextCKKS: ks = HYBRID, rs = EXACTRESCALE, dnum from
+ * multDepth; the reference's own evaluation key is palisade_pybind/SHELFI_FHE/resources/
+ * cryptoparams/key-eval-mult.txt).  Not on the aggregation path (ckks.cpp:26 multDepth = 1).
+ * A ciphertext of `towers` RNS towers holds q_0 .. q_{towers-1} (towers = L - level). */
+/* Host-only: PALISADE's HYBRID key-switching parameters for a chain: dnum digits of alpha
+ * towers and num_special special primes (special/special_roots hold 16). */
+int shelfi_special_primes(uint32_t ring_dim, uint32_t num_towers, const uint64_t* moduli, uint32_t* dnum,
+                          uint32_t* alpha, uint32_t* num_special, uint64_t* special, uint64_t* special_roots);
+/* The context's key-switching parameters; *has_key = 1 once an evaluation key is installed. */
+int shelfi_eval_key_info(const shelfi_ctx* ctx, uint32_t* dnum, uint32_t* alpha, uint32_t* num_special,
+                         uint64_t* special, int* has_key);
+/* cc->EvalMultKeyGen(sk) on the device: the relinearization key s^2 -> s, layout
+ * [2][dnum][L + num_special][N] (b-vector, a-vector; EVALUATION), seeded like keygen. */
+int shelfi_eval_mult_keygen(shelfi_ctx* ctx);
+size_t shelfi_eval_key_words(const shelfi_ctx* ctx); /* 2 * dnum * (L + num_special) * N */
+int shelfi_get_eval_key(const shelfi_ctx* ctx, uint64_t* evk);
+int shelfi_set_eval_key(shelfi_ctx* ctx, const uint64_t* evk);
+/* cc->EvalMult(ct_a, ct_b): tensor product + HYBRID relinearization, a, b, out
+ * [K][2][towers][N] in HBM (out may be a or b).  Result depth 2, scale = scale_a scale_b. */
+int shelfi_dev_mult(shelfi_ctx* ctx, const uint64_t* a_dev, const uint64_t* b_dev, size_t K, uint32_t towers,
+                    uint64_t* out_dev, void* stream);
+/* cc->ModReduce / Rescale: [K][2][towers][N] -> [K][2][towers-1][N] (no overlap), dividing by
+ * q_{towers-1} with rounding; scale / q_{towers-1}. */
+int shelfi_dev_rescale(shelfi_ctx* ctx, const uint64_t* in_dev, size_t K, uint32_t towers, uint64_t* out_dev,
+                       void* stream);
+/* shelfi_dev_decrypt for ciphertexts of `towers` <= L towers (after ModReduce). */
+int shelfi_dev_decrypt_level(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
+                             size_t n, double* out_dev, void* stream);
+
 /* ---- test hooks (host-visible tables) ------------------------------------- */
 /* CKKS special-FFT twiddles (flat, index lenh + j) as used by the kernels. */
 int shelfi_fft_twiddles(uint32_t slots, double* inv_re, double* inv_im, double* fwd_re,

@@ -947,3 +947,254 @@ int or_decrypt_flood(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_
   free(im);
   return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* EvalMult (ct x ct) + HYBRID relinearization, ModReduce,     */
+/* EvalMultKeyGen  [PALISADE-1.11: ParamsGenCKKS (HYBRID special primes),    */
+/* KeySwitchHYBRID::KeySwitchGen / EvalFastKeySwitchCore (ApproxModUp,       */
+/* ApproxModDown), DCRTPoly::DropLastElementAndScale].  The reference's      */
+/* contexts are HYBRID / EXACTRESCALE / dnum 2 (cryptocontext.txt@2514); its */
+/* one evaluation key (palisade_pybind/.../key-eval-mult.txt) pins the       */
+/* special primes (tests/test_oracle_f4.py).  Textbook form: every product   */
+/* reduced with u128 %, every conversion summed tower by tower.              */
+/* ------------------------------------------------------------------------ */
+
+/* bit length of prod(q[i0..i1)) via 32-bit limbs */
+static uint32_t prod_bits(const uint64_t* q, uint32_t i0, uint32_t i1) {
+  uint32_t limb[64] = {1};
+  uint32_t n = 1;
+  for (uint32_t i = i0; i < i1; ++i) {
+    uint32_t parts[2] = {(uint32_t)q[i], (uint32_t)(q[i] >> 32)};
+    uint32_t res[64] = {0};
+    for (uint32_t a = 0; a < n; ++a)
+      for (uint32_t b = 0; b < 2; ++b) {
+        uint64_t carry = (uint64_t)limb[a] * parts[b];
+        for (uint32_t c = a + b; carry; ++c) {
+          carry += res[c];
+          res[c] = (uint32_t)carry;
+          carry >>= 32;
+        }
+      }
+    n += 2;
+    while (n > 1 && !res[n - 1]) --n;
+    memcpy(limb, res, sizeof(limb));
+  }
+  uint32_t bits = 32 * (n - 1);
+  for (uint32_t top = limb[n - 1]; top; top >>= 1) ++bits;
+  return bits;
+}
+
+/* ComputeNumLargeDigits(0, multDepth = L - 1): 3 above depth 3, 2 from depth 1, else 1;
+ * alpha = ceil(L / dnum); kP = ceil(maxBits / 60) primes below FirstPrime(60, 2N) by
+ * PreviousPrime, skipping Q's moduli; roots are the minimal primitive 2N-th roots. */
+int or_special_primes(uint32_t N, uint32_t L, const uint64_t* q, uint32_t* dnum, uint32_t* alpha,
+                      uint32_t* kP, uint64_t* p, uint64_t* ppsi) {
+  uint32_t dn = (L - 1 > 3) ? 3 : (L - 1 > 0 ? 2 : 1);
+  if (dn > L) dn = L;
+  uint32_t al = (L + dn - 1) / dn, maxb = 0;
+  for (uint32_t j = 0; j < dn; ++j) {
+    uint32_t i1 = (j + 1) * al < L ? (j + 1) * al : L;
+    uint32_t b = prod_bits(q, j * al, i1);
+    if (b > maxb) maxb = b;
+  }
+  uint32_t k = (maxb + 59) / 60;
+  uint64_t m = 2ull * N, c = or_first_prime(60, m);
+  for (uint32_t i = 0; i < k; ++i) {
+    int dup;
+    do {
+      c = or_prev_prime(c, m);
+      dup = 0;
+      for (uint32_t t = 0; t < L; ++t) dup |= (c == q[t]);
+    } while (dup);
+    p[i] = c;
+    ppsi[i] = or_min_root(m, c);
+  }
+  *dnum = dn;
+  *alpha = al;
+  *kP = k;
+  return 0;
+}
+
+/* tower t of the extended basis Q u P */
+static inline uint64_t ext_mod(uint32_t t, uint32_t L, const uint64_t* q, const uint64_t* p) {
+  return t < L ? q[t] : p[t - L];
+}
+
+/* EvalMultKeyGen with the product's seeded ChaCha20 stream: e_j words [0,N) of nonce
+ * (4<<56)|(j<<16); a_{j,t} word pairs of nonce (4<<56)|(j<<16)|(1+t) (t over Q u P).
+ * b_j[t] = e_j - a_j s + [t in digit j] (P mod q_t) s^2; evk [2][dnum][L+kP][N]. */
+void or_evk_keygen(uint64_t seed, uint32_t N, uint32_t L, const uint64_t* q, const uint64_t* psi,
+                   uint32_t kP, const uint64_t* p, const uint64_t* ppsi, uint32_t dnum, uint32_t alpha,
+                   double sigma, const uint64_t* sk, uint64_t* evk) {
+  uint32_t key[8];
+  or_seed_to_key(seed, key);
+  uint64_t cdt[64];
+  int T = or_gauss_cdt(sigma, cdt, 64);
+  const uint32_t T0 = L + kP;
+  int64_t* s = malloc(sizeof(int64_t) * N);
+  int64_t* e = malloc(sizeof(int64_t) * N);
+  uint64_t* w = malloc(sizeof(uint64_t) * 2 * N);
+  uint64_t* S = malloc(sizeof(uint64_t) * (size_t)T0 * N);
+  uint64_t* E = malloc(sizeof(uint64_t) * N);
+  /* s: centred coefficients of tower 0 of the secret key */
+  memcpy(E, sk, sizeof(uint64_t) * N);
+  or_ntt_inv(E, N, q[0], psi[0]);
+  for (uint32_t i = 0; i < N; ++i) s[i] = E[i] > q[0] / 2 ? -(int64_t)(q[0] - E[i]) : (int64_t)E[i];
+  for (uint32_t t = 0; t < T0; ++t) {
+    uint64_t mt = ext_mod(t, L, q, p), rt = t < L ? psi[t] : ppsi[t - L];
+    for (uint32_t i = 0; i < N; ++i) S[(size_t)t * N + i] = or_mod_signed(s[i], mt);
+    or_ntt_fwd(S + (size_t)t * N, N, mt, rt);
+  }
+  for (uint32_t j = 0; j < dnum; ++j) {
+    uint64_t nonce = (4ull << 56) | ((uint64_t)j << 16);
+    or_stream_words(key, nonce, 0, N, w);
+    for (uint32_t i = 0; i < N; ++i) e[i] = gauss_from_word(w[i], cdt, T);
+    for (uint32_t t = 0; t < T0; ++t) {
+      uint64_t mt = ext_mod(t, L, q, p), rt = t < L ? psi[t] : ppsi[t - L];
+      for (uint32_t i = 0; i < N; ++i) E[i] = or_mod_signed(e[i], mt);
+      or_ntt_fwd(E, N, mt, rt);
+      uint64_t pm = 1;
+      for (uint32_t u = 0; u < kP; ++u) pm = mulmod(pm, p[u] % mt, mt);
+      int in_digit = t < L && t >= j * alpha && t < (j + 1) * alpha;
+      uint64_t* a = w; /* reuse: word pairs of this tower */
+      or_stream_words(key, nonce | (1 + t), 0, 2ull * N, a);
+      uint64_t* B = evk + ((size_t)j * T0 + t) * N;
+      uint64_t* A = evk + ((size_t)(dnum + j) * T0 + t) * N;
+      const uint64_t* St = S + (size_t)t * N;
+      for (uint32_t i = 0; i < N; ++i) {
+        uint64_t av = uniform_mod(a[2 * i], a[2 * i + 1], mt);
+        uint64_t b = submod(E[i], mulmod(av, St[i], mt), mt);
+        if (in_digit) b = addmod(b, mulmod(pm, mulmod(St[i], St[i], mt), mt), mt);
+        B[i] = b;
+        A[i] = av;
+      }
+    }
+  }
+  free(s);
+  free(e);
+  free(w);
+  free(S);
+  free(E);
+}
+
+/* EvalMult of one ciphertext pair x, y [2][Ll][N] (EVALUATION) -> out [2][Ll][N]. */
+void or_eval_mult(const uint64_t* x, const uint64_t* y, uint32_t N, uint32_t Ll, uint32_t L, const uint64_t* q,
+                  const uint64_t* psi, uint32_t kP, const uint64_t* p, const uint64_t* ppsi, uint32_t dnum,
+                  uint32_t alpha, const uint64_t* evk, uint64_t* out) {
+  const uint32_t T = Ll + kP, T0 = L + kP, dn = (Ll + alpha - 1) / alpha;
+  const size_t LN = (size_t)Ll * N;
+  uint64_t* c2 = malloc(sizeof(uint64_t) * LN);
+  uint64_t* ext = malloc(sizeof(uint64_t) * (size_t)T * N);
+  uint64_t* acc = calloc((size_t)2 * T * N, sizeof(uint64_t));
+  uint64_t* tmp = malloc(sizeof(uint64_t) * N);
+  uint64_t em[32], er[32];
+  for (uint32_t t = 0; t < T; ++t) {
+    em[t] = t < Ll ? q[t] : p[t - Ll];
+    er[t] = t < Ll ? psi[t] : ppsi[t - Ll];
+  }
+  /* tensor */
+  for (uint32_t t = 0; t < Ll; ++t)
+    for (uint32_t i = 0; i < N; ++i) {
+      size_t e0 = (size_t)t * N + i, e1 = LN + e0;
+      uint64_t qt = q[t];
+      out[e0] = mulmod(x[e0], y[e0], qt);
+      out[e1] = addmod(mulmod(x[e0], y[e1], qt), mulmod(x[e1], y[e0], qt), qt);
+      c2[e0] = mulmod(x[e1], y[e1], qt);
+    }
+  for (uint32_t t = 0; t < Ll; ++t) or_ntt_inv(c2 + (size_t)t * N, N, q[t], psi[t]);
+  /* ModUp per digit, inner product with the key */
+  for (uint32_t j = 0; j < dn; ++j) {
+    uint32_t s0 = j * alpha, cnt = (s0 + alpha <= Ll) ? alpha : Ll - s0;
+    for (uint32_t t = 0; t < T; ++t) {
+      uint64_t mt = em[t];
+      uint64_t* o = ext + (size_t)t * N;
+      if (t >= s0 && t < s0 + cnt) {
+        memcpy(o, c2 + (size_t)t * N, sizeof(uint64_t) * N);
+      } else {
+        for (uint32_t i = 0; i < N; ++i) {
+          uint64_t sum = 0;
+          for (uint32_t u = 0; u < cnt; ++u) {
+            uint64_t qi = q[s0 + u], hi_ = 1, ht = 1;
+            for (uint32_t v = 0; v < cnt; ++v)
+              if (v != u) {
+                hi_ = mulmod(hi_, q[s0 + v] % qi, qi);
+                ht = mulmod(ht, q[s0 + v] % mt, mt);
+              }
+            uint64_t yv = mulmod(c2[(size_t)(s0 + u) * N + i], inv_mod(hi_, qi), qi);
+            sum = addmod(sum, mulmod(yv % mt, ht, mt), mt);
+          }
+          o[i] = sum;
+        }
+      }
+      or_ntt_fwd(o, N, mt, er[t]);
+      uint32_t tk = t < Ll ? t : L + (t - Ll);
+      const uint64_t* B = evk + ((size_t)j * T0 + tk) * N;
+      const uint64_t* A = evk + ((size_t)(dnum + j) * T0 + tk) * N;
+      for (uint32_t i = 0; i < N; ++i) {
+        size_t a0 = (size_t)t * N + i, a1 = (size_t)(T + t) * N + i;
+        acc[a0] = addmod(acc[a0], mulmod(o[i], B[i], mt), mt);
+        acc[a1] = addmod(acc[a1], mulmod(o[i], A[i], mt), mt);
+      }
+    }
+  }
+  /* ModDown: (acc_Q - conv_{P->Q}(acc_P)) P^-1, added to the tensor's c0, c1 */
+  for (uint32_t poly = 0; poly < 2; ++poly) {
+    uint64_t* a = acc + (size_t)poly * T * N;
+    for (uint32_t m = 0; m < kP; ++m) or_ntt_inv(a + (size_t)(Ll + m) * N, N, p[m], ppsi[m]);
+    for (uint32_t t = 0; t < Ll; ++t) {
+      uint64_t qt = q[t], Pm = 1;
+      for (uint32_t m = 0; m < kP; ++m) Pm = mulmod(Pm, p[m] % qt, qt);
+      for (uint32_t i = 0; i < N; ++i) {
+        uint64_t sum = 0;
+        for (uint32_t m = 0; m < kP; ++m) {
+          uint64_t pm = p[m], hp = 1, hq = 1;
+          for (uint32_t v = 0; v < kP; ++v)
+            if (v != m) {
+              hp = mulmod(hp, p[v] % pm, pm);
+              hq = mulmod(hq, p[v] % qt, qt);
+            }
+          uint64_t yv = mulmod(a[(size_t)(Ll + m) * N + i], inv_mod(hp, pm), pm);
+          sum = addmod(sum, mulmod(yv % qt, hq, qt), qt);
+        }
+        tmp[i] = sum;
+      }
+      or_ntt_fwd(tmp, N, qt, psi[t]);
+      uint64_t pinv = inv_mod(Pm, qt);
+      uint64_t* o = out + (size_t)poly * LN + (size_t)t * N;
+      for (uint32_t i = 0; i < N; ++i)
+        o[i] = addmod(o[i], mulmod(submod(a[(size_t)t * N + i], tmp[i], qt), pinv, qt), qt);
+    }
+  }
+  free(c2);
+  free(ext);
+  free(acc);
+  free(tmp);
+}
+
+/* ModReduce of one ciphertext in [2][Ll][N] -> out [2][Ll-1][N]: (c_t - [c_l]) q_l^-1 with
+ * [c_l] the last tower's coefficients taken centred (NativeVector::SwitchModulus). */
+void or_rescale(const uint64_t* in, uint32_t N, uint32_t Ll, const uint64_t* q, const uint64_t* psi,
+                uint64_t* out) {
+  const uint32_t Lo = Ll - 1;
+  const uint64_t ql = q[Lo];
+  uint64_t* last = malloc(sizeof(uint64_t) * N);
+  uint64_t* v = malloc(sizeof(uint64_t) * N);
+  for (uint32_t poly = 0; poly < 2; ++poly) {
+    memcpy(last, in + ((size_t)poly * Ll + Lo) * N, sizeof(uint64_t) * N);
+    or_ntt_inv(last, N, ql, psi[Lo]);
+    for (uint32_t t = 0; t < Lo; ++t) {
+      uint64_t qt = q[t];
+      for (uint32_t i = 0; i < N; ++i) {
+        int64_t c = last[i] > ql / 2 ? -(int64_t)(ql - last[i]) : (int64_t)last[i];
+        v[i] = or_mod_signed(c, qt);
+      }
+      or_ntt_fwd(v, N, qt, psi[t]);
+      uint64_t inv = inv_mod(ql % qt, qt);
+      const uint64_t* x = in + ((size_t)poly * Ll + t) * N;
+      uint64_t* o = out + ((size_t)poly * Lo + t) * N;
+      for (uint32_t i = 0; i < N; ++i) o[i] = mulmod(submod(x[i], v[i], qt), inv, qt);
+    }
+  }
+  free(last);
+  free(v);
+}

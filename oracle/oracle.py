@@ -81,6 +81,12 @@ def _load():
         "or_sample_encrypt": (None, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_double, i64p, i64p, i64p]),
         "or_sample_keygen": (None, [C.c_uint64, C.c_uint32, C.c_uint32, u64p, C.c_double, i64p, i64p,
                                     u64p]),
+        "or_special_primes": (C.c_int, [C.c_uint32, C.c_uint32, u64p, u32p, u32p, u32p, u64p, u64p]),
+        "or_evk_keygen": (None, [C.c_uint64, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32, u64p, u64p,
+                                 C.c_uint32, C.c_uint32, C.c_double, u64p, u64p]),
+        "or_eval_mult": (None, [u64p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32, u64p,
+                                u64p, C.c_uint32, C.c_uint32, u64p, u64p]),
+        "or_rescale": (None, [u64p, C.c_uint32, C.c_uint32, u64p, u64p, u64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -375,3 +381,53 @@ def decrypt_flood(ct, sk, q, psi, slots: int, scale: float, n: int, seed: int, g
     if rc:
         raise ValueError("decrypt failed rc=%d" % rc)
     return out, le.value, bool(fail.value)
+
+
+# ------------------------------ §8 f4: EvalMult / relinearization / ModReduce ----
+def special_primes(N: int, q):
+    """PALISADE 1.11 ParamsGenCKKS (HYBRID): -> (dnum, alpha, special primes, their roots)."""
+    q = u64(q)
+    dn, al, k = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    p, r = np.zeros(16, np.uint64), np.zeros(16, np.uint64)
+    lib.or_special_primes(N, len(q), _p(q, u64p), C.byref(dn), C.byref(al), C.byref(k), _p(p, u64p),
+                          _p(r, u64p))
+    return dn.value, al.value, p[:k.value].copy(), r[:k.value].copy()
+
+
+def evk_keygen(seed: int, sk, q, psi, sigma: float = SIGMA):
+    """EvalMultKeyGen with the product's seeded stream -> evk [2][dnum][L+kP][N]."""
+    sk, q, psi = u64(sk), u64(q), u64(psi)
+    L, N = sk.shape
+    dn, al, p, pr = special_primes(N, q)
+    evk = np.zeros((2, dn, L + len(p), N), np.uint64)
+    lib.or_evk_keygen(seed, N, L, _p(q, u64p), _p(psi, u64p), len(p), _p(p, u64p), _p(pr, u64p), dn, al,
+                      sigma, _p(sk, u64p), _p(evk, u64p))
+    return evk
+
+
+def eval_mult(x, y, evk, q, psi):
+    """cc->EvalMult(x, y) with HYBRID relinearization; x, y [K][2][Ll][N] at level L - Ll
+    (q, psi: the context's whole chain)."""
+    x, y, evk, q, psi = u64(x), u64(y), u64(evk), u64(q), u64(psi)
+    K, _, Ll, N = x.shape
+    L = len(q)
+    dn, al, p, pr = special_primes(N, q)
+    out = np.zeros_like(x)
+    for k in range(K):
+        xk, yk, ok = u64(x[k]), u64(y[k]), np.zeros((2, Ll, N), np.uint64)
+        lib.or_eval_mult(_p(xk, u64p), _p(yk, u64p), N, Ll, L, _p(q, u64p), _p(psi, u64p), len(p), _p(p, u64p),
+                         _p(pr, u64p), dn, al, _p(evk, u64p), _p(ok, u64p))
+        out[k] = ok
+    return out
+
+
+def rescale(ct, q, psi):
+    """cc->ModReduce: [K][2][Ll][N] -> [K][2][Ll-1][N]."""
+    ct, q, psi = u64(ct), u64(q), u64(psi)
+    K, _, Ll, N = ct.shape
+    out = np.zeros((K, 2, Ll - 1, N), np.uint64)
+    for k in range(K):
+        ck, ok = u64(ct[k]), np.zeros((2, Ll - 1, N), np.uint64)
+        lib.or_rescale(_p(ck, u64p), N, Ll, _p(q, u64p), _p(psi, u64p), _p(ok, u64p))
+        out[k] = ok
+    return out

@@ -1,0 +1,126 @@
+"""SURVEY §8 f4 on the MI355X: EvalMultKeyGen, EvalMult (ct x ct) with HYBRID
+relinearization, ModReduce and decrypt at a level — every residue bit-exact against the
+oracle's restatement (oracle/ckks_oracle.c or_evk_keygen / or_eval_mult / or_rescale),
+and the decrypted values equal to the plaintext products.  PALISADE parity of the key
+switching itself is unpinned (tests/test_oracle_f4.py says why); its parameters (dnum,
+special primes, roots) are pinned by the reference's key-eval-mult.txt."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+# (batch, multDepth): cfg1's ring (2^13, L = 2, alpha = 1), an L = 3 chain whose second digit
+# is partial, and cfg2/3's ring (2^15, L = 4, two full digits)
+CASES = [(4096, 1), (4096, 2), (16384, 3)]
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.fixture(scope="module", params=CASES, ids=lambda c: "b%d_d%d" % c)
+def ctx(request):
+    batch, depth = request.param
+    c = m.CKKS("ckks", batch, 52, "", multDepth=depth, seed=404 + depth, decodeNoise=False)
+    assert c.genCryptoContextAndKeyGen() == 1
+    c.evalMultKeyGen()
+    inf = c.info()
+    q, psi = np.array(inf["moduli"], np.uint64), np.array(inf["roots"], np.uint64)
+    pk, sk = c.get_keys()
+    rng = np.random.default_rng(depth)
+    n = 2 * inf["batch"]
+    xs = [rng.uniform(-1, 1, n) for _ in range(3)]
+    cts = [D.encrypt(c, torch.tensor(x, dtype=torch.float64, device="cuda")) for x in xs]
+    return dict(c=c, inf=inf, q=q, psi=psi, sk=sk, seed=404 + depth, n=n, xs=xs, cts=cts)
+
+
+def test_eval_key_bitexact_and_parameters(ctx):
+    c, q, psi, sk = ctx["c"], ctx["q"], ctx["psi"], ctx["sk"]
+    info = c.eval_key_info()
+    dn, al, p, _ = O.special_primes(ctx["inf"]["ring_dim"], q)
+    assert info["has_key"] and (info["dnum"], info["alpha"]) == (dn, al)
+    assert info["special_moduli"] == [int(v) for v in p]
+    evk = c.get_eval_key()
+    assert evk.shape == (2, dn, len(q) + len(p), ctx["inf"]["ring_dim"])
+    assert np.array_equal(evk, O.evk_keygen(ctx["seed"], sk, q, psi))
+
+
+def test_mult_rescale_bitexact_and_values(ctx):
+    c, q, psi, sk, n = ctx["c"], ctx["q"], ctx["psi"], ctx["sk"], ctx["n"]
+    x, y = ctx["xs"][0], ctx["xs"][1]
+    a, b = ctx["cts"][0], ctx["cts"][1]
+    evk = c.get_eval_key()
+    S, L, d = ctx["inf"]["batch"], len(q), ctx["inf"]["delta"]
+    prod = D.mult(c, a, b)
+    ref = O.eval_mult(_u64(a), _u64(b), evk, q, psi)
+    assert np.array_equal(_u64(prod), ref)
+    dec = D.decrypt(c, prod, n, d * d).cpu().numpy()
+    assert np.array_equal(dec, O.decrypt_vector(ref, sk, q, psi, S, d * d, n))
+    assert np.abs(dec - x * y).max() < 1e-7
+    if L < 2:
+        return
+    r = D.rescale(c, prod)
+    rref = O.rescale(ref, q, psi)
+    assert r.shape[2] == L - 1 and np.array_equal(_u64(r), rref)
+    s1 = d * d / float(q[-1])
+    dec = D.decrypt(c, r, n, s1).cpu().numpy()
+    assert np.array_equal(dec, O.decrypt_vector(rref, sk[:L - 1], q[:L - 1], psi[:L - 1], S, s1, n))
+    assert np.abs(dec - x * y).max() < 1e-7
+
+
+def test_mult_below_the_top_level(ctx):
+    """(x y)^2: EvalMult of rescaled ciphertexts (L - 1 towers: fewer digits, the
+    partial last digit) — bit-exact vs the oracle at that level, then rescaled again."""
+    c, q, psi, sk, n = ctx["c"], ctx["q"], ctx["psi"], ctx["sk"], ctx["n"]
+    L = len(q)
+    if L < 3:
+        pytest.skip("needs two rescales")
+    x, y = ctx["xs"][0], ctx["xs"][1]
+    S, d = ctx["inf"]["batch"], ctx["inf"]["delta"]
+    evk = c.get_eval_key()
+    r = D.rescale(c, D.mult(c, ctx["cts"][0], ctx["cts"][1]))
+    sq = D.mult(c, r, r)
+    assert np.array_equal(_u64(sq), O.eval_mult(_u64(r), _u64(r), evk, q, psi))
+    r2 = D.rescale(c, sq)
+    s1 = d * d / float(q[-1])
+    s2 = s1 * s1 / float(q[-2])
+    assert np.array_equal(_u64(r2), O.rescale(_u64(sq), q, psi))
+    dec = D.decrypt(c, r2, n, s2).cpu().numpy()
+    assert np.abs(dec - (x * y) ** 2).max() < 1e-6
+
+
+def test_eval_key_import_gives_identical_products(ctx):
+    c = ctx["c"]
+    other = m.CKKS("ckks", ctx["inf"]["batch"], 52, "", multDepth=len(ctx["q"]) - 1, decodeNoise=False)
+    pk, sk = c.get_keys()
+    other.set_keys(pk, sk)
+    with pytest.raises(RuntimeError, match="evaluation key"):
+        D.mult(other, ctx["cts"][0], ctx["cts"][1])
+    other.set_eval_key(c.get_eval_key())
+    a, b = ctx["cts"][1], ctx["cts"][2]
+    assert torch.equal(D.mult(other, a, b), D.mult(c, a, b))
+    bad = c.get_eval_key()
+    bad[0, 0, 0, 0] = ctx["q"][0]  # a residue >= q
+    with pytest.raises(RuntimeError):
+        other.set_eval_key(bad)
+
+
+def test_argument_errors(ctx):
+    c = ctx["c"]
+    a = ctx["cts"][0]
+    with pytest.raises(ValueError):
+        D.mult(c, a, ctx["cts"][1][:1])  # different K
+    if a.shape[2] >= 2:
+        with pytest.raises(ValueError):
+            D.rescale(c, a, out=a)  # wrong shape (and overlapping)
+        K, _, l, N = a.shape
+        with pytest.raises(ValueError, match="overlap"):  # the C ABI's own overlap check
+            D.rescale(c, a, out=a.view(-1)[:K * 2 * (l - 1) * N].view(K, 2, l - 1, N))
+    one = a[:, :, :1].contiguous()
+    with pytest.raises(ValueError):
+        D.rescale(c, one)
