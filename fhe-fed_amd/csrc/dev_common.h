@@ -241,4 +241,158 @@ __device__ __forceinline__ int64_t gauss_sample_lds(uint64_t r, const uint64_t* 
   return (r & 1) ? -(int64_t)k : (int64_t)k;
 }
 
+// ---- LDS block passes: radix-2^k register chunks -------------------------
+// LDS layout: plain.  An XOR swizzle (i ^ h(i >> 5)) that removes the 8-/4-way bank
+// conflicts of the d = 4 / d = 1 chunks measured SLOWER (30.4 vs 27.5 ms for the
+// ntt_fwd_blocks share of a 11,424-ciphertext encrypt sweep): this pass is bound by
+// VALU issue (64-bit Shoup products), not by LDS.  lds_sw is kept as the one place
+// to change the layout.
+__device__ __forceinline__ uint32_t lds_sw(uint32_t i) { return i; }
+// 16-byte fill/drain: elements (2p, 2p+1) share one aligned 16-byte LDS slot under
+// lds_sw, swapped when the XOR flips bit 0.
+__device__ __forceinline__ void lds_put2(uint64_t* sm, uint32_t p, ulonglong2 v) {
+  const uint32_t i = 2 * p, s = lds_sw(i);
+  if (s & 1) {
+    const uint64_t t = v.x;
+    v.x = v.y;
+    v.y = t;
+  }
+  reinterpret_cast<ulonglong2*>(sm)[s >> 1] = v;
+}
+__device__ __forceinline__ ulonglong2 lds_get2(const uint64_t* sm, uint32_t p) {
+  const uint32_t i = 2 * p, s = lds_sw(i);
+  ulonglong2 v = reinterpret_cast<const ulonglong2*>(sm)[s >> 1];
+  if (s & 1) {
+    const uint64_t t = v.x;
+    v.x = v.y;
+    v.y = t;
+  }
+  return v;
+}
+// A block of blk = 2^blkLog contiguous elements (global block index b) sits in LDS.
+// Its stages are taken KCH = 3 at a time: each thread loads a set of 2^KCH elements
+// that only interact among themselves during those stages, runs them in registers
+// (2^KCH - 1 twiddle pairs), and writes the set back — one barrier per chunk instead
+// of one per stage.  256 threads; blocks of 2^blkLog <= 4096 elements (ntt_block_log).
+//
+// Forward (CT, half-size h = blk/2 .. 1): a chunk of k stages starting at half-size
+// h0 works on sets {j0 + d m}, d = h0 / 2^(k-1), j0 = g 2 h0 + off (off < d).
+template <int KC>
+__device__ __forceinline__ void fwd_chunk(uint64_t* sm, uint32_t blk, uint32_t h0Log, uint32_t b,
+                                          uint32_t blkLog, uint32_t logN,
+                                          const uint64_t* __restrict__ w,
+                                          const uint64_t* __restrict__ wp, uint64_t q) {
+  constexpr int M = 1 << KC;
+  const uint32_t dLog = h0Log - (KC - 1), d = 1u << dLog;
+  const uint32_t nsets = blk >> KC;
+  const uint64_t gbase = (uint64_t)b << blkLog;  // global index of the block start
+  for (uint32_t set = threadIdx.x; set < nsets; set += 256) {
+    const uint32_t g = set >> dLog, off = set & (d - 1);
+    const uint32_t j0 = (g << (h0Log + 1)) + off;
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = sm[lds_sw(j0 + (m << dLog))];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int hm = 1 << (KC - 1 - i);          // half-size in units of d
+      const uint32_t hLog = h0Log - i;           // log2 of the half-size
+      const uint32_t s = logN - 1 - hLog;        // global stage: m_stage = 2^s
+#pragma unroll
+      for (int gs = 0; gs < (1 << i); ++gs) {    // 2^i twiddle groups at this stage
+        const uint64_t gi = (gbase + j0 + ((uint64_t)(gs * 2 * hm) << dLog)) >> (hLog + 1);
+        const uint64_t W = w[(1ull << s) + gi], Wp = wp[(1ull << s) + gi];
+#pragma unroll
+        for (int mm = 0; mm < hm; ++mm) {
+          const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
+          ct_bfly(x[m0], x[m1], W, Wp, q);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) sm[lds_sw(j0 + (m << dLog))] = x[m];
+  }
+}
+
+// Runs every stage of the block (local half-sizes blk/2 .. 1), chunked 3 at a time.
+__device__ __forceinline__ void ntt_fwd_block_stages(uint64_t* sm, uint32_t blkLog, uint32_t b,
+                                                     uint32_t logN, const uint64_t* __restrict__ w,
+                                                     const uint64_t* __restrict__ wp, uint64_t q) {
+  const uint32_t blk = 1u << blkLog;
+  uint32_t left = blkLog;  // stages remaining; next half-size = 2^(left-1)
+  while (left > 0) {
+    const uint32_t h0Log = left - 1;
+    if (left >= 3) {
+      fwd_chunk<3>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 3;
+    } else if (left == 2) {
+      fwd_chunk<2>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 2;
+    } else {
+      fwd_chunk<1>(sm, blk, h0Log, b, blkLog, logN, w, wp, q);
+      left -= 1;
+    }
+    __syncthreads();
+  }
+}
+
+// Inverse (GS, half-size t = 1 .. blk/2): a chunk of k stages starting at half-size
+// t0 works on sets {j0 + t0 m}, j0 = g t0 2^k + off (off < t0); twiddle for half-size
+// t at global element j: ipsi_rev[N/(2t) + j/(2t)].
+template <int KC>
+__device__ __forceinline__ void inv_chunk(uint64_t* sm, uint32_t blk, uint32_t t0Log, uint32_t b,
+                                          uint32_t blkLog, uint32_t logN,
+                                          const uint64_t* __restrict__ w,
+                                          const uint64_t* __restrict__ wp, uint64_t q) {
+  constexpr int M = 1 << KC;
+  const uint32_t t0 = 1u << t0Log;
+  const uint32_t nsets = blk >> KC;
+  const uint64_t gbase = (uint64_t)b << blkLog;
+  for (uint32_t set = threadIdx.x; set < nsets; set += 256) {
+    const uint32_t g = set >> t0Log, off = set & (t0 - 1);
+    const uint32_t j0 = (g << (t0Log + KC)) + off;
+    uint64_t x[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = sm[lds_sw(j0 + (m << t0Log))];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int hm = 1 << i;                  // half-size in units of t0
+      const uint32_t tLog = t0Log + i;
+      const uint64_t hbase = (uint64_t)1 << (logN - 1 - tLog);  // N / (2t)
+#pragma unroll
+      for (int gs = 0; gs < (M >> (i + 1)); ++gs) {
+        const uint64_t gi = (gbase + j0 + ((uint64_t)(gs * 2 * hm) << t0Log)) >> (tLog + 1);
+        const uint64_t W = w[hbase + gi], Wp = wp[hbase + gi];
+#pragma unroll
+        for (int mm = 0; mm < hm; ++mm) {
+          const int m0 = gs * 2 * hm + mm, m1 = m0 + hm;
+          gs_bfly(x[m0], x[m1], W, Wp, q);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) sm[lds_sw(j0 + (m << t0Log))] = x[m];
+  }
+}
+
+__device__ __forceinline__ void ntt_inv_block_stages(uint64_t* sm, uint32_t blkLog, uint32_t b,
+                                                     uint32_t logN, const uint64_t* __restrict__ w,
+                                                     const uint64_t* __restrict__ wp, uint64_t q) {
+  const uint32_t blk = 1u << blkLog;
+  uint32_t t0Log = 0;
+  while (t0Log < blkLog) {
+    const uint32_t left = blkLog - t0Log;
+    if (left >= 3) {
+      inv_chunk<3>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 3;
+    } else if (left == 2) {
+      inv_chunk<2>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 2;
+    } else {
+      inv_chunk<1>(sm, blk, t0Log, b, blkLog, logN, w, wp, q);
+      t0Log += 1;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace shelfi

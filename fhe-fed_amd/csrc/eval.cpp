@@ -13,11 +13,14 @@
 
 namespace shelfi {
 
+constexpr int kMaxDigits = 3;  // ComputeNumLargeDigits never exceeds 3
+
 struct LevelState {
   bool built = false;
   bool own_q = false;  // q tables built here (levels below L); level L uses ctx->dt
   DeviceTables q;      // Q_l: NTT + CRT tables (decrypt at this level)
   DeviceTables ext;    // Q_l u P (key switching)
+  DeviceTables dtf[kMaxDigits];  // per digit: its foreign towers (Q_l minus the digit, then P)
   uint64_t* ks = nullptr;
   KsArgs args{};
 };
@@ -38,6 +41,7 @@ static void free_level(LevelState& l) {
     free_ntt_tables(l.q);
   }
   free_ntt_tables(l.ext);
+  for (auto& d : l.dtf) free_ntt_tables(d);
   dfree_t(l.ks);
   l = LevelState{};
 }
@@ -96,6 +100,19 @@ static LevelState& level(shelfi_ctx* ctx, uint32_t Ll) {
       pe.psi[Ll + m] = ev.ppsi[m];
     }
     build_ntt_tables(pe, l.ext);
+    if (dn > (uint32_t)kMaxDigits) throw Error{SHELFI_ERR_ARG, "EvalMult: more than 3 digits"};
+    for (uint32_t j = 0; j < dn; ++j) {  // digit j's foreign towers, in ModUp's order
+      const uint32_t s = j * al, cnt = std::min(al, Ll - s);
+      Params pf = P0;
+      pf.L = T - cnt;
+      for (uint32_t t = 0, u = 0; t < T; ++t)
+        if (t < s || t >= s + cnt) {
+          pf.q[u] = pe.q[t];
+          pf.psi[u] = pe.psi[t];
+          ++u;
+        }
+      build_ntt_tables(pf, l.dtf[j]);
+    }
     // constants: mu_inv | mu_inv_sh [dn][al] | mu_hat [dn][al][T] | md_inv | md_inv_sh [kP] |
     // md_hat [kP][Ll] | pinv | pinv_sh [Ll]
     const size_t o_mi = 0, o_mis = o_mi + dn * al, o_mh = o_mis + dn * al, o_di = o_mh + (size_t)dn * al * T,
@@ -320,13 +337,14 @@ int shelfi_dev_mult(shelfi_ctx* ctx, const uint64_t* a_dev, const uint64_t* b_de
     const KsArgs& a = l.args;
     const uint32_t N = ctx->p.N;
     hipStream_t s = (hipStream_t)stream;
-    const uint64_t kc_max = chunk_of(K, ks_scratch_bytes(a.Ll, a.kP, a.dn, N, 1));
-    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, ks_scratch_bytes(a.Ll, a.kP, a.dn, N, kc_max));
+    const uint64_t kc_max = chunk_of(K, ks_scratch_bytes(a.Ll, a.kP, a.dn, a.alpha, N, 1));
+    void* scratch =
+        ensure(ctx->scratch, ctx->scratch_bytes, ks_scratch_bytes(a.Ll, a.kP, a.dn, a.alpha, N, kc_max));
     const uint64_t ctw = 2ull * towers * N;
     for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
       const uint64_t kc = std::min<uint64_t>(kc_max, K - k0);
-      launch_eval_mult(a, ctx->dt, l.ext, ctx->ev->evk, ctx->ev->evk_sh, a_dev + k0 * ctw, b_dev + k0 * ctw, kc,
-                       out_dev + k0 * ctw, scratch, s);
+      launch_eval_mult(a, ctx->dt, l.ext, l.dtf, ctx->ev->evk, ctx->ev->evk_sh, a_dev + k0 * ctw,
+                       b_dev + k0 * ctw, kc, out_dev + k0 * ctw, scratch, s);
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
   });

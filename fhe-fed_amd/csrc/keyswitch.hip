@@ -22,6 +22,8 @@
 // so the tower constants are scalar loads.  The NTTs in between are launch_ntt's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dev_common.h"
 #include "shelfi_internal.h"
 
@@ -36,30 +38,83 @@ __device__ __forceinline__ uint64_t red128(du128 acc, const TowerConst& c) {
 }
 __device__ __forceinline__ du128 mul128(uint64_t a, uint64_t b) { return (du128)a * b; }
 
-// ---------------------------------------------------------------- tensor ----
-// d0 = a0 b0 -> out[.][0], d1 = a0 b1 + a1 b0 -> out[.][1], d2 = a1 b1 -> d2[k][t]
-__global__ __launch_bounds__(256) void tensor_kernel(const uint64_t* __restrict__ x,
-                                                     const uint64_t* __restrict__ y, uint32_t Ll,
-                                                     uint32_t logN, const TowerConst* __restrict__ tq,
-                                                     uint64_t* __restrict__ out, uint64_t* __restrict__ d2) {
-  const uint32_t N = 1u << logN, bpr = N >> 8;
-  const uint64_t row = blockIdx.x / bpr;  // k * Ll + t
-  const uint32_t n = (blockIdx.x % bpr) * 256 + threadIdx.x;
+// Digit j of a level owns towers [j alpha, j alpha + cnt) of Q_l; its "foreign" towers (the
+// rest of Q_l, then P) are the ones ModUp must produce, stored in that order (index u =
+// t < s ? t : t - cnt) so every NTT over them is a plain batch with per-digit tables.
+__device__ __forceinline__ void digit_span(const KsArgs& a, uint32_t j, uint32_t& s, uint32_t& cnt) {
+  s = j * a.alpha;
+  cnt = min(a.alpha, a.Ll - s);
+}
+__device__ __forceinline__ uint64_t ext_base(const KsArgs& a, uint32_t j, uint64_t K) {
+  uint64_t base = 0;
+  for (uint32_t i = 0; i < j; ++i) {
+    uint32_t s, cnt;
+    digit_span(a, i, s, cnt);
+    base += (uint64_t)(a.T - cnt) * K;  // in polynomials
+  }
+  return base << a.logN;
+}
+
+// ------------------------------------------------ tensor + first INTT pass ----
+// One workgroup per (ct, tower, block): c0 = a0 b0 and c1 = a0 b1 + a1 b0 go to `out`,
+// c2 = a1 b1 to d2e (EVALUATION, kept for the digits' own towers) and into LDS, where the
+// first inverse stages run; the lazy block goes to d2c for the columns pass (or, for a
+// single-block ring, the scaled canonical coefficients).
+// (x, y and out may alias: each element is read before it is written, by the same thread)
+__global__ __launch_bounds__(256) void ks_tensor_intt_kernel(const uint64_t* x, const uint64_t* y, uint32_t Ll,
+                                                             uint32_t logN, uint32_t blkLog,
+                                                             const uint64_t* __restrict__ itw,
+                                                             const uint64_t* __restrict__ itwp,
+                                                             const TowerConst* __restrict__ tq, uint64_t* out,
+                                                             uint64_t* __restrict__ d2e,
+                                                             uint64_t* __restrict__ d2c) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << logN, blk = 1u << blkLog, sh = logN - blkLog;
+  const uint64_t row = blockIdx.x >> sh;  // k * Ll + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint64_t k = row / Ll;
   const uint32_t t = (uint32_t)(row % Ll);
   const TowerConst c = tq[t];
-  const uint64_t i0 = ((k * 2 + 0) * Ll + t) * N + n, i1 = i0 + (uint64_t)Ll * N;
-  const uint64_t a0 = x[i0], a1 = x[i1], b0 = y[i0], b1 = y[i1];
-  const uint64_t d0 = mulmod_generic(a0, b0, c);
-  const uint64_t d1 = addmod(mulmod_generic(a0, b1, c), mulmod_generic(a1, b0, c), c.q);
-  d2[row * N + n] = mulmod_generic(a1, b1, c);
-  out[i0] = d0;
-  out[i1] = d1;
+  const uint64_t q = c.q;
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << blkLog);
+  const uint64_t i0 = ((k * 2 * Ll) << logN) + off, i1 = (((k * 2 + 1) * Ll) << logN) + off;
+  const uint64_t id = (row << logN) + ((uint64_t)b << blkLog);
+  const ulonglong2* A0 = reinterpret_cast<const ulonglong2*>(x + i0);
+  const ulonglong2* A1 = reinterpret_cast<const ulonglong2*>(x + i1);
+  const ulonglong2* B0 = reinterpret_cast<const ulonglong2*>(y + i0);
+  const ulonglong2* B1 = reinterpret_cast<const ulonglong2*>(y + i1);
+  ulonglong2* O0 = reinterpret_cast<ulonglong2*>(out + i0);
+  ulonglong2* O1 = reinterpret_cast<ulonglong2*>(out + i1);
+  ulonglong2* E2 = reinterpret_cast<ulonglong2*>(d2e + id);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+    const ulonglong2 a0 = A0[p], a1 = A1[p], b0 = B0[p], b1 = B1[p];
+    const ulonglong2 r0 = make_ulonglong2(mulmod_generic(a0.x, b0.x, c), mulmod_generic(a0.y, b0.y, c));
+    const ulonglong2 r1 =
+        make_ulonglong2(addmod(mulmod_generic(a0.x, b1.x, c), mulmod_generic(a1.x, b0.x, c), q),
+                        addmod(mulmod_generic(a0.y, b1.y, c), mulmod_generic(a1.y, b0.y, c), q));
+    const ulonglong2 r2 = make_ulonglong2(mulmod_generic(a1.x, b1.x, c), mulmod_generic(a1.y, b1.y, c));
+    O0[p] = r0;
+    O1[p] = r1;
+    E2[p] = r2;
+    lds_put2(sm, p, r2);
+  }
+  __syncthreads();
+  ntt_inv_block_stages(sm, blkLog, b, logN, itw + (uint64_t)t * N, itwp + (uint64_t)t * N, q);
+  ulonglong2* D = reinterpret_cast<ulonglong2*>(d2c + id);
+  if (sh == 0) {
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+      const ulonglong2 v = lds_get2(sm, p);
+      D[p] = make_ulonglong2(canon4(shoup_lazy(v.x, c.ninv, c.ninv_shoup, q), q),
+                             canon4(shoup_lazy(v.y, c.ninv, c.ninv_shoup, q), q));
+    }
+  } else {  // lazy values in [0, 4q): the columns pass canonicalises
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) D[p] = lds_get2(sm, p);
+  }
 }
 
 // ----------------------------------------------------------------- ModUp ----
-// c [K][Ll][N] (COEFFICIENT) -> ext [dn][K][T][N] (COEFFICIENT): digit j's own towers
-// copied, every other tower of Q_l u P by the fast basis conversion.
+// c [K][Ll][N] (COEFFICIENT) -> digit j's foreign towers ext_j [K][T - cnt][N]
+// (COEFFICIENT) by the fast basis conversion.
 __global__ __launch_bounds__(256) void modup_kernel(const uint64_t* __restrict__ c, uint64_t K,
                                                     KsArgs a, uint64_t* __restrict__ ext) {
   const uint32_t N = 1u << a.logN, bpr = N >> 8;
@@ -67,59 +122,103 @@ __global__ __launch_bounds__(256) void modup_kernel(const uint64_t* __restrict__
   const uint32_t n = (blockIdx.x % bpr) * 256 + threadIdx.x;
   const uint32_t j = (uint32_t)(row / K);
   const uint64_t k = row % K;
-  const uint32_t s = j * a.alpha, cnt = min(a.alpha, a.Ll - s);
-  uint64_t x[kMaxTowers], yv[kMaxTowers];
+  uint32_t s, cnt;
+  digit_span(a, j, s, cnt);
+  uint64_t yv[kMaxTowers];
   for (uint32_t i = 0; i < cnt; ++i) {
     const TowerConst ci = a.tq[s + i];
-    x[i] = c[(k * a.Ll + s + i) * N + n];
-    yv[i] = shoup_mul(x[i], a.mu_inv[j * a.alpha + i], a.mu_inv_sh[j * a.alpha + i], ci.q);
+    yv[i] = shoup_mul(c[((k * a.Ll + s + i) << a.logN) + n], a.mu_inv[j * a.alpha + i],
+                      a.mu_inv_sh[j * a.alpha + i], ci.q);
   }
-  uint64_t* __restrict__ o = ext + row * a.T * N + n;
-  for (uint32_t t = 0; t < a.T; ++t) {
-    uint64_t v;
-    if (t >= s && t < s + cnt) {
-      v = x[t - s];
-    } else {
-      du128 acc = 0;
-      const uint64_t* __restrict__ h = a.mu_hat + (uint64_t)j * a.alpha * a.T + t;
-      for (uint32_t i = 0; i < cnt; ++i) acc += mul128(yv[i], h[(uint64_t)i * a.T]);
-      v = red128(acc, a.te[t]);
-    }
-    o[(uint64_t)t * N] = v;
+  const uint32_t Tf = a.T - cnt;
+  uint64_t* __restrict__ o = ext + ext_base(a, j, K) + ((k * Tf) << a.logN) + n;
+  for (uint32_t u = 0; u < Tf; ++u) {
+    const uint32_t t = u < s ? u : u + cnt;
+    du128 acc = 0;
+    const uint64_t* __restrict__ h = a.mu_hat + (uint64_t)j * a.alpha * a.T + t;
+    for (uint32_t i = 0; i < cnt; ++i) acc += mul128(yv[i], h[(uint64_t)i * a.T]);
+    o[(uint64_t)u << a.logN] = red128(acc, a.te[t]);
   }
 }
 
-// --------------------------------------------------------- inner product ----
-// ext [dn][K][T][N] (EVALUATION) x key [2][dnFull][Lfull + kP][N] -> accQ [K][2][Ll][N],
-// accP [K][2][kP][N]
-__global__ __launch_bounds__(256) void ks_inner_kernel(const uint64_t* __restrict__ ext, uint64_t K,
-                                                       KsArgs a, const uint64_t* __restrict__ evk,
-                                                       const uint64_t* __restrict__ evk_sh,
-                                                       uint64_t* __restrict__ accQ,
-                                                       uint64_t* __restrict__ accP) {
-  const uint32_t N = 1u << a.logN, bpr = N >> 8;
-  const uint64_t row = blockIdx.x / bpr;  // k * T + t
-  const uint32_t n = (blockIdx.x % bpr) * 256 + threadIdx.x;
+// ------------------------------------- last NTT pass + key inner product ----
+// One workgroup per (ct, tower t of Q_l u P, block): every digit j's block of tower t in
+// EVALUATION — straight from d2e when t is one of the digit's own towers, else the foreign
+// block after its last NTT stages in LDS slot j — is multiplied by the key (b_j, a_j) and
+// summed; (u0, u1) go to accQ / accP.  The extended polynomials never return to HBM in
+// EVALUATION form.  All digits' blocks sit in LDS together (dn x 16 KiB at 2^11 blocks), so
+// the products are formed in one pass with nothing held in registers across digits.
+__global__ __launch_bounds__(256) void ks_inner_blocks_kernel(const uint64_t* __restrict__ d2e,
+                                                              const uint64_t* __restrict__ ext, uint64_t K,
+                                                              KsArgs a, uint32_t blkLog,
+                                                              const uint64_t* __restrict__ tw,
+                                                              const uint64_t* __restrict__ twp,
+                                                              const uint64_t* __restrict__ evk,
+                                                              const uint64_t* __restrict__ evk_sh,
+                                                              uint64_t* __restrict__ accQ,
+                                                              uint64_t* __restrict__ accP) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << a.logN, blk = 1u << blkLog, sh = a.logN - blkLog;
+  const uint64_t row = blockIdx.x >> sh;  // k * T + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint64_t k = row / a.T;
   const uint32_t t = (uint32_t)(row % a.T);
   const TowerConst c = a.te[t];
+  const uint64_t q = c.q;
   const uint32_t TF = a.Lfull + a.kP;
   const uint32_t tk = t < a.Ll ? t : a.Lfull + (t - a.Ll);  // the key's tower
-  uint64_t u0 = 0, u1 = 0;
+  const uint64_t boff = (uint64_t)b << blkLog;
+  uint32_t own_mask = 0;
   for (uint32_t j = 0; j < a.dn; ++j) {
-    const uint64_t xv = ext[((uint64_t)j * K + k) * a.T * N + (uint64_t)t * N + n];
-    const uint64_t ib = ((uint64_t)j * TF + tk) * N + n;
-    const uint64_t ia = ((uint64_t)(a.dnFull + j) * TF + tk) * N + n;
-    u0 = addmod(u0, shoup_mul(xv, evk[ib], evk_sh[ib], c.q), c.q);
-    u1 = addmod(u1, shoup_mul(xv, evk[ia], evk_sh[ia], c.q), c.q);
+    uint32_t s, cnt;
+    digit_span(a, j, s, cnt);
+    if (t >= s && t < s + cnt) {
+      own_mask |= 1u << j;
+      continue;
+    }
+    const uint32_t u = t < s ? t : t - cnt;
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(
+        ext + ext_base(a, j, K) + ((k * (a.T - cnt) + u) << a.logN) + boff);
+    for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) lds_put2(sm + ((uint64_t)j << blkLog), p, src[p]);
   }
+  __syncthreads();
+  for (uint32_t j = 0; j < a.dn; ++j)
+    if (!(own_mask & (1u << j)))
+      ntt_fwd_block_stages(sm + ((uint64_t)j << blkLog), blkLog, b, a.logN, tw + (uint64_t)t * N,
+                           twp + (uint64_t)t * N, q);
+  const ulonglong2* own_src = reinterpret_cast<const ulonglong2*>(d2e + ((k * a.Ll + t) << a.logN) + boff);
+  ulonglong2 *o0, *o1;
   if (t < a.Ll) {
-    accQ[((k * 2 + 0) * a.Ll + t) * N + n] = u0;
-    accQ[((k * 2 + 1) * a.Ll + t) * N + n] = u1;
+    o0 = reinterpret_cast<ulonglong2*>(accQ + ((((k * 2 + 0) * a.Ll + t)) << a.logN) + boff);
+    o1 = reinterpret_cast<ulonglong2*>(accQ + ((((k * 2 + 1) * a.Ll + t)) << a.logN) + boff);
   } else {
     const uint32_t m = t - a.Ll;
-    accP[((k * 2 + 0) * a.kP + m) * N + n] = u0;
-    accP[((k * 2 + 1) * a.kP + m) * N + n] = u1;
+    o0 = reinterpret_cast<ulonglong2*>(accP + ((((k * 2 + 0) * a.kP + m)) << a.logN) + boff);
+    o1 = reinterpret_cast<ulonglong2*>(accP + ((((k * 2 + 1) * a.kP + m)) << a.logN) + boff);
+  }
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+    ulonglong2 u0 = make_ulonglong2(0, 0), u1 = make_ulonglong2(0, 0);
+    for (uint32_t j = 0; j < a.dn; ++j) {
+      ulonglong2 v;
+      if (own_mask & (1u << j)) {
+        v = own_src[p];
+      } else {
+        v = lds_get2(sm + ((uint64_t)j << blkLog), p);
+        v = make_ulonglong2(canon8(v.x, q), canon8(v.y, q));
+      }
+      const uint64_t kb = ((((uint64_t)j * TF + tk)) << a.logN) + boff + 2ull * p;
+      const uint64_t ka = ((((uint64_t)(a.dnFull + j) * TF + tk)) << a.logN) + boff + 2ull * p;
+      const ulonglong2 bv = *reinterpret_cast<const ulonglong2*>(evk + kb);
+      const ulonglong2 bs = *reinterpret_cast<const ulonglong2*>(evk_sh + kb);
+      const ulonglong2 av = *reinterpret_cast<const ulonglong2*>(evk + ka);
+      const ulonglong2 as = *reinterpret_cast<const ulonglong2*>(evk_sh + ka);
+      u0.x = addmod(u0.x, shoup_mul(v.x, bv.x, bs.x, q), q);
+      u0.y = addmod(u0.y, shoup_mul(v.y, bv.y, bs.y, q), q);
+      u1.x = addmod(u1.x, shoup_mul(v.x, av.x, as.x, q), q);
+      u1.y = addmod(u1.y, shoup_mul(v.y, av.y, as.y, q), q);
+    }
+    o0[p] = u0;
+    o1[p] = u1;
   }
 }
 
@@ -142,55 +241,96 @@ __global__ __launch_bounds__(256) void moddown_kernel(const uint64_t* __restrict
   }
 }
 
-// out[k][poly][t] += (accQ - z) P^-1 mod q_t   (all EVALUATION)
-__global__ __launch_bounds__(256) void ks_finish_kernel(const uint64_t* __restrict__ accQ,
-                                                        const uint64_t* __restrict__ z, KsArgs a,
-                                                        uint64_t* __restrict__ out) {
-  const uint32_t N = 1u << a.logN, bpr = N >> 8;
-  const uint64_t row = blockIdx.x / bpr;  // (k * 2 + poly) * Ll + t
-  const uint32_t n = (blockIdx.x % bpr) * 256 + threadIdx.x;
+// ------------------------------------- last NTT pass of z + the ModDown finish ----
+// out[k][poly][t] += (accQ - NTT(z)) P^-1 mod q_t, z's last stages in LDS
+__global__ __launch_bounds__(256) void ks_finish_blocks_kernel(const uint64_t* __restrict__ z,
+                                                               const uint64_t* __restrict__ accQ, KsArgs a,
+                                                               uint32_t blkLog, const uint64_t* __restrict__ tw,
+                                                               const uint64_t* __restrict__ twp,
+                                                               uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << a.logN, blk = 1u << blkLog, sh = a.logN - blkLog;
+  const uint64_t row = blockIdx.x >> sh;  // (k * 2 + poly) * Ll + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint32_t t = (uint32_t)(row % a.Ll);
   const TowerConst c = a.tq[t];
-  const uint64_t e = row * N + n;
-  const uint64_t d = submod(accQ[e], z[e], c.q);
-  out[e] = addmod(out[e], shoup_mul(d, a.pinv[t], a.pinv_sh[t], c.q), c.q);
+  const uint64_t q = c.q, pinv = a.pinv[t], pinv_sh = a.pinv_sh[t];
+  const uint64_t off = (row << a.logN) + ((uint64_t)b << blkLog);
+  const ulonglong2* Z = reinterpret_cast<const ulonglong2*>(z + off);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) lds_put2(sm, p, Z[p]);
+  __syncthreads();
+  ntt_fwd_block_stages(sm, blkLog, b, a.logN, tw + (uint64_t)t * N, twp + (uint64_t)t * N, q);
+  const ulonglong2* AQ = reinterpret_cast<const ulonglong2*>(accQ + off);
+  ulonglong2* O = reinterpret_cast<ulonglong2*>(out + off);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+    const ulonglong2 v = lds_get2(sm, p), aq = AQ[p], o = O[p];
+    const uint64_t dx = submod(aq.x, canon8(v.x, q), q), dy = submod(aq.y, canon8(v.y, q), q);
+    O[p] = make_ulonglong2(addmod(o.x, shoup_mul(dx, pinv, pinv_sh, q), q),
+                           addmod(o.y, shoup_mul(dy, pinv, pinv_sh, q), q));
+  }
 }
 
-size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t N, uint64_t K) {
+size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t alpha, uint32_t N, uint64_t K) {
   const uint64_t T = Ll + kP;
-  // [d2 | ext] (z reuses it: Ll + dn T >= 2 Ll) | accQ | accP
-  return K * (uint64_t)N * 8 * (Ll + dn * T + 2ull * Ll + 2ull * kP) + 64;
+  uint64_t ext = 0;
+  for (uint32_t j = 0; j < dn; ++j) ext += T - std::min(alpha, Ll - j * alpha);
+  // d2e | d2c | ext | accQ | accP | z
+  return K * (uint64_t)N * 8 * (2ull * Ll + ext + 2ull * Ll + 2ull * kP + 2ull * Ll) + 64;
 }
 
 void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTables& dte,
-                      const uint64_t* evk, const uint64_t* evk_sh, const uint64_t* x, const uint64_t* y,
-                      uint64_t K, uint64_t* out, void* scratch, hipStream_t s) {
+                      const DeviceTables* dtf, const uint64_t* evk, const uint64_t* evk_sh, const uint64_t* x,
+                      const uint64_t* y, uint64_t K, uint64_t* out, void* scratch, hipStream_t s) {
   if (!K) return;
   const uint32_t N = 1u << a.logN, bpr = N >> 8;
+  const uint32_t blkLog = ntt_block_log(a.logN), sh = a.logN - blkLog;
+  const size_t lds = sizeof(uint64_t) << blkLog;
   const uint64_t KN = K * N;
-  uint64_t* d2 = reinterpret_cast<uint64_t*>(scratch);
-  uint64_t* ext = d2 + KN * a.Ll;
-  uint64_t* accQ = ext + KN * a.dn * a.T;
+  uint64_t* d2e = reinterpret_cast<uint64_t*>(scratch);
+  uint64_t* d2c = d2e + KN * a.Ll;
+  uint64_t* ext = d2c + KN * a.Ll;
+  uint64_t next = 0;
+  for (uint32_t j = 0; j < a.dn; ++j) next += a.T - std::min(a.alpha, a.Ll - j * a.alpha);
+  uint64_t* accQ = ext + KN * next;
   uint64_t* accP = accQ + KN * 2 * a.Ll;
-  uint64_t* z = d2;
-  auto grid = [&](uint64_t rows) {
-    const uint64_t b = rows * bpr;
+  uint64_t* z = accP + KN * 2 * a.kP;
+  auto grid = [&](uint64_t rows, uint32_t per_row) {
+    const uint64_t b = rows * per_row;
     if (b > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "EvalMult batch too large"};
     return dim3((uint32_t)b);
   };
-  hipLaunchKernelGGL(tensor_kernel, grid(K * a.Ll), dim3(256), 0, s, x, y, a.Ll, a.logN, a.tq, out, d2);
+  const uint32_t nb = 1u << sh;
+  // tensor -> c0, c1 (out), c2 (EVALUATION) + first INTT pass; then the INTT columns pass
+  hipLaunchKernelGGL(ks_tensor_intt_kernel, grid(K * a.Ll, nb), dim3(256), lds, s, x, y, a.Ll, a.logN, blkLog,
+                     dtq.ipsi_rev, dtq.ipsi_rev_sh, a.tq, out, d2e, d2c);
   SHELFI_HIP(hipGetLastError());
-  launch_ntt(d2, K * a.Ll, a.Ll, a.logN, true, dtq, s);  // c2 -> COEFFICIENT
-  hipLaunchKernelGGL(modup_kernel, grid((uint64_t)a.dn * K), dim3(256), 0, s, d2, K, a, ext);
+  launch_ntt_cols(d2c, K * a.Ll, a.Ll, a.logN, true, dtq, s);
+  // ModUp of every digit's foreign towers, their first NTT stages per digit
+  hipLaunchKernelGGL(modup_kernel, grid((uint64_t)a.dn * K, bpr), dim3(256), 0, s, d2c, K, a, ext);
   SHELFI_HIP(hipGetLastError());
-  launch_ntt(ext, (uint64_t)a.dn * K * a.T, a.T, a.logN, false, dte, s);
-  hipLaunchKernelGGL(ks_inner_kernel, grid(K * a.T), dim3(256), 0, s, ext, K, a, evk, evk_sh, accQ, accP);
+  {
+    uint64_t* e = ext;
+    for (uint32_t j = 0; j < a.dn; ++j) {
+      const uint32_t Tf = a.T - std::min(a.alpha, a.Ll - j * a.alpha);
+      launch_ntt_cols(e, K * Tf, Tf, a.logN, false, dtf[j], s);
+      e += KN * Tf;
+    }
+  }
+  // last NTT stages + the key inner product (one LDS block per digit; > 64 KiB only for
+  // 2^12-element blocks with 3 digits, which a gfx950 workgroup may still declare)
+  if (lds * a.dn > 65536)
+    SHELFI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ks_inner_blocks_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds * a.dn)));
+  hipLaunchKernelGGL(ks_inner_blocks_kernel, grid(K * a.T, nb), dim3(256), lds * a.dn, s, d2e, ext, K, a, blkLog,
+                     dte.psi_rev, dte.psi_rev_sh, evk, evk_sh, accQ, accP);
   SHELFI_HIP(hipGetLastError());
+  // ModDown: INTT of the P part, P -> Q_l conversion, its NTT fused with the finish
   launch_ntt(accP, K * 2 * a.kP, a.kP, a.logN, true, tower_view(dte, a.Ll, N), s);
-  hipLaunchKernelGGL(moddown_kernel, grid(K * 2), dim3(256), 0, s, accP, a, z);
+  hipLaunchKernelGGL(moddown_kernel, grid(K * 2, bpr), dim3(256), 0, s, accP, a, z);
   SHELFI_HIP(hipGetLastError());
-  launch_ntt(z, K * 2 * a.Ll, a.Ll, a.logN, false, dtq, s);
-  hipLaunchKernelGGL(ks_finish_kernel, grid(K * 2 * a.Ll), dim3(256), 0, s, accQ, z, a, out);
+  launch_ntt_cols(z, K * 2 * a.Ll, a.Ll, a.logN, false, dtq, s);
+  hipLaunchKernelGGL(ks_finish_blocks_kernel, grid(K * 2 * a.Ll, nb), dim3(256), lds, s, z, accQ, a, blkLog,
+                     dtq.psi_rev, dtq.psi_rev_sh, out);
   SHELFI_HIP(hipGetLastError());
 }
 
@@ -216,18 +356,33 @@ __global__ __launch_bounds__(256) void rescale_lift_kernel(const uint64_t* __res
   v[row * N + n] = r;
 }
 
-__global__ __launch_bounds__(256) void rescale_finish_kernel(const uint64_t* __restrict__ in,
-                                                             const uint64_t* __restrict__ v, uint32_t Lo,
-                                                             uint32_t logN, const TowerConst* __restrict__ tq,
-                                                             RescaleConst rc, uint64_t* __restrict__ out) {
-  const uint32_t N = 1u << logN, bpr = N >> 8;
-  const uint64_t row = blockIdx.x / bpr;  // (k * 2 + poly) * Lo + t
-  const uint32_t n = (blockIdx.x % bpr) * 256 + threadIdx.x;
+// v's last NTT stages in LDS, then out = (in - v) q_l^-1 mod q_t
+__global__ __launch_bounds__(256) void rescale_finish_blocks_kernel(const uint64_t* __restrict__ in,
+                                                                    const uint64_t* __restrict__ v, uint32_t Lo,
+                                                                    uint32_t logN, uint32_t blkLog,
+                                                                    const uint64_t* __restrict__ tw,
+                                                                    const uint64_t* __restrict__ twp,
+                                                                    const TowerConst* __restrict__ tq,
+                                                                    RescaleConst rc, uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  const uint32_t N = 1u << logN, blk = 1u << blkLog, sh = logN - blkLog;
+  const uint64_t row = blockIdx.x >> sh;  // (k * 2 + poly) * Lo + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint64_t kp = row / Lo;
   const uint32_t t = (uint32_t)(row % Lo);
-  const TowerConst c = tq[t];
-  const uint64_t xin = in[(kp * (Lo + 1) + t) * N + n];
-  out[row * N + n] = shoup_mul(submod(xin, v[row * N + n], c.q), rc.qlinv[t], rc.qlinv_sh[t], c.q);
+  const uint64_t q = tq[t].q, w = rc.qlinv[t], wp = rc.qlinv_sh[t];
+  const uint64_t boff = (uint64_t)b << blkLog;
+  const ulonglong2* V = reinterpret_cast<const ulonglong2*>(v + (row << logN) + boff);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) lds_put2(sm, p, V[p]);
+  __syncthreads();
+  ntt_fwd_block_stages(sm, blkLog, b, logN, tw + (uint64_t)t * N, twp + (uint64_t)t * N, q);
+  const ulonglong2* X = reinterpret_cast<const ulonglong2*>(in + ((kp * (Lo + 1) + t) << logN) + boff);
+  ulonglong2* O = reinterpret_cast<ulonglong2*>(out + (row << logN) + boff);
+  for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
+    const ulonglong2 y = lds_get2(sm, p), x = X[p];
+    O[p] = make_ulonglong2(shoup_mul(submod(x.x, canon8(y.x, q), q), w, wp, q),
+                           shoup_mul(submod(x.y, canon8(y.y, q), q), w, wp, q));
+  }
 }
 
 size_t rescale_scratch_bytes(uint32_t Ll, uint32_t N, uint64_t K) {
@@ -249,9 +404,11 @@ void launch_rescale(const DeviceTables& dt, uint32_t Ll, uint32_t logN, const Re
   hipLaunchKernelGGL(rescale_lift_kernel, dim3((uint32_t)(rows * bpr)), dim3(256), 0, s, last, Lo, logN, rc.ql,
                      dt.tc, v);
   SHELFI_HIP(hipGetLastError());
-  launch_ntt(v, rows, Lo, logN, false, dt, s);
-  hipLaunchKernelGGL(rescale_finish_kernel, dim3((uint32_t)(rows * bpr)), dim3(256), 0, s, in, v, Lo, logN,
-                     dt.tc, rc, out);
+  launch_ntt_cols(v, rows, Lo, logN, false, dt, s);
+  const uint32_t blkLog = ntt_block_log(logN);
+  hipLaunchKernelGGL(rescale_finish_blocks_kernel, dim3((uint32_t)(rows << (logN - blkLog))), dim3(256),
+                     sizeof(uint64_t) << blkLog, s, in, v, Lo, logN, blkLog, dt.psi_rev, dt.psi_rev_sh, dt.tc, rc,
+                     out);
   SHELFI_HIP(hipGetLastError());
 }
 

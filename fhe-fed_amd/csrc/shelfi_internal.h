@@ -217,6 +217,8 @@ void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const 
                  hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                 const DeviceTables& dt, hipStream_t s);
+void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
+                     const DeviceTables& dt, hipStream_t s);
 void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const double* x, uint64_t n, uint64_t K, uint64_t* ct, void* scratch,
                     const uint32_t key[8], uint64_t g0, uint32_t* flag, hipStream_t s);
@@ -266,11 +268,12 @@ struct KsArgs {
   const TowerConst* te;       // towers of Q_l u P (extended tables)
 };
 // out = relinearized (a x b): tensor, ModUp per digit, inner product with the key,
-// ModDown.  a, b, out [K][2][Ll][N]; scratch = ks_scratch_bytes(.., K).
-size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t N, uint64_t K);
+// ModDown.  a, b, out [K][2][Ll][N] (out may alias a or b); scratch = ks_scratch_bytes(.., K).
+// dtq: tables of Q (prefix Q_l used); dte: Q_l u P; dtf[j]: digit j's foreign towers.
+size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t alpha, uint32_t N, uint64_t K);
 void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTables& dte,
-                      const uint64_t* evk, const uint64_t* evk_sh, const uint64_t* x, const uint64_t* y,
-                      uint64_t K, uint64_t* out, void* scratch, hipStream_t s);
+                      const DeviceTables* dtf, const uint64_t* evk, const uint64_t* evk_sh, const uint64_t* x,
+                      const uint64_t* y, uint64_t K, uint64_t* out, void* scratch, hipStream_t s);
 // ModReduce: in [K][2][Ll][N] -> out [K][2][Ll-1][N] (EVAL); qlinv[t] = q_{Ll-1}^-1 mod q_t
 struct RescaleConst {
   uint64_t ql;  // the dropped modulus q_{Ll-1}
