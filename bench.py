@@ -88,6 +88,12 @@ def parse():
     ap.add_argument("--api-cts", type=int, default=64,
                     help="ciphertexts per learner for the bytes-API (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
+    ap.add_argument("--f4-cts", type=int, default=256,
+                    help="ciphertext pairs for the §8 f4 sample (EvalMult + relinearization, ModReduce; "
+                         "rank 0, 2^15/L4 workloads); 0 = skip")
+    ap.add_argument("--f4-counters-json", default=os.path.join(ROOT, "profiles", "r02_f4_counters.json"),
+                    help="PMC VALU instructions and HBM bytes per ciphertext of one EvalMult / ModReduce "
+                         "(tools/profile_f4.sh)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
                     help="PMC-derived HBM bytes per wavg launch (from tools/pmc_traffic.py)")
     ap.add_argument("--encdec-traffic-json", default=os.path.join(ROOT, "profiles", "encdec_traffic.json"),
@@ -522,6 +528,56 @@ def main():
 
     enc_steady_ms = time_encrypt()
 
+    # §8 f4 (not on the aggregation path): EvalMult with HYBRID relinearization and ModReduce
+    # of fresh ciphertexts, device-resident, median of 5 calls each; a decrypt checks x*y
+    f4 = None
+    if args.f4_cts > 0 and rank == 0 and L >= 2 and L + 2 <= 16:
+        Kf = args.f4_cts
+        ck.evalMultKeyGen()
+        ck.set_decode_noise(False)
+        xf = torch.rand(Kf * batch, device=dev, dtype=torch.float64) * 2 - 1
+        yf = torch.rand(Kf * batch, device=dev, dtype=torch.float64) * 2 - 1
+        fa, fb = D.encrypt(ck, xf), D.encrypt(ck, yf)
+        fp = torch.empty_like(fa)
+        fr = torch.empty((Kf, 2, L - 1, N), dtype=fa.dtype, device=dev)
+        D.mult(ck, fa, fb, out=fp)
+        D.rescale(ck, fp, out=fr)
+        torch.cuda.synchronize()
+
+        def med(fn):
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            return sorted(ts)[2] * 1e6 / Kf
+
+        mult_us = med(lambda: D.mult(ck, fa, fb, out=fp))
+        res_us = med(lambda: D.rescale(ck, fp, out=fr))
+        s1 = delta * delta / float(q[-1])
+        nchk = 4 * batch
+        got = D.decrypt(ck, fr[:4].contiguous(), nchk, s1)
+        err = (got - xf[:nchk] * yf[:nchk]).abs().max().item()
+        f4 = {"what": "EvalMult (tensor + HYBRID relinearization) and ModReduce, device-resident",
+              "ciphertexts": Kf, "eval_mult_us_per_ct": round(mult_us, 3),
+              "mod_reduce_us_per_ct": round(res_us, 3), "decrypt_max_abs_err_vs_xy": err}
+        try:
+            with open(args.f4_counters_json) as f:
+                fc = json.load(f)
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            peak = simds * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST
+            if args.workload in ("cfg3", "cfg2", "cfg5"):
+                for name, key, us in (("eval_mult", "mult", mult_us), ("mod_reduce", "rescale", res_us)):
+                    wi, hb = fc[key]["SQ_INSTS_VALU"], fc[key]["hbm_bytes"]
+                    f4[name + "_valu_frac"] = round(wi / (us * 1e-6) / 1e9 / peak, 3)
+                    f4[name + "_hbm_frac"] = round(hb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3)
+                f4["counters_source"] = os.path.relpath(args.f4_counters_json, ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
+        del xf, yf, fa, fb, fp, fr, got
+        torch.cuda.empty_cache()
+
     # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`
     api = None
     if args.api_cts > 0 and rank == 0:
@@ -662,6 +718,8 @@ def main():
         res["c_abi_comm_check"] = comm_check
     if api:
         res["api_bytes_path"] = api
+    if f4:
+        res["f4_eval_mult"] = f4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, L, q, psi, delta, batch, Cl, args.cpu_seconds)
     if rank == 0:
