@@ -31,6 +31,17 @@ namespace shelfi {
 
 typedef unsigned __int128 du128;
 
+#define NTT_DISPATCH_KS(LOGRV, KERNEL, ...)                                               \
+  switch (LOGRV) {                                                                       \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                           \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                           \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                           \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                           \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break;                           \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                           \
+    default: throw Error{SHELFI_ERR_ARG, "EvalMult: unsupported ring dimension"};        \
+  }
+
 // sum of products (< 2^124) -> [0, q)
 __device__ __forceinline__ uint64_t red128(du128 acc, const TowerConst& c) {
   const uint64_t hi = (uint64_t)(acc >> 64), lo = (uint64_t)acc;
@@ -138,6 +149,126 @@ __global__ __launch_bounds__(256) void modup_kernel(const uint64_t* __restrict__
     const uint64_t* __restrict__ h = a.mu_hat + (uint64_t)j * a.alpha * a.T + t;
     for (uint32_t i = 0; i < cnt; ++i) acc += mul128(yv[i], h[(uint64_t)i * a.T]);
     o[(uint64_t)u << a.logN] = red128(acc, a.te[t]);
+  }
+}
+
+// ModUp fused with the first NTT stages (rings with a columns pass): one thread per
+// (digit, ct, column of R = 2^LOGR rows).  It converts its R coefficients of the digit's
+// towers once (y_i = [c_i (Q_j/q_i)^-1]_{q_i}, kept in registers), then for every foreign
+// tower forms the column by the basis conversion, runs the LOGR register stages with that
+// tower's twiddles and writes the lazy column — the coefficient-domain extension never
+// round-trips through HBM.  (Recomputing y per tower instead, to drop to 97 VGPRs / 4 waves,
+// measured slower: 11.7 vs 11.0 us per product at 2^15/L4.)
+template <int LOGR>
+__global__ __launch_bounds__(256) void modup_cols_kernel(const uint64_t* __restrict__ c, uint64_t K, KsArgs a,
+                                                         const uint64_t* __restrict__ tw,
+                                                         const uint64_t* __restrict__ twp,
+                                                         uint64_t* __restrict__ ext) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t N = 1u << a.logN, BLK = N >> LOGR, bpp = BLK / 256;
+  const uint64_t row = blockIdx.x / bpp;  // j * K + k
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  const uint32_t j = (uint32_t)(row / K);
+  const uint64_t k = row % K;
+  uint32_t s, cnt;
+  digit_span(a, j, s, cnt);
+  // the digit's converted coefficients, [i][r] (cnt <= 2 here: launch_eval_mult checks)
+  uint64_t y[2][R];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if ((uint32_t)i < cnt) {
+      const TowerConst ci = a.tq[s + i];
+      const uint64_t w = a.mu_inv[j * a.alpha + i], wp = a.mu_inv_sh[j * a.alpha + i];
+      const uint64_t* __restrict__ src = c + ((k * a.Ll + s + i) << a.logN) + col;
+#pragma unroll
+      for (int r = 0; r < R; ++r) y[i][r] = shoup_mul(src[(uint64_t)r * BLK], w, wp, ci.q);
+    }
+  }
+  const uint32_t Tf = a.T - cnt;
+  uint64_t* __restrict__ o = ext + ext_base(a, j, K) + ((k * Tf) << a.logN) + col;
+  for (uint32_t u = 0; u < Tf; ++u) {
+    const uint32_t t = u < s ? u : u + cnt;
+    const TowerConst ct = a.te[t];
+    const uint64_t h0 = a.mu_hat[(uint64_t)j * a.alpha * a.T + t];
+    const uint64_t h1 = cnt > 1 ? a.mu_hat[((uint64_t)j * a.alpha + 1) * a.T + t] : 0;
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      du128 acc = mul128(y[0][r], h0);
+      if (cnt > 1) acc += mul128(y[1][r], h1);
+      x[r] = red128(acc, ct);
+    }
+    const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+    const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+#pragma unroll
+    for (int st = 0; st < LOGR; ++st) {
+      const int m = 1 << st, tr = R >> (st + 1);
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        const uint64_t W = w[m + i], Wp = wp[m + i];
+#pragma unroll
+        for (int jj = 0; jj < tr; ++jj) {
+          const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+          ct_bfly(x[r0], x[r1], W, Wp, ct.q);
+        }
+      }
+    }
+    uint64_t* __restrict__ ou = o + ((uint64_t)u << a.logN);
+#pragma unroll
+    for (int r = 0; r < R; ++r) ou[(uint64_t)r * BLK] = x[r];
+  }
+}
+
+// ModDown's P -> Q_l conversion fused with z's first NTT stages: one thread per (ct, poly,
+// column), y_m of the special towers in registers (kP <= 2 here), then per target tower the
+// conversion, the LOGR register stages and the lazy write.
+template <int LOGR>
+__global__ __launch_bounds__(256) void moddown_cols_kernel(const uint64_t* __restrict__ accP, KsArgs a,
+                                                           const uint64_t* __restrict__ tw,
+                                                           const uint64_t* __restrict__ twp,
+                                                           uint64_t* __restrict__ z) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t N = 1u << a.logN, BLK = N >> LOGR, bpp = BLK / 256;
+  const uint64_t row = blockIdx.x / bpp;  // k * 2 + poly
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  uint64_t y[2][R];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    if ((uint32_t)m < a.kP) {
+      const TowerConst cp = a.te[a.Ll + m];
+      const uint64_t* __restrict__ src = accP + ((row * a.kP + m) << a.logN) + col;
+#pragma unroll
+      for (int r = 0; r < R; ++r) y[m][r] = shoup_mul(src[(uint64_t)r * BLK], a.md_inv[m], a.md_inv_sh[m], cp.q);
+    }
+  }
+  for (uint32_t t = 0; t < a.Ll; ++t) {
+    const TowerConst ct = a.tq[t];
+    const uint64_t h0 = a.md_hat[t], h1 = a.kP > 1 ? a.md_hat[(uint64_t)a.Ll + t] : 0;
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      du128 acc = mul128(y[0][r], h0);
+      if (a.kP > 1) acc += mul128(y[1][r], h1);
+      x[r] = red128(acc, ct);
+    }
+    const uint64_t* __restrict__ w = tw + (uint64_t)t * N;
+    const uint64_t* __restrict__ wp = twp + (uint64_t)t * N;
+#pragma unroll
+    for (int st = 0; st < LOGR; ++st) {
+      const int m = 1 << st, tr = R >> (st + 1);
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        const uint64_t W = w[m + i], Wp = wp[m + i];
+#pragma unroll
+        for (int jj = 0; jj < tr; ++jj) {
+          const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+          ct_bfly(x[r0], x[r1], W, Wp, ct.q);
+        }
+      }
+    }
+    uint64_t* __restrict__ ot = z + ((row * a.Ll + t) << a.logN) + col;
+#pragma unroll
+    for (int r = 0; r < R; ++r) ot[(uint64_t)r * BLK] = x[r];
   }
 }
 
@@ -305,17 +436,25 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
                      dtq.ipsi_rev, dtq.ipsi_rev_sh, a.tq, out, d2e, d2c);
   SHELFI_HIP(hipGetLastError());
   launch_ntt_cols(d2c, K * a.Ll, a.Ll, a.logN, true, dtq, s);
-  // ModUp of every digit's foreign towers, their first NTT stages per digit
-  hipLaunchKernelGGL(modup_kernel, grid((uint64_t)a.dn * K, bpr), dim3(256), 0, s, d2c, K, a, ext);
-  SHELFI_HIP(hipGetLastError());
-  {
+  // ModUp of every digit's foreign towers with their first NTT stages (fused when the ring has
+  // a columns pass and digits / special primes have <= 2 towers; else ModUp, then the blocks pass
+  // runs the whole transform)
+  const int logR = (int)sh;
+  const bool fuse_cols = logR > 0 && logR <= 4 && a.alpha <= 2 && a.kP <= 2;  // 2^32+ registers past 4
+  if (fuse_cols) {
+    const uint64_t rows = (uint64_t)a.dn * K, per = (N >> logR) / 256;
+    NTT_DISPATCH_KS(logR, modup_cols_kernel, grid(rows, (uint32_t)per), dim3(256), 0, s, d2c, K, a, dte.psi_rev,
+                    dte.psi_rev_sh, ext);
+  } else {
+    hipLaunchKernelGGL(modup_kernel, grid((uint64_t)a.dn * K, bpr), dim3(256), 0, s, d2c, K, a, ext);
     uint64_t* e = ext;
-    for (uint32_t j = 0; j < a.dn; ++j) {
+    for (uint32_t j = 0; j < a.dn && logR > 0; ++j) {
       const uint32_t Tf = a.T - std::min(a.alpha, a.Ll - j * a.alpha);
       launch_ntt_cols(e, K * Tf, Tf, a.logN, false, dtf[j], s);
       e += KN * Tf;
     }
   }
+  SHELFI_HIP(hipGetLastError());
   // last NTT stages + the key inner product (one LDS block per digit; > 64 KiB only for
   // 2^12-element blocks with 3 digits, which a gfx950 workgroup may still declare)
   if (lds * a.dn > 65536)
@@ -326,9 +465,15 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
   SHELFI_HIP(hipGetLastError());
   // ModDown: INTT of the P part, P -> Q_l conversion, its NTT fused with the finish
   launch_ntt(accP, K * 2 * a.kP, a.kP, a.logN, true, tower_view(dte, a.Ll, N), s);
-  hipLaunchKernelGGL(moddown_kernel, grid(K * 2, bpr), dim3(256), 0, s, accP, a, z);
+  if (fuse_cols) {
+    NTT_DISPATCH_KS(logR, moddown_cols_kernel, grid(K * 2, (uint32_t)((N >> logR) / 256)), dim3(256), 0, s, accP, a,
+                    dtq.psi_rev, dtq.psi_rev_sh, z);
+  } else {
+    hipLaunchKernelGGL(moddown_kernel, grid(K * 2, bpr), dim3(256), 0, s, accP, a, z);
+    SHELFI_HIP(hipGetLastError());
+    launch_ntt_cols(z, K * 2 * a.Ll, a.Ll, a.logN, false, dtq, s);
+  }
   SHELFI_HIP(hipGetLastError());
-  launch_ntt_cols(z, K * 2 * a.Ll, a.Ll, a.logN, false, dtq, s);
   hipLaunchKernelGGL(ks_finish_blocks_kernel, grid(K * 2 * a.Ll, nb), dim3(256), lds, s, z, accQ, a, blkLog,
                      dtq.psi_rev, dtq.psi_rev_sh, out);
   SHELFI_HIP(hipGetLastError());
