@@ -440,7 +440,8 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
   // a columns pass and digits / special primes have <= 2 towers; else ModUp, then the blocks pass
   // runs the whole transform)
   const int logR = (int)sh;
-  const bool fuse_cols = logR > 0 && logR <= 4 && a.alpha <= 2 && a.kP <= 2;  // 2^32+ registers past 4
+  // (LOGR 5 would hold 2 x 32 converted rows + 32 lanes: 256 VGPRs, 1 wave/SIMD; unfused there)
+  const bool fuse_cols = logR > 0 && logR <= 4 && a.alpha <= 2 && a.kP <= 2;
   if (fuse_cols) {
     const uint64_t rows = (uint64_t)a.dn * K, per = (N >> logR) / 256;
     NTT_DISPATCH_KS(logR, modup_cols_kernel, grid(rows, (uint32_t)per), dim3(256), 0, s, d2c, K, a, dte.psi_rev,
