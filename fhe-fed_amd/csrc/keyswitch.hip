@@ -436,9 +436,9 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
                      dtq.ipsi_rev, dtq.ipsi_rev_sh, a.tq, out, d2e, d2c);
   SHELFI_HIP(hipGetLastError());
   launch_ntt_cols(d2c, K * a.Ll, a.Ll, a.logN, true, dtq, s);
-  // ModUp of every digit's foreign towers with their first NTT stages (fused when the ring has
-  // a columns pass and digits / special primes have <= 2 towers; else ModUp, then the blocks pass
-  // runs the whole transform)
+  // ModUp of every digit's foreign towers with their first NTT stages: fused when the ring has
+  // a columns pass and digits / special primes have <= 2 towers; else modup_kernel, then a
+  // columns pass per digit (none for a single-block ring, whose blocks pass runs every stage)
   const int logR = (int)sh;
   // (LOGR 5 would hold 2 x 32 converted rows + 32 lanes: 256 VGPRs, 1 wave/SIMD; unfused there)
   const bool fuse_cols = logR > 0 && logR <= 4 && a.alpha <= 2 && a.kP <= 2;
