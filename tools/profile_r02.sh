@@ -11,7 +11,7 @@ mkdir -p "$out"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o "$tag" \
   -- /usr/bin/python3 bench.py > "$out/${tag}_bench.json" 2> "$out/${tag}_bench.err"
 python3 tools/kstat_summary.py "$out/${tag}_kernel_stats.csv" > "$out/${tag}_kernel_summary.txt"
-B="--steps 2 --warmup 1 --no-cpu-baseline --api-cts 0 --no-check --place-output 0"
+B="--steps 2 --warmup 1 --no-cpu-baseline --api-cts 0 --no-check --place-output 0 --f4-cts 0"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out" -o wfetch \
   -- /usr/bin/python3 bench.py $B > /dev/null 2> "$out/wfetch.err"
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out" -o wwrite \
