@@ -219,6 +219,17 @@ class CKKS(Scheme):
         check(self._lib.shelfi_get_eval_key(self._ctx, out.ctypes.data_as(_lib.u64p)), "get_eval_key")
         return out
 
+    def saveEvalMultKey(self, path: str | None = None) -> None:
+        """Write the evaluation key as a PALISADE key-eval-mult.txt (default: in cryptodir)."""
+        path = os.path.join(self.cryptodir, "key-eval-mult.txt") if path is None else path
+        check(self._lib.shelfi_save_eval_key(self._ctx, path.encode()), "saveEvalMultKey")
+
+    def loadEvalMultKey(self, path: str | None = None) -> None:
+        """Load a PALISADE key-eval-mult.txt made for these keys (loadCryptoParams already
+        picks up a matching one in cryptodir)."""
+        path = os.path.join(self.cryptodir, "key-eval-mult.txt") if path is None else path
+        check(self._lib.shelfi_load_eval_key(self._ctx, path.encode()), "loadEvalMultKey")
+
     def set_eval_key(self, evk: np.ndarray) -> None:
         evk = np.ascontiguousarray(evk, dtype=np.uint64)
         if evk.size != self._lib.shelfi_eval_key_words(self._ctx):
@@ -433,6 +444,36 @@ def palisade_key_context(key_public: bytes):
     tag = C.create_string_buffer(257)
     check(lib.shelfi_palisade_key_context(b, len(b), C.byref(out), C.byref(n), tag), "palisade_key_context")
     return _take_lib_bytes(lib, out, n.value), tag.value.decode()
+
+
+def palisade_evalkey_parse(evk_file: bytes, polys: bool = True):
+    """Parse a PALISADE key-eval-mult.txt (§8 f4) -> (info dict, [2][dnum][T][N] uint64 or None):
+    T = the context's towers followed by the special primes."""
+    lib = _lib.load()
+    b = bytes(evk_file)
+    inf = _lib.EvalKeyInfo()
+    check(lib.shelfi_palisade_evalkey_parse(b, len(b), C.byref(inf), None), "palisade_evalkey_parse")
+    T = inf.num_towers
+    d = {"ring_dim": inf.ring_dim, "num_towers": T, "ctx_towers": inf.ctx_towers, "dnum": inf.dnum,
+         "moduli": [int(inf.moduli[t]) for t in range(T)], "roots": [int(inf.roots[t]) for t in range(T)],
+         "keytag": inf.keytag.decode()}
+    if not polys:
+        return d, None
+    r = np.empty((2, inf.dnum, T, inf.ring_dim), np.uint64)
+    check(lib.shelfi_palisade_evalkey_parse(b, len(b), C.byref(inf), r.ctypes.data_as(_lib.u64p)),
+          "palisade_evalkey_parse")
+    return d, r
+
+
+def palisade_evalkey_rewrite(evk_file: bytes, polys: np.ndarray) -> bytes:
+    """The same key-eval-mult.txt re-serialized around `polys` ([2][dnum][T][N])."""
+    lib = _lib.load()
+    b = bytes(evk_file)
+    pp = np.ascontiguousarray(polys, dtype=np.uint64)
+    out, n = _lib.u8p(), C.c_size_t()
+    check(lib.shelfi_palisade_evalkey_rewrite(b, len(b), pp.ctypes.data_as(_lib.u64p), C.byref(out), C.byref(n)),
+          "palisade_evalkey_rewrite")
+    return _take_lib_bytes(lib, out, n.value)
 
 
 def palisade_embed_context(ctxfile: bytes) -> bytes:

@@ -46,6 +46,13 @@ class Info(C.Structure):
     ]
 
 
+class EvalKeyInfo(C.Structure):
+    """shelfi_palisade_evk_info (include/shelfi.h)."""
+    _fields_ = [("ring_dim", C.c_uint32), ("num_towers", C.c_uint32), ("ctx_towers", C.c_uint32),
+                ("dnum", C.c_uint32), ("moduli", C.c_uint64 * 16), ("roots", C.c_uint64 * 16),
+                ("keytag", C.c_char * 257)]
+
+
 class PalisadeInfo(C.Structure):
     _fields_ = [
         ("ring_dim", C.c_uint32),
@@ -144,6 +151,11 @@ SIGNATURES = {
     "shelfi_dev_rescale": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt_level": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_double,
                                            C.c_size_t, C.c_void_p, C.c_void_p]),
+    "shelfi_save_eval_key": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "shelfi_load_eval_key": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "shelfi_palisade_evalkey_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.c_void_p, u64p]),
+    "shelfi_palisade_evalkey_rewrite": (C.c_int, [C.c_char_p, C.c_size_t, u64p, C.POINTER(u8p),
+                                                  C.POINTER(C.c_size_t)]),
     "shelfi_fft_twiddles": (C.c_int, [C.c_uint32, f64p, f64p, f64p, f64p]),
     "shelfi_gauss_cdt": (C.c_int, [C.c_double, u64p, C.c_int]),
 }

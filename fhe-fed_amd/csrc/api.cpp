@@ -750,6 +750,7 @@ int shelfi_load(shelfi_ctx* ctx, const char* cryptodir) {
       install_keys(ctx, pk.data(), sk.data(), true);
       ctx->pal_ctx_obj = std::move(ctx_obj);
       ctx->pal_keytag = std::move(keytag);
+      load_evalkey_if_present(ctx, dir);  // §8 f4: a key-eval-mult.txt of these keys
     }
   });
 }

@@ -7,8 +7,11 @@
 // precomputes constants and moves keys; every per-ciphertext step is in keyswitch.hip.
 #include <algorithm>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 
 #include "api_util.h"
+#include "palisade_codec.h"
 #include "shelfi_internal.h"
 
 namespace shelfi {
@@ -211,6 +214,75 @@ static void install_evk(shelfi_ctx* ctx, EvalState& ev, const uint64_t* evk) {
   ev.evk_sh = upload(sh.data(), words);
 }
 
+// key-eval-mult.txt metadata of this context's evaluation key (PALISADE keys required: the
+// file embeds the context object and key tag of key-public.txt)
+static PalisadeEvalKey evalkey_meta(const shelfi_ctx* ctx, const EvalState& ev) {
+  if (ctx->pal_ctx_obj.empty() || ctx->pal_keytag.empty())
+    throw Error{SHELFI_ERR_STATE, "evaluation-key files need PALISADE keys (loadCryptoParams or keygen)"};
+  const Params& p = ctx->p;
+  PalisadeEvalKey K;
+  uint32_t id0 = 0;
+  K.ctx = palisade_parse_context_object(ctx->pal_ctx_obj, &id0, 1);
+  K.keytag = ctx->pal_keytag;
+  K.N = p.N;
+  K.T = p.L + ev.kP;
+  K.dnum = ev.dnum;
+  for (uint32_t t = 0; t < K.T; ++t) {
+    K.q.push_back(t < p.L ? p.q[t] : ev.p[t - p.L]);
+    K.psi.push_back(t < p.L ? p.psi[t] : ev.ppsi[t - p.L]);
+  }
+  // class versions as in the reference's own key-eval-mult.txt
+  for (auto& v : K.poly_versions) v = 0;
+  return K;
+}
+
+static std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error{SHELFI_ERR_IO, "cannot read " + path};
+  std::ostringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+// install a parsed PALISADE evaluation key after checking it belongs to these keys / params
+static void load_evalkey(shelfi_ctx* ctx, const std::string& file) {
+  EvalState& ev = eval_state(ctx);
+  const PalisadeEvalKey K = palisade_parse_evalmult_key((const uint8_t*)file.data(), file.size());
+  const Params& p = ctx->p;
+  if (ctx->pal_keytag.empty() || K.keytag != ctx->pal_keytag)
+    throw Error{SHELFI_ERR_FORMAT, "evaluation key belongs to another key pair (key tag)"};
+  if (K.N != p.N || K.T != p.L + ev.kP || K.dnum != ev.dnum)
+    throw Error{SHELFI_ERR_FORMAT, "evaluation key was made for other parameters"};
+  for (uint32_t t = 0; t < K.T; ++t)
+    if (K.q[t] != (t < p.L ? p.q[t] : ev.p[t - p.L]))
+      throw Error{SHELFI_ERR_FORMAT, "evaluation key towers differ from this context's Q and special primes"};
+  if (K.tower_off.size() != 2ull * K.dnum * K.T) throw Error{SHELFI_ERR_FORMAT, "evaluation key tower count"};
+  // residues: the key's roots may differ from ours for the special primes (PALISADE picks its
+  // own); the EVALUATION order then differs, so only keys on the same roots are accepted
+  for (uint32_t t = 0; t < K.T; ++t)
+    if (K.psi[t] != (t < p.L ? p.psi[t] : ev.ppsi[t - p.L]))
+      throw Error{SHELFI_ERR_FORMAT, "evaluation key roots of unity differ from this context's"};
+  std::vector<uint64_t> polys(K.tower_off.size() * (size_t)K.N);
+  for (size_t i = 0; i < K.tower_off.size(); ++i)
+    std::memcpy(polys.data() + i * K.N, file.data() + K.tower_off[i], (size_t)K.N * 8);
+  install_evk(ctx, ev, polys.data());
+}
+
+// shelfi_load: a key-eval-mult.txt beside PALISADE keys is loaded when it is theirs
+void load_evalkey_if_present(shelfi_ctx* ctx, const std::string& dir) {
+  std::string file;
+  try {
+    file = slurp(dir + "key-eval-mult.txt");
+  } catch (const Error&) {
+    return;  // optional file
+  }
+  try {
+    load_evalkey(ctx, file);
+  } catch (const Error&) {
+    // another key pair's or another ring's key (e.g. palisade_pybind's resources): not ours
+  }
+}
+
 static uint64_t chunk_of(uint64_t K, size_t per_ct) {
   const uint64_t cap = std::max<uint64_t>(1, (2048ull << 20) / std::max<size_t>(per_ct, 1));
   const uint64_t n = (K + cap - 1) / cap;
@@ -321,6 +393,65 @@ int shelfi_set_eval_key(shelfi_ctx* ctx, const uint64_t* evk) {
   return guarded([&] {
     DeviceGuard g(ctx->device);
     install_evk(ctx, eval_state(ctx), evk);
+  });
+}
+
+int shelfi_palisade_evalkey_parse(const uint8_t* file, size_t len, shelfi_palisade_evk_info* info,
+                                  uint64_t* polys) {
+  if (!file || !info) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    const PalisadeEvalKey K = palisade_parse_evalmult_key(file, len);
+    std::memset(info, 0, sizeof(*info));
+    info->ring_dim = K.N;
+    info->num_towers = K.T;
+    info->ctx_towers = K.ctx.L;
+    info->dnum = K.dnum;
+    for (uint32_t t = 0; t < K.T; ++t) {
+      info->moduli[t] = K.q[t];
+      info->roots[t] = K.psi[t];
+    }
+    std::memcpy(info->keytag, K.keytag.data(), std::min<size_t>(K.keytag.size(), 256));
+    if (polys)
+      for (size_t i = 0; i < K.tower_off.size(); ++i)
+        std::memcpy(polys + i * (size_t)K.N, file + K.tower_off[i], (size_t)K.N * 8);
+  });
+}
+
+int shelfi_palisade_evalkey_rewrite(const uint8_t* file, size_t len, const uint64_t* polys, uint8_t** out,
+                                    size_t* out_len) {
+  if (!file || !polys || !out || !out_len) return SHELFI_ERR_ARG;
+  *out = nullptr;
+  *out_len = 0;
+  return guarded([&] {
+    const PalisadeEvalKey K = palisade_parse_evalmult_key(file, len);
+    const std::string w = palisade_evalmult_key_file(K, polys);
+    uint8_t* buf = (uint8_t*)std::malloc(w.size());
+    if (!buf) throw std::bad_alloc();
+    std::memcpy(buf, w.data(), w.size());
+    *out = buf;
+    *out_len = w.size();
+  });
+}
+
+int shelfi_save_eval_key(const shelfi_ctx* ctx, const char* path) {
+  if (!ctx || !path) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded([&] {
+    if (!ctx->ev || ctx->ev->evk_host.empty())
+      throw Error{SHELFI_ERR_STATE, "no evaluation key: call evalMultKeyGen() first"};
+    const std::string w = palisade_evalmult_key_file(evalkey_meta(ctx, *ctx->ev), ctx->ev->evk_host.data());
+    std::ofstream f(path, std::ios::binary);
+    if (!f || !f.write(w.data(), (std::streamsize)w.size()))
+      throw Error{SHELFI_ERR_IO, std::string("cannot write ") + path};
+  });
+}
+
+int shelfi_load_eval_key(shelfi_ctx* ctx, const char* path) {
+  if (!ctx || !path) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    load_evalkey(ctx, slurp(path));
   });
 }
 

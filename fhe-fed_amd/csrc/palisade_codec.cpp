@@ -214,11 +214,11 @@ void put_dcrt_params_refs(Out& o, const PalisadeCtxParams& p, uint32_t tower_id0
 
 }  // namespace
 
-PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id) {
+PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id, uint32_t name0) {
   PalisadeCtxParams p;
   Cursor c{(const uint8_t*)obj.data(), obj.size(), 0};
   if (c.u32() != 1) bad("context version");
-  if (c.u32() != (kNew | 1u) || get_str(c, 256) != kParamsName) bad("crypto parameters type");
+  if (c.u32() != (kNew | name0) || get_str(c, 256) != kParamsName) bad("crypto parameters type");
   const uint32_t id = c.u32();
   if (!(id & kNew)) bad("crypto parameters pointer");
   const uint32_t id0 = id & ~kNew;
@@ -288,7 +288,7 @@ PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t
   p.fields.clear();
   for (;;) {
     const uint32_t v = c.u32();
-    if (v == (kNew | 2u)) break;
+    if (v == (kNew | (name0 + 1))) break;
     p.fields.push_back(v);
     if (p.fields.size() > 16) bad("crypto parameter fields");
   }
@@ -309,11 +309,11 @@ PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t
   return p;
 }
 
-std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t id0) {
+std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t id0, uint32_t name0) {
   if (p.L < 1 || p.q.size() != p.L || p.psi.size() != p.L) bad("context parameters");
   Out o;
   o.u32(1);  // CryptoContextImpl version
-  o.u32(kNew | 1u);
+  o.u32(kNew | name0);
   o.str(kParamsName);
   o.u32(kNew | id0);
   for (int i = 0; i < 3; ++i) o.u32(0);
@@ -362,7 +362,7 @@ std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t id0) {
   o.f32(p.assurance);
   o.f32(p.root_hermite);
   for (uint32_t v : p.fields) o.u32(v);
-  o.u32(kNew | 2u);
+  o.u32(kNew | (name0 + 1));
   o.str(kSchemeName);
   o.u32(kNew | (id0 + 3 + p.L));
   o.u32(0);
@@ -720,6 +720,175 @@ std::string palisade_embed_context(const std::string& f) {
     std::memcpy(&obj[p], &v, 4);
   }
   return obj;
+}
+
+
+// ------------------------------------------------ evaluation-key files (§8 f4) ----
+namespace {
+constexpr const char* kEvalKeyName = "lbcrypto::LPEvalKeyRelinImpl<lbcrypto::DCRTPoly>";
+}
+
+PalisadeEvalKey palisade_parse_evalmult_key(const uint8_t* b, size_t len) {
+  PalisadeEvalKey K;
+  Cursor c{b, len, 0};
+  if (c.get<uint8_t>() != 0x01) bad("not a little-endian PortableBinary archive");
+  if (c.u64() != 1) bad("evaluation-key map must hold one key tag");
+  K.keytag = get_str(c, 256);
+  if (c.u64() != 1) bad("evaluation-key vector must hold one key");
+  if (c.u32() != (kNew | 1u) || get_str(c, 256) != kEvalKeyName) bad("evaluation key type");
+  if (c.u32() != (kNew | 1u)) bad("evaluation key pointer");
+  for (int i = 0; i < 4; ++i) K.key_versions[i] = c.u32();
+  c.expect32(kPoly, "context pointer");
+  if (c.u32() != (kNew | 2u)) bad("context id");
+  // the context object ends at its "CKKS" scheme id string, followed by the key tag
+  const size_t ctx0 = c.p;
+  size_t ctx1 = std::string::npos;
+  for (size_t p = ctx0; p + 12 <= len; ++p)
+    if (std::memcmp(b + p, "\x04\0\0\0\0\0\0\0CKKS", 12) == 0) {
+      ctx1 = p + 12;
+      break;
+    }
+  if (ctx1 == std::string::npos) bad("context object end");
+  K.ctx_obj.assign((const char*)b + ctx0, ctx1 - ctx0);
+  uint32_t id0 = 0;
+  K.ctx = palisade_parse_context_object(K.ctx_obj, &id0, 2);
+  if (id0 != 3) bad("context ids");
+  c.p = ctx1;
+  if (get_str(c, 256) != K.keytag) bad("key tag differs from the map's");
+  if (c.u64() != 2) bad("relinearization key must be (b, a) vectors");
+  const uint32_t next_id = id0 + 4 + K.ctx.L;  // first id after the context's objects
+  uint32_t dcrt_id = 0;
+  for (int v = 0; v < 2; ++v) {
+    const uint64_t dn = c.u64();
+    if (dn < 1 || dn > 8 || (v == 1 && dn != K.dnum)) bad("digit count");
+    K.dnum = (uint32_t)dn;
+    for (uint32_t j = 0; j < K.dnum; ++j) {
+      const bool first = v == 0 && j == 0;
+      if (first) K.poly_versions[0] = c.u32();
+      const uint64_t T = c.u64();
+      if (T < 1 || T > (uint64_t)kMaxTowers || (!first && T != K.T)) bad("tower count");
+      K.T = (uint32_t)T;
+      for (uint32_t t = 0; t < K.T; ++t) {
+        if (first && t == 0) K.poly_versions[1] = c.u32();
+        c.expect32(kPoly, "residue vector pointer");
+        if (c.get<uint8_t>() != 0x01) bad("residue vector marker");
+        if (first && t == 0) K.poly_versions[2] = c.u32();
+        const uint64_t N = c.u64();
+        if (N < 2 || N > (1u << 17) || (N & (N - 1)) || (K.N && N != K.N)) bad("ring dimension");
+        K.N = (uint32_t)N;
+        c.need((size_t)N * 8);
+        K.tower_off.push_back(c.p);
+        c.p += (size_t)N * 8;
+        const uint64_t q = c.u64();
+        if (c.u32() != 0) bad("key polynomials must be in EVALUATION format");
+        c.expect32(kPoly, "tower parameters pointer");
+        const uint32_t pid = c.u32();
+        if (first) {
+          if (pid != (kNew | (next_id + t))) bad("tower parameters id");
+          if (c.u32() != 2 * N || c.u32() != N || c.get<uint8_t>() != 1) bad("tower parameters");
+          if (c.u64() != q) bad("tower parameters modulus");
+          K.psi.push_back(c.u64());
+          c.u64();
+          c.u64();
+          K.q.push_back(q);
+        } else {
+          if (pid != next_id + t || q != K.q[t]) bad("tower parameters reference");
+        }
+      }
+      if (c.u32() != 0) bad("key polynomials must be in EVALUATION format");
+      c.expect32(kPoly, "element parameters pointer");
+      const uint32_t pid = c.u32();
+      if (first) {
+        dcrt_id = next_id + K.T;
+        if (pid != (kNew | dcrt_id)) bad("element parameters id");
+        if (c.u32() != 2 * K.N || c.u32() != K.N || c.get<uint8_t>() != 1) bad("element parameters");
+        const uint32_t B = K.ctx.bigint_bytes;
+        if (read_bigint(c, B) != [&] {
+              std::vector<uint32_t> m = modulus_product(K.q);
+              m.resize((B - 2) / 4, 0);
+              return m;
+            }())
+          bad("element modulus is not the product of the key's towers");
+        c.need(3ull * B);
+        K.elem_bigints.assign((const char*)b + c.p, 3ull * B);
+        c.p += 3ull * B;
+        if (c.u64() != K.T) bad("element tower count");
+        for (uint32_t t = 0; t < K.T; ++t) {
+          c.expect32(kPoly, "element tower pointer");
+          if (c.u32() != next_id + t) bad("element tower reference");
+        }
+        read_bigint(c, B);  // originalModulus
+      } else if (pid != dcrt_id) {
+        bad("element parameters reference");
+      }
+    }
+  }
+  if (c.p != len) bad("trailing bytes after the evaluation key");
+  // Q's towers lead the key's (Q u P), the special towers follow
+  if (K.T <= K.ctx.L) bad("no special towers");
+  for (uint32_t t = 0; t < K.ctx.L; ++t)
+    if (K.q[t] != K.ctx.q[t]) bad("key towers do not start with the context's");
+  return K;
+}
+
+std::string palisade_evalmult_key_file(const PalisadeEvalKey& K, const uint64_t* polys) {
+  const uint32_t N = K.N, T = K.T, B = K.ctx.bigint_bytes;
+  if (K.q.size() != T || K.psi.size() != T || K.dnum < 1) bad("evaluation key parameters");
+  Out o;
+  o.u8(0x01);
+  o.u64(1);
+  o.str(K.keytag);
+  o.u64(1);
+  o.u32(kNew | 1u);
+  o.str(kEvalKeyName);
+  o.u32(kNew | 1u);
+  for (int i = 0; i < 4; ++i) o.u32(K.key_versions[i]);
+  o.u32(kPoly);
+  o.u32(kNew | 2u);
+  o.s += K.ctx_obj.empty() ? palisade_context_object(K.ctx, 3, 2) : K.ctx_obj;
+  o.str(K.keytag);
+  o.u64(2);
+  const uint32_t next_id = 3 + 4 + K.ctx.L, dcrt_id = next_id + T;
+  o.s.reserve(o.s.size() + 2ull * K.dnum * T * ((size_t)N * 8 + 64) + 4096);
+  for (int v = 0; v < 2; ++v) {
+    o.u64(K.dnum);
+    for (uint32_t j = 0; j < K.dnum; ++j) {
+      const bool first = v == 0 && j == 0;
+      if (first) o.u32(K.poly_versions[0]);
+      o.u64(T);
+      for (uint32_t t = 0; t < T; ++t) {
+        if (first && t == 0) o.u32(K.poly_versions[1]);
+        o.u32(kPoly);
+        o.u8(0x01);
+        if (first && t == 0) o.u32(K.poly_versions[2]);
+        o.u64(N);
+        o.put(polys + (((size_t)v * K.dnum + j) * T + t) * N, (size_t)N * 8);
+        o.u64(K.q[t]);
+        o.u32(0);  // EVALUATION
+        o.u32(kPoly);
+        if (first) {
+          o.u32(kNew | (next_id + t));
+          put_tower_params(o, N, K.q[t], K.psi[t]);
+        } else {
+          o.u32(next_id + t);
+        }
+      }
+      o.u32(0);
+      o.u32(kPoly);
+      if (first) {
+        o.u32(kNew | dcrt_id);
+        PalisadeCtxParams e = K.ctx;
+        e.L = T;
+        e.q = K.q;
+        e.psi = K.psi;
+        e.elem_bigints = K.elem_bigints.size() == 3ull * B ? K.elem_bigints : std::string();
+        put_dcrt_params_refs(o, e, next_id);
+      } else {
+        o.u32(dcrt_id);
+      }
+    }
+  }
+  return o.s;
 }
 
 }  // namespace shelfi

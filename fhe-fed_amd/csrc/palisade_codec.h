@@ -87,8 +87,11 @@ struct PalisadeCtxParams {
 
 // Structured parse of a context object whose first shared-ptr id is *first_id
 // (2: standalone cryptocontext.txt body, 3: embedded in a key or ciphertext archive).
-PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id);
-std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t first_id);
+// name0: the id of its first polymorphic type name (1 in context / key / ciphertext files, 2
+// inside an evaluation-key file, whose key type name comes first)
+PalisadeCtxParams palisade_parse_context_object(const std::string& obj, uint32_t* first_id,
+                                                uint32_t name0 = 1);
+std::string palisade_context_object(const PalisadeCtxParams& p, uint32_t first_id, uint32_t name0 = 1);
 // Structured parse of a standalone cryptocontext.txt (throws on other layouts)
 PalisadeCtxParams palisade_parse_context_file(const std::string& file);
 // cryptocontext.txt as ckks.cpp:41 writes it (Serial::SerializeToFile of the context)
@@ -103,5 +106,30 @@ void palisade_key_context(const std::string& pub, std::string& ctx_obj, std::str
 // A standalone context file (cryptocontext.txt) re-embedded one shared-ptr id later
 // (what a key or ciphertext archive holds).  Exposed for the tests' pin.
 std::string palisade_embed_context(const std::string& ctxfile);
+
+// key-eval-mult.txt (§8 f4): the cereal archive of EvalMultKeyGen's relinearization key as
+// PALISADE 1.11 serializes the evaluation-key map (the reference's palisade_pybind/
+// SHELFI_FHE/resources/cryptoparams/key-eval-mult.txt; grammar pinned by rewriting that file
+// byte for byte, tests/test_palisade_codec.py):
+//   file   := 0x01 u64 1 str(tag) u64 1  new-name(1) str(LPEvalKeyRelinImpl<DCRTPoly>) new(1)
+//             u32 ver x4  0x40000000 new(2) ctxobj(ids from 3, names from 2)  str(tag)
+//             u64 2 ( u64 dnum dcrt^dnum )^2                 m_rKey: b-vector, a-vector
+//   dcrt   := [ver] u64 T tower^T u32 0 0x40000000 params    (Q u P towers, EVALUATION)
+//   tower  := [ver] 0x40000000 0x01 [ver] u64 N u64[N] u64 q u32 0 0x40000000 tparams
+// The first polynomial embeds the key's ILNativeParams per tower and its ILDCRTParams (new
+// ids after the context's); the others reference them.
+struct PalisadeEvalKey {
+  std::string keytag;
+  std::string ctx_obj;  // the embedded context object (empty when writing: synthesized from ctx)
+  PalisadeCtxParams ctx;
+  uint32_t N = 0, T = 0, dnum = 0;
+  std::vector<uint64_t> q, psi;    // towers of the key polynomials: Q, then the special primes
+  std::string elem_bigints;        // raw root / bigQ / bigRoot of the key's ILDCRTParams
+  uint32_t key_versions[4] = {0, 0, 0, 0};   // LPEvalKeyRelinImpl, LPEvalKeyImpl, LPKey, CryptoObject
+  uint32_t poly_versions[3] = {1, 1, 1};     // DCRTPoly, PolyImpl, NativeVector class versions
+  std::vector<size_t> tower_off;   // parse: [2][dnum][T] byte offsets of the N residues
+};
+PalisadeEvalKey palisade_parse_evalmult_key(const uint8_t* b, size_t len);
+std::string palisade_evalmult_key_file(const PalisadeEvalKey& k, const uint64_t* polys);
 
 }  // namespace shelfi

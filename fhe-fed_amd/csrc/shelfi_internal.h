@@ -244,6 +244,8 @@ size_t keygen_scratch_bytes(const Params& p);
 void comm_release(shelfi_ctx* ctx);
 // eval.cpp: drop the relinearization key (keys_only) or all EvalMult / ModReduce state
 void eval_release(shelfi_ctx* ctx, bool keys_only);
+// eval.cpp: install cryptodir's key-eval-mult.txt when it belongs to the loaded keys
+void load_evalkey_if_present(shelfi_ctx* ctx, const std::string& dir);
 // eval.cpp: NTT / CRT tables of Q_l (towers q_0 .. q_{Ll-1}) for decrypt at a level
 const DeviceTables& level_tables(shelfi_ctx* ctx, uint32_t Ll);
 // api.cpp helpers shared with eval.cpp

@@ -274,6 +274,24 @@ int shelfi_eval_mult_keygen(shelfi_ctx* ctx);
 size_t shelfi_eval_key_words(const shelfi_ctx* ctx); /* 2 * dnum * (L + num_special) * N */
 int shelfi_get_eval_key(const shelfi_ctx* ctx, uint64_t* evk);
 int shelfi_set_eval_key(shelfi_ctx* ctx, const uint64_t* evk);
+/* PALISADE key-eval-mult.txt (cereal archive of the evaluation-key map, as the reference's
+ * palisade_pybind/SHELFI_FHE/resources/cryptoparams/key-eval-mult.txt).  save: this context's
+ * key (PALISADE keys required: the file embeds their context and key tag); load: a file made
+ * for this key pair and these parameters (shelfi_load also picks up a matching
+ * key-eval-mult.txt beside the key files). */
+int shelfi_save_eval_key(const shelfi_ctx* ctx, const char* path);
+int shelfi_load_eval_key(shelfi_ctx* ctx, const char* path);
+typedef struct {
+  uint32_t ring_dim, num_towers, ctx_towers, dnum; /* num_towers = Q's ctx_towers + special */
+  uint64_t moduli[16], roots[16];
+  char keytag[257];
+} shelfi_palisade_evk_info;
+/* Host-only: parse a key-eval-mult.txt; polys [2][dnum][num_towers][ring_dim] when non-NULL. */
+int shelfi_palisade_evalkey_parse(const uint8_t* file, size_t len, shelfi_palisade_evk_info* info,
+                                  uint64_t* polys);
+/* Host-only: the same file re-serialized around other residues (the format's pin). */
+int shelfi_palisade_evalkey_rewrite(const uint8_t* file, size_t len, const uint64_t* polys, uint8_t** out,
+                                    size_t* out_len);
 /* cc->EvalMult(ct_a, ct_b): tensor product + HYBRID relinearization, a, b, out
  * [K][2][towers][N] in HBM (out may be a or b).  Result depth 2, scale = scale_a scale_b. */
 int shelfi_dev_mult(shelfi_ctx* ctx, const uint64_t* a_dev, const uint64_t* b_dev, size_t K, uint32_t towers,

@@ -4,10 +4,13 @@ oracle's restatement (oracle/ckks_oracle.c or_evk_keygen / or_eval_mult / or_res
 and the decrypted values equal to the plaintext products.  PALISADE parity of the key
 switching itself is unpinned (tests/test_oracle_f4.py says why); its parameters (dnum,
 special primes, roots) are pinned by the reference's key-eval-mult.txt."""
+import os
+
 import numpy as np
 import pytest
 
 import oracle as O
+from conftest import PALISADE_PYBIND_DIR
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -131,3 +134,43 @@ def test_argument_errors(ctx):
     one = a[:, :, :1].contiguous()
     with pytest.raises(ValueError):
         D.rescale(c, one)
+
+
+def test_eval_key_file_round_trip(tmp_path):
+    """saveEvalMultKey writes PALISADE's key-eval-mult.txt (the format the reference's own file
+    pins byte for byte, tests/test_oracle_f4.py); loadCryptoParams of the directory picks it up
+    for the same key pair, and products match."""
+    d = str(tmp_path) + os.sep
+    c = m.CKKS("ckks", 4096, 52, d, multDepth=2, seed=5, decodeNoise=False)
+    assert c.genCryptoContextAndKeyGen() == 1
+    c.evalMultKeyGen()
+    c.saveEvalMultKey()
+    f = open(d + "key-eval-mult.txt", "rb").read()
+    info, polys = m.palisade_evalkey_parse(f)
+    _, tag = m.palisade_key_context(open(d + "key-public.txt", "rb").read())
+    assert info["keytag"] == tag and info["dnum"] == 2 and info["ctx_towers"] == 3
+    assert np.array_equal(polys, c.get_eval_key())
+    assert m.palisade_evalkey_rewrite(f, polys) == f
+    u = m.CKKS("ckks", 4096, 52, d, multDepth=2, decodeNoise=False)
+    u.loadCryptoParams()
+    assert u.eval_key_info()["has_key"] and np.array_equal(u.get_eval_key(), c.get_eval_key())
+    rng = np.random.default_rng(3)
+    a, b = (D.encrypt(c, torch.tensor(rng.uniform(-1, 1, 8192), device="cuda")) for _ in range(2))
+    assert torch.equal(D.mult(u, a, b), D.mult(c, a, b))
+    # keys without a PALISADE context cannot be written in PALISADE's format
+    raw = m.CKKS("ckks", 4096, 52, "", multDepth=2, decodeNoise=False)
+    raw.set_keys(*c.get_keys())
+    raw.set_eval_key(c.get_eval_key())
+    with pytest.raises(RuntimeError, match="PALISADE keys"):
+        raw.saveEvalMultKey(str(tmp_path / "x.txt"))
+
+
+def test_reference_evaluation_key_is_not_taken_for_other_keys():
+    """palisade_pybind's resources hold keys (tag 83cfbab5...) and an evaluation key of another
+    key pair and ring (a2d03f86..., 2^14): loadCryptoParams leaves it out, and an explicit load
+    refuses it."""
+    r = m.CKKS("ckks", 4096, 52, PALISADE_PYBIND_DIR)
+    r.loadCryptoParams()
+    assert r.info()["keys_loaded"] and not r.eval_key_info()["has_key"]
+    with pytest.raises(RuntimeError, match="another key pair"):
+        r.loadEvalMultKey()

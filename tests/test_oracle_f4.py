@@ -125,3 +125,42 @@ def test_rescale_is_rounding_division(small):
         # round half away is irrelevant here: q_l is odd, so no coefficient sits on .5
         exp = np.array([((2 * v + ql) // (2 * ql)) % int(q[t]) for v in c], dtype=np.uint64)
         assert np.array_equal(got, exp)
+
+
+def _evk_file():
+    from conftest import PALISADE_PYBIND_DIR
+
+    return open(os.path.join(PALISADE_PYBIND_DIR, "key-eval-mult.txt"), "rb").read()
+
+
+def test_reference_evaluation_key_file_rewrites_byte_for_byte():
+    """The key-eval-mult.txt codec (palisade_codec.cpp) parses the reference's file into
+    its context, key tag, towers and residues, and writes it back identically; the
+    towers are the context's Q followed by the restated special primes and roots."""
+    m = pytest.importorskip("SHELFI_FHE")
+    f = _evk_file()
+    info, polys = m.palisade_evalkey_parse(f)
+    assert info["keytag"] == EVK["keytag"] and info["ring_dim"] == EVK["ring_dim"]
+    assert (info["ctx_towers"], info["num_towers"], info["dnum"]) == (3, 5, 2)
+    Q = EVK["context_moduli"]
+    dn, al, p, pr = O.special_primes(info["ring_dim"], Q)
+    assert info["moduli"] == Q + [int(x) for x in p]
+    assert info["roots"][3:] == [int(x) for x in pr]
+    assert polys.shape == (2, 2, 5, EVK["ring_dim"])
+    assert all(int(polys[:, :, t].max()) < info["moduli"][t] for t in range(5))
+    assert m.palisade_evalkey_rewrite(f, polys) == f
+    # the residues sit where the parser says: other residues give the same framing
+    rng = np.random.default_rng(0)
+    other = np.stack([rng.integers(0, q, size=polys[:, :, t].shape, dtype=np.uint64)
+                      for t, q in enumerate(info["moduli"])], axis=2)
+    g = m.palisade_evalkey_rewrite(f, other)
+    assert len(g) == len(f)
+    assert np.array_equal(m.palisade_evalkey_parse(g)[1], other)
+
+
+def test_evaluation_key_parser_rejects_damage():
+    m = pytest.importorskip("SHELFI_FHE")
+    f = _evk_file()
+    for bad in (f[:-1], f[:3000], f + b"\0", f[:9] + b"\x02" + f[10:]):
+        with pytest.raises((RuntimeError, ValueError)):
+            m.palisade_evalkey_parse(bad, polys=False)
