@@ -313,6 +313,7 @@ int shelfi_special_primes(uint32_t ring_dim, uint32_t num_towers, const uint64_t
 int shelfi_eval_key_info(const shelfi_ctx* ctx, uint32_t* dnum, uint32_t* alpha, uint32_t* num_special,
                          uint64_t* special, int* has_key) {
   if (!ctx || !dnum || !alpha || !num_special) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   return guarded([&] {
     uint64_t p[kMaxTowers];
     special_primes(ctx->p.N, ctx->p.L, ctx->p.q, dnum, alpha, num_special, p, nullptr);
@@ -379,6 +380,7 @@ int shelfi_eval_mult_keygen(shelfi_ctx* ctx) {
 
 int shelfi_get_eval_key(const shelfi_ctx* ctx, uint64_t* evk) {
   if (!ctx || !evk) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);  // against a concurrent keygen / load replacing it
   if (!ctx->ev || ctx->ev->evk_host.empty()) {
     set_error("no evaluation key: call shelfi_eval_mult_keygen first");
     return SHELFI_ERR_STATE;
