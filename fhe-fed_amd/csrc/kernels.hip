@@ -161,6 +161,15 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_arena_many(const uint64_t* 
   __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + base + 2u * threadIdx.x));
 }
 
+// Host side of xcd_block: the combo count G when the block passes may deal (tower, block)
+// combos per XCD (G % 8 == 0), else 0.  SHELFI_XCD_ORDER=0 keeps the natural order (A/B
+// probe switch, read per launch).
+static uint32_t xcd_combos(uint64_t G) {
+  const char* env = getenv("SHELFI_XCD_ORDER");
+  if (env && *env == '0') return 0;
+  return (G % 8 == 0 && G <= 0xFFFFFFFFull) ? (uint32_t)G : 0;
+}
+
 void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,
                             uint32_t L, uint32_t logN, const TowerConst* tc, uint64_t* out,
                             hipStream_t s) {
@@ -352,6 +361,21 @@ __device__ constexpr uint32_t lofs(int m) {
 }
 constexpr uint32_t lpad_size(int BL) { return (1u << BL) + (1u << (BL - 3)); }
 
+// XCD-aware block order for the block passes.  Blocks b and b + 8 share an XCD (observed
+// round-robin dealing, MI355X_MICROARCH "Workgroup dispatch"; used for speed only: any
+// placement gives the same results).  The G = L 2^sstart (tower, block) combos each own a
+// shared slice of twiddles and key words (64-160 KiB per workgroup, 4-6 MiB per launch at
+// 2^15/L4, more than one XCD's 4 MiB L2); dealt in natural order every XCD touches all of
+// them and they stream from the Infinity Cache.  With xg = G (G % 8 == 0) XCD slot x = bid % 8
+// owns combos [x G/8, (x+1) G/8) for every ciphertext, 1/8 of the slices.  Returns the
+// logical block id k G + combo; xg == 0 keeps the natural order.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t xg) {
+  if (!xg) return bid;
+  const uint32_t g8 = xg >> 3, i = bid >> 3;
+  const uint32_t k = i / g8;
+  return k * xg + (bid & 7) * g8 + (i - k * g8);
+}
+
 // ---- compile-time block passes over per-block twiddle tables ---------------
 // For blocks of 2^BL elements (BL = ntt_block_log), block b owns the twiddle slice
 // tb = tw_*_blk[t][b << BL]: local stage l (the l-th of the block's stages, in the
@@ -448,14 +472,15 @@ template <int BL, int K1, int K2, int K3, int K4>
 __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
     const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
     const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk,
-    const uint64_t* __restrict__ pksh, uint64_t* __restrict__ ct, uint32_t zero) {
+    const uint64_t* __restrict__ pksh, uint64_t* __restrict__ ct, uint32_t zero, uint32_t xg) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
   constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
   const uint32_t sstart = logN - BL;
-  const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
-  const uint32_t rest = blockIdx.x >> sstart;
+  const uint32_t bid = xcd_block(blockIdx.x, xg);
+  const uint32_t b = bid & ((1u << sstart) - 1);
+  const uint32_t rest = bid >> sstart;
   const uint32_t t = rest % L, k = rest / L;
   const TowerConst& cst = tcs[t];
   const uint64_t q = cst.q, n8q = cst.n8q;
@@ -534,12 +559,14 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
                                                              const TowerConst* __restrict__ tcs,
                                                              const uint64_t* __restrict__ ct,
                                                              const uint64_t* __restrict__ sk,
-                                                             const uint64_t* __restrict__ sksh) {
+                                                             const uint64_t* __restrict__ sksh,
+                                                             uint32_t xg) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
   const uint32_t sstart = logN - BL;
-  const uint32_t b = blockIdx.x & ((1u << sstart) - 1);
-  const uint32_t poly = blockIdx.x >> sstart;  // k * L + t
+  const uint32_t bid = xcd_block(blockIdx.x, xg);
+  const uint32_t b = bid & ((1u << sstart) - 1);
+  const uint32_t poly = bid >> sstart;  // k * L + t
   const uint32_t t = poly % L, k = poly / L;
   const uint64_t q = tcs[t].q, n4q = tcs[t].n4q;
   const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
@@ -1178,12 +1205,13 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   }
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
+  const uint32_t xg = xcd_combos(p.L << nlogR);
   if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u);
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
                      pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
@@ -1692,12 +1720,13 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   {
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
+    const uint32_t xg = xcd_combos(p.L << (logR > 0 ? logR : 0));
     if (logR > 0 && blkLog == 11 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
     else if (logR > 0 && blkLog == 12 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
