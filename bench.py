@@ -36,6 +36,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -44,6 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "fhe-fed_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_CLOCK_GHZ = 2.4  # MI355X peak engine clock
 VALU_CYCLES_PER_INST = 4.0  # one wave64 VOP3 instruction per SIMD (tools/valu_rates.hip, profiles/r02_valu_rates.txt)
+COMM_CHECK_TIMEOUT_S = 120  # the C-ABI communicator check at N > 1 (main(): c_abi_comm_check)
 # name -> (slots, multDepth, params per learner, learners per GPU, description)
 WORKLOADS = {
     "cfg2": (16384, 3, 61_706, 16, "LeNet-5"),
@@ -430,9 +432,11 @@ def main():
     check = None if args.no_check else checked(main_mode)
     # the library's own C-ABI communicator (comm.cpp: RCCL uint64 SUM + mod-q fold inside
     # libshelfi) on the same partial sums, outside the timed region: its all-reduced
-    # aggregate must equal the torch path's owned shares bit for bit on every rank
-    comm_check = None
-    if distributed and main_mode["shard"] == "learners" and args.combine == "torch":
+    # aggregate must equal the torch path's owned shares bit for bit on every rank.  It runs
+    # after every measurement, under a watchdog: a second RCCL instance in the process that
+    # never returns must not cost the headline line (the line is then written with the
+    # check marked as timed out and every rank exits).
+    def c_abi_comm_check():
         try:
             t0 = time.perf_counter()
             comm = SD.Comm(ck, rank, world)
@@ -445,11 +449,12 @@ def main():
             comm.close()
             okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-            comm_check = {"ok": bool(okt.item()), "seconds": round(time.perf_counter() - t0, 3),
-                          "what": "shelfi_dev_allreduce (C ABI, world %d) == torch reduce_scatter shares" % world}
             del full
+            return {"ok": bool(okt.item()), "seconds": round(time.perf_counter() - t0, 3),
+                    "what": "shelfi_dev_allreduce (C ABI, world %d) == torch reduce_scatter shares" % world}
         except Exception as e:  # reported, never fatal to the headline
-            comm_check = {"ok": False, "error": repr(e)[:300]}
+            return {"ok": False, "error": repr(e)[:300]}
+
     # the same launches into a plain torch.empty output (no placement tuning): the
     # kernel's placement-independent rate
     untuned = None
@@ -714,19 +719,36 @@ def main():
         res["check"] = check
     if alt:
         res["alternative_partitioning"] = alt
-    if comm_check:
-        res["c_abi_comm_check"] = comm_check
     if api:
         res["api_bytes_path"] = api
     if f4:
         res["f4_eval_mult"] = f4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, L, q, psi, delta, batch, Cl, args.cpu_seconds)
-    if rank == 0:
-        os.write(json_fd, (json.dumps(res) + "\n").encode())
+    emit_lock = threading.Lock()
+    emitted = []
+
+    def emit():
+        with emit_lock:
+            if rank == 0 and not emitted:
+                emitted.append(1)
+                os.write(json_fd, (json.dumps(res) + "\n").encode())
+
+    finished = threading.Event()
+    if distributed:
+        def watchdog():
+            if not finished.wait(COMM_CHECK_TIMEOUT_S):
+                res["c_abi_comm_check"] = {"ok": False, "error": "no result within %d s; exited" % COMM_CHECK_TIMEOUT_S}
+                emit()
+                os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+        if main_mode["shard"] == "learners" and args.combine == "torch":
+            res["c_abi_comm_check"] = c_abi_comm_check()
+    emit()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+    finished.set()
 
 
 if __name__ == "__main__":
