@@ -736,6 +736,8 @@ def main():
 
     finished = threading.Event()
     if distributed:
+        dist.barrier()  # rank 0 ran the f4 / bytes-API samples alone: start every watchdog together
+
         def watchdog():
             if not finished.wait(COMM_CHECK_TIMEOUT_S):
                 res["c_abi_comm_check"] = {"ok": False, "error": "no result within %d s; exited" % COMM_CHECK_TIMEOUT_S}
