@@ -19,7 +19,8 @@ from SHELFI_FHE import device as D  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-ck = m.CKKS("ckks", 16384, 52, "", multDepth=3, seed=7, decodeNoise=False)
+ck = m.CKKS("ckks", int(os.environ.get("BATCH", "16384")), 52, "", multDepth=int(os.environ.get("DEPTH", "3")),
+           seed=7, decodeNoise=False)
 assert ck.genCryptoContextAndKeyGen() == 1
 ck.evalMultKeyGen()
 inf = ck.info()
