@@ -129,12 +129,32 @@ __device__ __forceinline__ void ct_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, 
   Y = x + (q << 2) - t;
 }
 
-// Inverse (GS) butterfly, [0, 4q) in and out, borrow-free reduction of the sum.
+// Inverse (GS) butterfly, [0, 4q) in and out, borrow-free reduction of the sum (the generic
+// passes; the compile-time ones schedule the reduction with gs_bfly_b below).
 __device__ __forceinline__ void gs_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
                                           uint64_t q, uint64_t n4q) {
   const uint64_t x = X, y = Y;
   X = csub_neg(x + y, n4q);
   Y = shoup_lazy(x + (q << 2) - y, W, Wp, q);
+}
+// Inverse (GS) butterfly with the sum's reduction scheduled by the caller (q < 2^60): inputs
+// below B = 4q (B8 false: X = x + y < 8q, left unreduced) or B = 8q (B8: X = x + y < 16q,
+// reduced by 8q to < 8q); Y = (x + B - y) w lazily, < 4q.  Inside a register group the bound
+// of a stage's inputs is known at compile time: an element written as a sum (X) by the
+// previous stage is below 8q, one written as a product (Y) below 4q, so only pairs of sums
+// pay the reduction.
+template <bool B8>
+__device__ __forceinline__ void gs_bfly_b(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp, uint64_t q,
+                                          uint64_t n8q) {
+  const uint64_t x = X, y = Y;
+  X = B8 ? csub_neg(x + y, n8q) : x + y;
+  Y = shoup_lazy(x + (q << (B8 ? 3 : 2)) - y, W, Wp, q);
+}
+// Stage v (pairs 2^v apart) of a register group whose inputs are below 8q (IN8) or 4q: does
+// the pair at group index a take the 8q form?
+template <bool IN8>
+__device__ constexpr bool gs_in8(int v, int a) {
+  return v == 0 ? IN8 : ((a >> (v - 1)) & 1) == 0;
 }
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t canon8(uint64_t x, uint64_t q) {

@@ -435,9 +435,9 @@ __device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, 
 // Inverse (GS) chunk of KC stages starting at local half-size 2^T0: set s -> g = s >> T0,
 // j0 = g 2^(T0+KC) + (s mod 2^T0), elements j0 + m 2^T0; stage-i twiddles are
 // tb[2^l + g 2^(KC-1-i) + gs], gs < 2^(KC-1-i), l = BL - 1 - T0 - i.
-template <int BL, int T0, int KC, class Load, class Store>
+template <int BL, int T0, int KC, bool IN8, class Load, class Store>
 __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, uint64_t q,
-                                             uint64_t n4q, Load ld, Store st) {
+                                             uint64_t n8q, Load ld, Store st) {
   constexpr int M = 1 << KC, NS = (1 << (BL - KC)) / 256;
   static_assert(NS >= 1, "chunk plan");
 #pragma unroll
@@ -457,7 +457,12 @@ __device__ __forceinline__ void inv_chunk_ct(const ulonglong2* __restrict__ tb, 
       for (int gs = 0; gs < (M >> (i + 1)); ++gs) {
         const ulonglong2 W = tw[gs];
 #pragma unroll
-        for (int mm = 0; mm < hm; ++mm) gs_bfly_s(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n4q);
+        for (int mm = 0; mm < hm; ++mm) {
+          if (gs_in8<IN8>(i, mm))
+            gs_bfly_b<true>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+          else
+            gs_bfly_b<false>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+        }
       }
     }
     st(r, j0, pj0, x);
@@ -549,7 +554,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
 
 // Decrypt's first INTT pass at compile-time shape (chunks K1..K4, sum BL; needs
 // logN > BL): c0 + c1*s is formed straight into the first chunk's registers from the
-// ciphertext batch [K][2][L][N], and the last chunk writes the lazy ([0, 4q)) block to
+// ciphertext batch [K][2][L][N], and the last chunk writes the lazy ([0, 8q)) block to
 // dbuf [K][L][N] from registers for ntt_inv_cols.  Same contract as ntt_inv_blocks with
 // ct != nullptr and scale_ninv = 0.
 template <int BL, int K1, int K2, int K3, int K4>
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint32_t b = bid & ((1u << sstart) - 1);
   const uint32_t poly = bid >> sstart;  // k * L + t
   const uint32_t t = poly % L, k = poly / L;
-  const uint64_t q = tcs[t].q, n4q = tcs[t].n4q;
+  const uint64_t q = tcs[t].q, n4q = tcs[t].n4q, n8q = tcs[t].n8q;
   const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint64_t* __restrict__ ss = sksh + off;
   const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
   // first chunk: contiguous sets of 2^K1 (T0 = 0)
-  inv_chunk_ct<BL, 0, K1>(tb, q, n4q,
+  inv_chunk_ct<BL, 0, K1, false>(tb, q, n8q,
                           [&](uint32_t j, uint32_t) {
                             return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q);
                           },
@@ -587,18 +592,18 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
                             for (int m = 0; m < (1 << K1); ++m) sm[pj0 + lofs<1>(m)] = x[m];
                           });
   __syncthreads();
-  inv_chunk_ct<BL, K1, K2>(tb, q, n4q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
+  inv_chunk_ct<BL, K1, K2, true>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
     for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << K1)>(m)] = x[m];
   });
   __syncthreads();
-  inv_chunk_ct<BL, K1 + K2, K3>(tb, q, n4q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
+  inv_chunk_ct<BL, K1 + K2, K3, true>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
     for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (K1 + K2))>(m)] = x[m];
   });
   __syncthreads();
   uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
-  inv_chunk_ct<BL, BL - K4, K4>(tb, q, n4q, lds_ld, [&](int, uint32_t j0, uint32_t, auto& x) {
+  inv_chunk_ct<BL, BL - K4, K4, true>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, uint32_t, auto& x) {
 #pragma unroll
     for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = x[m];
   });
@@ -685,7 +690,10 @@ __global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys
 #pragma unroll
       for (int jj = 0; jj < tr; ++jj) {
         const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-        gs_bfly_s(x[r0], x[r1], W, Wp, q, c.n4q);
+        if (gs_in8<true>(v, jj))  // inputs below 8q (ntt_inv_blocks_dec_ct leaves sums < 8q)
+          gs_bfly_b<true>(x[r0], x[r1], W, Wp, q, c.n8q);
+        else
+          gs_bfly_b<false>(x[r0], x[r1], W, Wp, q, c.n8q);
       }
     }
   }
@@ -1390,7 +1398,12 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
       for (int i = 0; i < h; ++i) {
         const uint64_t W = w[h + i], Wp = wp[h + i];
 #pragma unroll
-        for (int jj = 0; jj < tr; ++jj) gs_bfly_s(x[2 * i * tr + jj], x[2 * i * tr + jj + tr], W, Wp, q, c.n4q);
+        for (int jj = 0; jj < tr; ++jj) {
+          if (gs_in8<true>(v, jj))
+            gs_bfly_b<true>(x[2 * i * tr + jj], x[2 * i * tr + jj + tr], W, Wp, q, c.n8q);
+          else
+            gs_bfly_b<false>(x[2 * i * tr + jj], x[2 * i * tr + jj + tr], W, Wp, q, c.n8q);
+        }
       }
     }
 #pragma unroll
