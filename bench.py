@@ -59,7 +59,7 @@ METRIC = "ciphertexts aggregated/sec (+ encode+enc / dec+decode ms), N clients, 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)  # ~0.8 s timed at cfg3: long enough for a 1 s GPU-activity sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
     ap.add_argument("--learners-per-gpu", type=int, default=0, help="0 = the workload's default")
