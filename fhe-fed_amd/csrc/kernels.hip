@@ -348,19 +348,6 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc(const uint64_t* __rest
   }
 }
 
-// Padded LDS blocks of the compile-time passes: 4 spare u64 after every 32, so that the
-// set patterns of the chunk plans (element distance 1, 4 or 8 inside a run of 32, or a
-// multiple of 32) fall on distinct banks for ds_read_b64 / ds_write_b64 (unpadded, the
-// distance-4 sets were 8-way conflicts: 9.3 extra LDS cycles per instruction measured).
-// A set's elements are j0 + m D with D = 2^dLog, j0 mod D < D and the group aligned to
-// D M, so element m sits at lpad(j0) + lofs<D>(m): the run crossings depend on m only.
-__device__ __forceinline__ uint32_t lpad(uint32_t i) { return i + ((i >> 5) << 2); }
-template <int D>
-__device__ constexpr uint32_t lofs(int m) {
-  return (uint32_t)(m * D + (((m * D) >> 5) << 2));
-}
-constexpr uint32_t lpad_size(int BL) { return (1u << BL) + (1u << (BL - 3)); }
-
 // XCD-aware block order for the block passes.  Blocks b and b + 8 share an XCD (observed
 // round-robin dealing, MI355X_MICROARCH "Workgroup dispatch"; used for speed only: any
 // placement gives the same results).  The G = L 2^sstart (tower, block) combos each own a
@@ -376,62 +363,6 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t xg) {
   return k * xg + (bid & 7) * g8 + (i - k * g8);
 }
 
-// ---- compile-time block passes over per-block twiddle tables ---------------
-// For blocks of 2^BL elements (BL = ntt_block_log), block b owns the twiddle slice
-// tb = tw_*_blk[t][b << BL]: local stage l (the l-th of the block's stages, in the
-// transform's own order) and group i sit at tb[2^l + i] as one 16-byte {w, w'} pair
-// (DeviceTables::tw_fwd_blk / tw_inv_blk).  Every shift below is a compile-time constant
-// and every twiddle address is a block-uniform base plus a 32-bit offset: the generic
-// passes above spend ~40 VALU instructions per butterfly, mostly on 64-bit index math.
-//
-// Forward chunk of KC stages starting at local half-size 2^H0: set s -> g = s >> dLog,
-// j0 = g 2^(H0+1) + (s mod 2^dLog), elements j0 + m 2^dLog (dLog = H0 - KC + 1); its
-// stage-i twiddles are tb[2^l + g 2^i + gs], gs < 2^i, l = BL - 1 - H0 + i.
-//
-// Reduction schedule: the stage at local half-size 2^h reduces its x inputs iff h is
-// even, so the block's last stage (h = 0) always does: inputs below 12q (the columns
-// pass leaves < 8q), outputs below 12q, never above 16q in between (ct_bfly_s).
-template <int BL, int H0, int KC>
-__device__ __forceinline__ void fwd_set_ct(uint64_t (&x)[1 << KC], uint32_t g,
-                                           const ulonglong2* __restrict__ tb, uint64_t q,
-                                           uint64_t n8q) {
-#pragma unroll
-  for (int i = 0; i < KC; ++i) {
-    const int hm = 1 << (KC - 1 - i);
-    const ulonglong2* __restrict__ tw = tb + (1u << (BL - 1 - H0 + i)) + (g << i);
-#pragma unroll
-    for (int gs = 0; gs < (1 << i); ++gs) {
-      const ulonglong2 W = tw[gs];
-#pragma unroll
-      for (int mm = 0; mm < hm; ++mm) {
-        if (((H0 - i) & 1) == 0)
-          ct_bfly_s<true>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
-        else
-          ct_bfly_s<false>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
-      }
-    }
-  }
-}
-// One forward chunk over all 2^(BL-KC) sets of the block (NS per thread): Load(j) gives
-// element j, Store(r, j0, x) receives set r's transformed elements (positions j0 + m 2^dLog).
-template <int BL, int H0, int KC, class Load, class Store>
-__device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, uint64_t q,
-                                             uint64_t n8q, Load ld, Store st) {
-  constexpr int M = 1 << KC, dLog = H0 - KC + 1, NS = (1 << (BL - KC)) / 256;
-  static_assert(NS >= 1 && dLog >= 0, "chunk plan");
-#pragma unroll
-  for (int r = 0; r < NS; ++r) {
-    const uint32_t s = threadIdx.x + 256u * r;
-    const uint32_t g = (H0 == BL - 1) ? 0u : s >> dLog;  // first chunk: one group
-    const uint32_t j0 = (g << (H0 + 1)) + (s & ((1u << dLog) - 1));
-    const uint32_t pj0 = lpad(j0);
-    uint64_t x[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << dLog), pj0 + lofs<(1 << dLog)>(m));
-    fwd_set_ct<BL, H0, KC>(x, g, tb, q, n8q);
-    st(r, j0, pj0, x);
-  }
-}
 // Inverse (GS) chunk of KC stages starting at local half-size 2^T0: set s -> g = s >> T0,
 // j0 = g 2^(T0+KC) + (s mod 2^T0), elements j0 + m 2^T0; stage-i twiddles are
 // tb[2^l + g 2^(KC-1-i) + gs], gs < 2^(KC-1-i), l = BL - 1 - T0 - i.

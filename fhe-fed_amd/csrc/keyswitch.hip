@@ -353,6 +353,80 @@ __global__ __launch_bounds__(256) void ks_inner_blocks_kernel(const uint64_t* __
   }
 }
 
+// The same inner product at compile-time shape: every foreign digit's block runs its last
+// stages through fwd_block_pass_ct (first chunk straight from ext, per-block twiddle slices of
+// the extended basis) and leaves canonical residues in its own padded LDS slot; then the key
+// products are summed as above.  Dynamic LDS: dn slots of lpad_size(BL) u64.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ks_inner_blocks_ct(const uint64_t* __restrict__ d2e,
+                                                          const uint64_t* __restrict__ ext, uint64_t K, KsArgs a,
+                                                          const ulonglong2* __restrict__ twb,
+                                                          const uint64_t* __restrict__ evk,
+                                                          const uint64_t* __restrict__ evk_sh,
+                                                          uint64_t* __restrict__ accQ, uint64_t* __restrict__ accP) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+  constexpr uint32_t SL = lpad_size(BL);
+  const uint32_t sh = a.logN - BL;
+  const uint64_t row = blockIdx.x >> sh;  // k * T + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint64_t k = row / a.T;
+  const uint32_t t = (uint32_t)(row % a.T);
+  const TowerConst& c = a.te[t];
+  const uint64_t q = c.q;
+  const uint32_t TF = a.Lfull + a.kP;
+  const uint32_t tk = t < a.Ll ? t : a.Lfull + (t - a.Ll);  // the key's tower
+  const uint64_t boff = (uint64_t)b << BL;
+  const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << a.logN) + boff;
+  uint32_t own_mask = 0;
+  for (uint32_t j = 0; j < a.dn; ++j) {
+    uint32_t s, cnt;
+    digit_span(a, j, s, cnt);
+    if (t >= s && t < s + cnt) {
+      own_mask |= 1u << j;
+      continue;
+    }
+    const uint32_t u = t < s ? t : t - cnt;
+    uint64_t* slot = sm + (uint64_t)j * SL;
+    fwd_block_pass_ct<BL, K1, K2, K3, K4>(ext + ext_base(a, j, K) + ((k * (a.T - cnt) + u) << a.logN) + boff, tb,
+                                          q, c.n8q, slot, [&](uint32_t j0, auto& x) {
+                                            const uint32_t pj0 = lpad(j0);
+#pragma unroll
+                                            for (int m = 0; m < (1 << K4); ++m) slot[pj0 + m] = red_any(x[m], c);
+                                          });
+  }
+  __syncthreads();
+  const ulonglong2* own_src = reinterpret_cast<const ulonglong2*>(d2e + ((k * a.Ll + t) << a.logN) + boff);
+  ulonglong2 *o0, *o1;
+  if (t < a.Ll) {
+    o0 = reinterpret_cast<ulonglong2*>(accQ + ((((k * 2 + 0) * a.Ll + t)) << a.logN) + boff);
+    o1 = reinterpret_cast<ulonglong2*>(accQ + ((((k * 2 + 1) * a.Ll + t)) << a.logN) + boff);
+  } else {
+    const uint32_t m = t - a.Ll;
+    o0 = reinterpret_cast<ulonglong2*>(accP + ((((k * 2 + 0) * a.kP + m)) << a.logN) + boff);
+    o1 = reinterpret_cast<ulonglong2*>(accP + ((((k * 2 + 1) * a.kP + m)) << a.logN) + boff);
+  }
+  for (uint32_t p = threadIdx.x; p < (1u << BL) / 2; p += 256) {
+    ulonglong2 u0 = make_ulonglong2(0, 0), u1 = make_ulonglong2(0, 0);
+    for (uint32_t j = 0; j < a.dn; ++j) {
+      const ulonglong2 v = (own_mask & (1u << j))
+                               ? own_src[p]
+                               : *reinterpret_cast<const ulonglong2*>(sm + (uint64_t)j * SL + lpad(2 * p));
+      const uint64_t kb = ((((uint64_t)j * TF + tk)) << a.logN) + boff + 2ull * p;
+      const uint64_t ka = ((((uint64_t)(a.dnFull + j) * TF + tk)) << a.logN) + boff + 2ull * p;
+      const ulonglong2 bv = *reinterpret_cast<const ulonglong2*>(evk + kb);
+      const ulonglong2 bs = *reinterpret_cast<const ulonglong2*>(evk_sh + kb);
+      const ulonglong2 av = *reinterpret_cast<const ulonglong2*>(evk + ka);
+      const ulonglong2 as = *reinterpret_cast<const ulonglong2*>(evk_sh + ka);
+      u0.x = addmod(u0.x, shoup_mul(v.x, bv.x, bs.x, q), q);
+      u0.y = addmod(u0.y, shoup_mul(v.y, bv.y, bs.y, q), q);
+      u1.x = addmod(u1.x, shoup_mul(v.x, av.x, as.x, q), q);
+      u1.y = addmod(u1.y, shoup_mul(v.y, av.y, as.y, q), q);
+    }
+    o0[p] = u0;
+    o1[p] = u1;
+  }
+}
+
 // --------------------------------------------------------------- ModDown ----
 // accP [K][2][kP][N] (COEFFICIENT) -> z [K][2][Ll][N] (COEFFICIENT), P -> Q_l conversion
 __global__ __launch_bounds__(256) void moddown_kernel(const uint64_t* __restrict__ accP, KsArgs a,
@@ -399,6 +473,36 @@ __global__ __launch_bounds__(256) void ks_finish_blocks_kernel(const uint64_t* _
     O[p] = make_ulonglong2(addmod(o.x, shoup_mul(dx, pinv, pinv_sh, q), q),
                            addmod(o.y, shoup_mul(dy, pinv, pinv_sh, q), q));
   }
+}
+
+// The same finish at compile-time shape (fwd_block_pass_ct over the per-block twiddle slices
+// tw_fwd_blk; needs logN > BL and every q_t >= 2^40 for red_any): z's last stages run on the
+// registers of the chunk passes and the finish reads them from registers.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ks_finish_blocks_ct(const uint64_t* __restrict__ z,
+                                                           const uint64_t* __restrict__ accQ, KsArgs a,
+                                                           const ulonglong2* __restrict__ twb,
+                                                           uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sh = a.logN - BL;
+  const uint64_t row = blockIdx.x >> sh;  // (k * 2 + poly) * Ll + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint32_t t = (uint32_t)(row % a.Ll);
+  const TowerConst& c = a.tq[t];
+  const uint64_t q = c.q, pinv = a.pinv[t], pinv_sh = a.pinv_sh[t];
+  const uint64_t off = (row << a.logN) + ((uint64_t)b << BL);
+  const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << a.logN) + ((uint64_t)b << BL);
+  fwd_block_pass_ct<BL, K1, K2, K3, K4>(z + off, tb, q, c.n8q, sm, [&](uint32_t j0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K4); m += 2) {
+      const ulonglong2 aq = *reinterpret_cast<const ulonglong2*>(accQ + off + j0 + m);
+      ulonglong2* O = reinterpret_cast<ulonglong2*>(out + off + j0 + m);
+      const ulonglong2 o = *O;
+      const uint64_t dx = submod(aq.x, red_any(x[m], c), q), dy = submod(aq.y, red_any(x[m + 1], c), q);
+      *O = make_ulonglong2(addmod(o.x, shoup_mul(dx, pinv, pinv_sh, q), q),
+                           addmod(o.y, shoup_mul(dy, pinv, pinv_sh, q), q));
+    }
+  });
 }
 
 size_t ks_scratch_bytes(uint32_t Ll, uint32_t kP, uint32_t dn, uint32_t alpha, uint32_t N, uint64_t K) {
@@ -458,11 +562,17 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
   SHELFI_HIP(hipGetLastError());
   // last NTT stages + the key inner product (one LDS block per digit; > 64 KiB only for
   // 2^12-element blocks with 3 digits, which a gfx950 workgroup may still declare)
-  if (lds * a.dn > 65536)
-    SHELFI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ks_inner_blocks_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds * a.dn)));
-  hipLaunchKernelGGL(ks_inner_blocks_kernel, grid(K * a.T, nb), dim3(256), lds * a.dn, s, d2e, ext, K, a, blkLog,
-                     dte.psi_rev, dte.psi_rev_sh, evk, evk_sh, accQ, accP);
+  if (sh > 0 && blkLog == 11 && dte.red_ok) {
+    hipLaunchKernelGGL((ks_inner_blocks_ct<11, 3, 3, 3, 2>), grid(K * a.T, nb), dim3(256),
+                       sizeof(uint64_t) * lpad_size(11) * a.dn, s, d2e, ext, K, a, dte.tw_fwd_blk, evk, evk_sh, accQ,
+                       accP);
+  } else {
+    if (lds * a.dn > 65536)
+      SHELFI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ks_inner_blocks_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds * a.dn)));
+    hipLaunchKernelGGL(ks_inner_blocks_kernel, grid(K * a.T, nb), dim3(256), lds * a.dn, s, d2e, ext, K, a, blkLog,
+                       dte.psi_rev, dte.psi_rev_sh, evk, evk_sh, accQ, accP);
+  }
   SHELFI_HIP(hipGetLastError());
   // ModDown: INTT of the P part, P -> Q_l conversion, its NTT fused with the finish
   launch_ntt(accP, K * 2 * a.kP, a.kP, a.logN, true, tower_view(dte, a.Ll, N), s);
@@ -475,8 +585,15 @@ void launch_eval_mult(const KsArgs& a, const DeviceTables& dtq, const DeviceTabl
     launch_ntt_cols(z, K * 2 * a.Ll, a.Ll, a.logN, false, dtq, s);
   }
   SHELFI_HIP(hipGetLastError());
-  hipLaunchKernelGGL(ks_finish_blocks_kernel, grid(K * 2 * a.Ll, nb), dim3(256), lds, s, z, accQ, a, blkLog,
-                     dtq.psi_rev, dtq.psi_rev_sh, out);
+  if (sh > 0 && blkLog == 11 && dtq.red_ok)
+    hipLaunchKernelGGL((ks_finish_blocks_ct<11, 3, 3, 3, 2>), grid(K * 2 * a.Ll, nb), dim3(256), 0, s, z, accQ, a,
+                       dtq.tw_fwd_blk, out);
+  else if (sh > 0 && blkLog == 12 && dtq.red_ok)
+    hipLaunchKernelGGL((ks_finish_blocks_ct<12, 3, 3, 3, 3>), grid(K * 2 * a.Ll, nb), dim3(256), 0, s, z, accQ, a,
+                       dtq.tw_fwd_blk, out);
+  else
+    hipLaunchKernelGGL(ks_finish_blocks_kernel, grid(K * 2 * a.Ll, nb), dim3(256), lds, s, z, accQ, a, blkLog,
+                       dtq.psi_rev, dtq.psi_rev_sh, out);
   SHELFI_HIP(hipGetLastError());
 }
 
@@ -535,6 +652,36 @@ size_t rescale_scratch_bytes(uint32_t Ll, uint32_t N, uint64_t K) {
   return K * 2ull * N * 8 * (1 + (uint64_t)(Ll - 1)) + 64;  // last | v
 }
 
+// The same finish at compile-time shape (see ks_finish_blocks_ct).
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void rescale_finish_blocks_ct(const uint64_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ v, uint32_t Lo,
+                                                                uint32_t logN, const ulonglong2* __restrict__ twb,
+                                                                const TowerConst* __restrict__ tq, RescaleConst rc,
+                                                                uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sh = logN - BL;
+  const uint64_t row = blockIdx.x >> sh;  // (k * 2 + poly) * Lo + t
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint64_t kp = row / Lo;
+  const uint32_t t = (uint32_t)(row % Lo);
+  const TowerConst& c = tq[t];
+  const uint64_t q = c.q, w = rc.qlinv[t], wp = rc.qlinv_sh[t];
+  const uint64_t boff = (uint64_t)b << BL;
+  const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + boff;
+  const uint64_t* __restrict__ X = in + ((kp * (Lo + 1) + t) << logN) + boff;
+  uint64_t* __restrict__ O = out + (row << logN) + boff;
+  fwd_block_pass_ct<BL, K1, K2, K3, K4>(v + (row << logN) + boff, tb, q, c.n8q, sm, [&](uint32_t j0, auto& y) {
+#pragma unroll
+    for (int m = 0; m < (1 << K4); m += 2) {
+      const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(X + j0 + m);
+      *reinterpret_cast<ulonglong2*>(O + j0 + m) =
+          make_ulonglong2(shoup_mul(submod(x.x, red_any(y[m], c), q), w, wp, q),
+                          shoup_mul(submod(x.y, red_any(y[m + 1], c), q), w, wp, q));
+    }
+  });
+}
+
 void launch_rescale(const DeviceTables& dt, uint32_t Ll, uint32_t logN, const RescaleConst& rc,
                     const uint64_t* in, uint64_t K, uint64_t* out, void* scratch, hipStream_t s) {
   if (!K) return;
@@ -552,9 +699,16 @@ void launch_rescale(const DeviceTables& dt, uint32_t Ll, uint32_t logN, const Re
   SHELFI_HIP(hipGetLastError());
   launch_ntt_cols(v, rows, Lo, logN, false, dt, s);
   const uint32_t blkLog = ntt_block_log(logN);
-  hipLaunchKernelGGL(rescale_finish_blocks_kernel, dim3((uint32_t)(rows << (logN - blkLog))), dim3(256),
-                     sizeof(uint64_t) << blkLog, s, in, v, Lo, logN, blkLog, dt.psi_rev, dt.psi_rev_sh, dt.tc, rc,
-                     out);
+  const dim3 nbf((uint32_t)(rows << (logN - blkLog)));
+  if (logN > blkLog && blkLog == 11 && dt.red_ok)
+    hipLaunchKernelGGL((rescale_finish_blocks_ct<11, 3, 3, 3, 2>), nbf, dim3(256), 0, s, in, v, Lo, logN,
+                       dt.tw_fwd_blk, dt.tc, rc, out);
+  else if (logN > blkLog && blkLog == 12 && dt.red_ok)
+    hipLaunchKernelGGL((rescale_finish_blocks_ct<12, 3, 3, 3, 3>), nbf, dim3(256), 0, s, in, v, Lo, logN,
+                       dt.tw_fwd_blk, dt.tc, rc, out);
+  else
+    hipLaunchKernelGGL(rescale_finish_blocks_kernel, nbf, dim3(256), sizeof(uint64_t) << blkLog, s, in, v, Lo,
+                       logN, blkLog, dt.psi_rev, dt.psi_rev_sh, dt.tc, rc, out);
   SHELFI_HIP(hipGetLastError());
 }
 
