@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-ciphertext counters of one EvalMult and one ModReduce (tools/f4_time.py K 0 under
 rocprofv3 --pmc): the mult is every dispatch from the first ks_tensor_intt_kernel to the last
-ks_finish_blocks_kernel, the rescale the dispatches after it up to rescale_finish_blocks_kernel.
+ks_finish_blocks (kernel or _ct), the rescale the dispatches after it up to rescale_finish_blocks (kernel or _ct).
 usage: f4_counters.py K counter_collection.csv [more.csv ...] -o out.json
 Counters summed per phase and divided by K; FETCH_SIZE is doubled (the gfx950 correction of
 MI355X_MICROARCH.md) and reported with WRITE_SIZE as HBM bytes."""
@@ -14,8 +14,8 @@ import json
 def phases(rows):
     order = sorted({(int(r["Dispatch_Id"]), r["Kernel_Name"]) for r in rows})
     first = next(i for i, (_, k) in enumerate(order) if "ks_tensor_intt_kernel" in k)
-    last_m = max(i for i, (_, k) in enumerate(order) if "ks_finish_blocks_kernel" in k)
-    last_r = max(i for i, (_, k) in enumerate(order) if "rescale_finish_blocks_kernel" in k)
+    last_m = max(i for i, (_, k) in enumerate(order) if "ks_finish_blocks" in k)
+    last_r = max(i for i, (_, k) in enumerate(order) if "rescale_finish_blocks" in k)
     ph = {}
     for i, (d, _) in enumerate(order):
         if first <= i <= last_m:
