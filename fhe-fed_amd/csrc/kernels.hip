@@ -644,6 +644,66 @@ __global__ __launch_bounds__(256) void ntt_inv_cols(uint64_t* __restrict__ polys
     default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};                  \
   }
 
+// launch_ntt's block passes at compile-time shape (rings with a columns pass whose blocks are
+// 2^11 or 2^12 elements and every q >= 2^40), in place over the per-block twiddle slices:
+// forward after ntt_fwd_cols (inputs < 8q, canonical outputs), inverse before ntt_inv_cols
+// (canonical inputs, lazy outputs below 8q).  A workgroup reads its whole block in the first
+// chunk, before any of its writes.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ntt_fwd_blocks_ct(uint64_t* polys, uint32_t L, uint32_t logN,
+                                                         const ulonglong2* __restrict__ twb,
+                                                         const TowerConst* __restrict__ tcs) {
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sh = logN - BL;
+  const uint64_t poly = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint32_t t = (uint32_t)(poly % L);
+  const TowerConst& c = tcs[t];
+  uint64_t* base = polys + (poly << logN) + ((uint64_t)b << BL);
+  fwd_block_pass_ct<BL, K1, K2, K3, K4>(base, twb + ((uint64_t)t << logN) + ((uint64_t)b << BL), c.q, c.n8q, sm,
+                                        [&](uint32_t j0, auto& x) {
+#pragma unroll
+                                          for (int m = 0; m < (1 << K4); m += 2)
+                                            *reinterpret_cast<ulonglong2*>(base + j0 + m) =
+                                                make_ulonglong2(red_any(x[m], c), red_any(x[m + 1], c));
+                                        });
+}
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(256) void ntt_inv_blocks_ct(uint64_t* polys, uint32_t L, uint32_t logN,
+                                                         const ulonglong2* __restrict__ twb,
+                                                         const TowerConst* __restrict__ tcs) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sh = logN - BL;
+  const uint64_t poly = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  const uint32_t t = (uint32_t)(poly % L);
+  const uint64_t q = tcs[t].q, n8q = tcs[t].n8q;
+  uint64_t* base = polys + (poly << logN) + ((uint64_t)b << BL);
+  const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
+  inv_chunk_ct<BL, 0, K1, false>(tb, q, n8q, [&](uint32_t j, uint32_t) { return base[j]; },
+                                 [&](int, uint32_t, uint32_t pj0, auto& x) {
+#pragma unroll
+                                   for (int m = 0; m < (1 << K1); ++m) sm[pj0 + lofs<1>(m)] = x[m];
+                                 });
+  __syncthreads();
+  inv_chunk_ct<BL, K1, K2, true>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << K1)>(m)] = x[m];
+  });
+  __syncthreads();
+  inv_chunk_ct<BL, K1 + K2, K3, true>(tb, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (K1 + K2))>(m)] = x[m];
+  });
+  __syncthreads();
+  inv_chunk_ct<BL, BL - K4, K4, true>(tb, q, n8q, lds_ld, [&](int, uint32_t j0, uint32_t, auto& x) {
+#pragma unroll
+    for (int m = 0; m < (1 << K4); ++m) base[j0 + (m << (BL - K4))] = x[m];
+  });
+}
+
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                 const DeviceTables& dt, hipStream_t s) {
   if (!P) return;
@@ -661,12 +721,26 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
       NTT_DISPATCH(logR, ntt_fwd_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
                    dt.psi_rev, dt.psi_rev_sh, dt.tc);
     }
-    hipLaunchKernelGGL(ntt_fwd_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
-                       logN, (uint32_t)logR, dt.psi_rev, dt.psi_rev_sh, dt.tc);
+    if (logR > 0 && blkLog == 11 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_fwd_blocks_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbBlocks), dim3(256), 0, s, polys, L,
+                         logN, dt.tw_fwd_blk, dt.tc);
+    else if (logR > 0 && blkLog == 12 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_fwd_blocks_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0, s, polys, L,
+                         logN, dt.tw_fwd_blk, dt.tc);
+    else
+      hipLaunchKernelGGL(ntt_fwd_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
+                         logN, (uint32_t)logR, dt.psi_rev, dt.psi_rev_sh, dt.tc);
   } else {
-    hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
-                       logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0,
-                       (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr);
+    if (logR > 0 && blkLog == 11 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0, s, polys, L,
+                         logN, dt.tw_inv_blk, dt.tc);
+    else if (logR > 0 && blkLog == 12 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0, s, polys, L,
+                         logN, dt.tw_inv_blk, dt.tc);
+    else
+      hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
+                         logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0,
+                         (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr);
     if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
