@@ -46,6 +46,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_CLOCK_GHZ = 2.4  # MI355X peak engine clock
 VALU_CYCLES_PER_INST = 4.0  # one wave64 VOP3 instruction per SIMD (tools/valu_rates.hip, profiles/r02_valu_rates.txt)
 COMM_CHECK_TIMEOUT_S = 120  # the C-ABI communicator check at N > 1 (main(): c_abi_comm_check)
+COMM_HANG_EXIT = 3  # exit status when a collective never returned
 # name -> (slots, multDepth, params per learner, learners per GPU, description)
 WORKLOADS = {
     "cfg2": (16384, 3, 61_706, 16, "LeNet-5"),
@@ -740,9 +741,10 @@ def main():
 
         def watchdog():
             if not finished.wait(COMM_CHECK_TIMEOUT_S):
-                res["c_abi_comm_check"] = {"ok": False, "error": "no result within %d s; exited" % COMM_CHECK_TIMEOUT_S}
+                res["c_abi_comm_check"] = {"ok": False, "error": "no result within %d s; exited with status %d"
+                                           % (COMM_CHECK_TIMEOUT_S, COMM_HANG_EXIT)}
                 emit()
-                os._exit(0)
+                os._exit(COMM_HANG_EXIT)  # the line is written, but a hung collective fails the run
         threading.Thread(target=watchdog, daemon=True).start()
         if main_mode["shard"] == "learners" and args.combine == "torch":
             res["c_abi_comm_check"] = c_abi_comm_check()

@@ -161,6 +161,7 @@ class CKKS(Scheme):
     # ---------------------------------------------------------- keys (a2/a3) --
     def loadCryptoParams(self) -> None:
         """ckks.cpp:11-23: failures are printed, never raised."""
+        self._params_gen = getattr(self, "_params_gen", 0) + 1  # N / L may change (device._ln)
         rc = self._lib.shelfi_load(self._ctx, self.cryptodir.encode())
         if rc != 0:
             print("Could not read serialization from %scryptocontext.txt: %s"
@@ -168,6 +169,7 @@ class CKKS(Scheme):
 
     def genCryptoContextAndKeyGen(self) -> int:
         """ckks.cpp:25-59: returns 1 on success, 0 on a file-write error."""
+        self._params_gen = getattr(self, "_params_gen", 0) + 1
         rc = self._lib.shelfi_keygen(self._ctx, self.cryptodir.encode())
         if rc == _lib.SHELFI_ERR_IO:
             print("Error writing serialization: %s"

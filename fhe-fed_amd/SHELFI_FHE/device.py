@@ -39,13 +39,16 @@ def empty_ct(ckks, K: int, device=None):
 
 
 def _ln(ckks):
-    """(L, N) of a context: fixed at construction, cached (info() is a library call and a
-    dict build, too slow for the per-launch path of small aggregations)."""
+    """(L, N) of a context, cached (info() is a library call and a dict build, too slow for
+    the per-launch path of small aggregations).  The cache is keyed on the context's
+    parameter generation: loadCryptoParams / genCryptoContextAndKeyGen can change N and L
+    (PALISADE files carry their own ring), and bump it (SHELFI_FHE.CKKS._params_gen)."""
+    gen = getattr(ckks, "_params_gen", 0)
     ln = getattr(ckks, "_dev_ln", None)
-    if ln is None:
+    if ln is None or ln[0] != gen:
         inf = ckks.info()
-        ln = ckks._dev_ln = (inf["num_towers"], inf["ring_dim"])
-    return ln
+        ln = ckks._dev_ln = (gen, inf["num_towers"], inf["ring_dim"])
+    return ln[1], ln[2]
 
 
 def _check_ct(t, ckks, K=None, any_level=False):
@@ -95,22 +98,23 @@ class Arena:
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
 
     def put(self, learner: int, ct):
-        """Place learner `learner`'s batch: a [K][2][L][N] CUDA tensor or a blob (bytes)."""
+        """Place learner `learner`'s batch: a [K][2][L][N] CUDA tensor, or its upload as it
+        came over the wire (a library blob or a PALISADE archive, bytes-like).  An upload's
+        header is checked against the context (parameters, key, length, K) before any copy;
+        every put then checks that each placed residue is < q_t, and a refused slot keeps
+        wavg() failing until a valid put replaces it (shelfi_dev_arena_put[_blob])."""
         if isinstance(ct, (bytes, bytearray, memoryview)):
-            from . import blob_info
             import numpy as np
 
-            b = bytes(ct)
-            if blob_info(b)["num_cts"] != self.K:
-                raise ValueError("blob holds a different number of ciphertexts")
-            hdr = _lib.load().shelfi_blob_header_bytes()
-            host = np.frombuffer(b, dtype=np.uint8, offset=hdr)
-            check(_lib.load().shelfi_dev_arena_put(self.ckks._ctx, C.c_void_p(host.ctypes.data), 1, self.K,
-                                                   int(learner), self.C, C.c_void_p(self.buf.data_ptr()),
-                                                   C.c_void_p(_stream_ptr(self.buf))), "arena_put")
-            _torch().cuda.synchronize(self.buf.device)  # host buffer must outlive the copy
+            host = np.frombuffer(ct, dtype=np.uint8)
+            check(_lib.load().shelfi_dev_arena_put_blob(self.ckks._ctx, C.c_void_p(host.ctypes.data), host.size,
+                                                        self.K, int(learner), self.C,
+                                                        C.c_void_p(self.buf.data_ptr()),
+                                                        C.c_void_p(_stream_ptr(self.buf))), "arena_put")
             return
         _check_ct(ct, self.ckks, self.K)
+        if ct.device != self.buf.device:
+            raise ValueError("the batch must live on the arena's device")
         check(_lib.load().shelfi_dev_arena_put(self.ckks._ctx, C.c_void_p(ct.data_ptr()), 0, self.K,
                                                int(learner), self.C, C.c_void_p(self.buf.data_ptr()),
                                                C.c_void_p(_stream_ptr(ct))), "arena_put")
@@ -204,10 +208,13 @@ def mult(ckks, a, b, out=None):
     _check_ct(b, ckks, a.shape[0], any_level=True)
     if a.shape != b.shape:
         raise ValueError("EvalMult operands must have the same shape (same level)")
+    if b.device != a.device:
+        raise ValueError("EvalMult operands must live on the same device")
     if out is None:
         out = torch.empty_like(a)
-    if out.shape != a.shape or not out.is_contiguous():
-        raise ValueError("out must be a contiguous tensor shaped like a")
+    _check_ct(out, ckks, a.shape[0], any_level=True)
+    if out.shape != a.shape or out.device != a.device:
+        raise ValueError("out must be a contiguous tensor shaped like a, on a's device")
     check(_lib.load().shelfi_dev_mult(ckks._ctx, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.shape[0],
                                       int(a.shape[2]), C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(a))),
           "dev_mult")
@@ -224,8 +231,9 @@ def rescale(ckks, ct, out=None):
         raise ValueError("ModReduce needs at least 2 towers")
     if out is None:
         out = torch.empty((K, 2, l - 1, N), dtype=ct.dtype, device=ct.device)
-    if tuple(out.shape) != (K, 2, l - 1, N) or not out.is_contiguous() or out.element_size() != 8:
-        raise ValueError("out must be a contiguous [K][2][l-1][N] 64-bit tensor")
+    _check_ct(out, ckks, K, any_level=True)
+    if tuple(out.shape) != (K, 2, l - 1, N) or out.device != ct.device:
+        raise ValueError("out must be a contiguous [K][2][l-1][N] 64-bit tensor on ct's device")
     check(_lib.load().shelfi_dev_rescale(ckks._ctx, C.c_void_p(ct.data_ptr()), K, int(l),
                                          C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(ct))), "dev_rescale")
     return out

@@ -553,7 +553,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
-    SHELFI_HIP(hipMalloc(&ctx->dev_flag, 16));
+    SHELFI_HIP(hipMalloc(&ctx->dev_flag, 32));
     set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
   });
   if (rc != SHELFI_OK) {
@@ -1314,9 +1314,45 @@ size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K) {
   return C * K * 2ull * ctx->p.L * ctx->p.N;
 }
 
+// Validation of a freshly placed arena slot: one read of the learner's slices for residues
+// >= q_t (~0.2 ms of HBM per 1.4 GiB, against ~30 ms of PCIe for the upload), then the
+// slot's refusal mark is set or cleared.  Synchronises `s`.  Called under the ctx lock.
+static void arena_validate(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t K, size_t learner, size_t C,
+                           hipStream_t s) {
+  const Params& p = ctx->p;
+  uint32_t* bad = ctx->dev_flag + 4;
+  SHELFI_HIP(hipMemsetAsync(bad, 0, 4, s));
+  launch_arena_check(arena_dev, (uint32_t)C, (uint32_t)learner, (uint64_t)K * 2 * p.L, p.L, p.logN,
+                     ctx->dt.tc, bad, s);
+  uint32_t flag = 0;
+  SHELFI_HIP(hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, s));
+  SHELFI_HIP(hipStreamSynchronize(s));
+  auto& R = ctx->arena_refused;
+  for (size_t i = 0; i < R.size();)  // this slot's earlier refusal, if any, is superseded
+    if (R[i].arena == arena_dev && R[i].learner == learner) R.erase(R.begin() + (long)i);
+    else ++i;
+  if (flag) {
+    R.push_back({arena_dev, C * K * 2ull * p.L * p.N, learner});
+    throw Error{SHELFI_ERR_FORMAT,
+                "learner " + std::to_string(learner) +
+                    ": ciphertext residue >= its tower modulus (malformed upload; the arena slot is "
+                    "marked refused until a valid upload replaces it)"};
+  }
+}
+
+// An aggregation over arena words [a, a + words) must not read a refused slot.
+static void arena_require_valid(shelfi_ctx* ctx, const uint64_t* a, size_t words) {
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  for (const auto& r : ctx->arena_refused)
+    if (a < r.arena + r.words && r.arena < a + words)
+      throw Error{SHELFI_ERR_STATE, "the arena holds a refused upload for learner " +
+                                        std::to_string(r.learner) + "; put a valid batch first"};
+}
+
 int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size_t K, size_t learner,
                          size_t C, uint64_t* arena_dev, void* stream) {
   if (!ctx || !arena_dev || (K && !src) || learner >= C) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     DeviceGuard g(ctx->device);
     const size_t total = K * 2ull * ctx->p.L * ctx->p.N;  // residues per learner
@@ -1326,6 +1362,35 @@ int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size
                                 row_bytes, rows,
                                 src_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
                                 (hipStream_t)stream));
+    arena_validate(ctx, arena_dev, K, learner, C, (hipStream_t)stream);
+  });
+}
+
+int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t K, size_t learner,
+                              size_t C, uint64_t* arena_dev, void* stream) {
+  if (!ctx || !arena_dev || !blob || learner >= C) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    // header first, against the context (parameters, key tag / key id), before any copy
+    const CtLayout v = open_cts(ctx, blob, len);
+    if (v.K != K)
+      throw Error{SHELFI_ERR_FORMAT, "upload holds " + std::to_string(v.K) + " ciphertexts, the arena " +
+                                         std::to_string(K)};
+    if (!K) return;
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t row_bytes = kArenaChunk * 8;
+    std::vector<HostPiece> pcs;
+    v.pieces(0, K, p, pcs);  // a blob: one payload run; an archive: 2 L tower runs per ciphertext
+    size_t r0 = 0;           // first chunk row of the next piece
+    for (const HostPiece& pc : pcs) {
+      const size_t rows = pc.n / row_bytes;
+      SHELFI_HIP(hipMemcpy2DAsync(arena_dev + (r0 * C + learner) * kArenaChunk, C * row_bytes, pc.p,
+                                  row_bytes, row_bytes, rows, hipMemcpyHostToDevice, s));
+      r0 += rows;
+    }
+    arena_validate(ctx, arena_dev, K, learner, C, s);
   });
 }
 
@@ -1335,6 +1400,7 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
   return guarded([&] {
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
     check_weights(w, C, ctx->p.delta);
+    arena_require_valid(ctx, arena_dev, C * K * 2ull * ctx->p.L * ctx->p.N);
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners

@@ -19,7 +19,8 @@ namespace shelfi {
 constexpr int kMaxDigits = 3;  // ComputeNumLargeDigits never exceeds 3
 
 struct LevelState {
-  bool built = false;
+  bool built = false;  // key-switching state (ext, dtf, ks, args)
+  bool q_built = false;
   bool own_q = false;  // q tables built here (levels below L); level L uses ctx->dt
   DeviceTables q;      // Q_l: NTT + CRT tables (decrypt at this level)
   DeviceTables ext;    // Q_l u P (key switching)
@@ -31,6 +32,7 @@ struct LevelState {
 struct EvalState {
   uint32_t dnum = 0, alpha = 0, kP = 0;
   uint64_t p[kMaxTowers] = {0}, ppsi[kMaxTowers] = {0};
+  std::string ks_error;        // why this chain cannot key-switch ("" = it can)
   uint64_t* evk = nullptr;     // [2][dnum][L + kP][N] (b-vector, a-vector)
   uint64_t* evk_sh = nullptr;  // Shoup companions
   std::vector<uint64_t> evk_host;
@@ -39,13 +41,20 @@ struct EvalState {
 
 static uint64_t mm(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)(((u128)a * b) % q); }
 
-static void free_level(LevelState& l) {
-  if (l.own_q) {
-    free_ntt_tables(l.q);
-  }
+// key-switching state of a level (its Q_l tables stay: decrypt at the level uses them)
+static void free_level_ks(LevelState& l) {
   free_ntt_tables(l.ext);
   for (auto& d : l.dtf) free_ntt_tables(d);
   dfree_t(l.ks);
+  l.ext = DeviceTables{};
+  for (auto& d : l.dtf) d = DeviceTables{};
+  l.args = KsArgs{};
+  l.built = false;
+}
+
+static void free_level(LevelState& l) {
+  if (l.own_q) free_ntt_tables(l.q);
+  free_level_ks(l);
   l = LevelState{};
 }
 
@@ -61,41 +70,65 @@ void eval_release(shelfi_ctx* ctx, bool keys_only) {
   ctx->ev = nullptr;
 }
 
+// Per-context level state.  The special primes are derived here, but a chain that cannot
+// key-switch (L + kP > 16) only fails EvalMult: decrypt and ModReduce at any level need
+// nothing but the Q_l tables.
 static EvalState& eval_state(shelfi_ctx* ctx) {
   if (ctx->ev) return *ctx->ev;
   const Params& p = ctx->p;
   auto ev = new EvalState();
-  special_primes(p.N, p.L, p.q, &ev->dnum, &ev->alpha, &ev->kP, ev->p, ev->ppsi);
-  if (p.L + ev->kP > (uint32_t)kMaxTowers) {
-    delete ev;
-    throw Error{SHELFI_ERR_ARG, "EvalMult needs num_towers + special primes <= 16"};
+  try {
+    special_primes(p.N, p.L, p.q, &ev->dnum, &ev->alpha, &ev->kP, ev->p, ev->ppsi);
+    if (p.L + ev->kP > (uint32_t)kMaxTowers) ev->ks_error = "EvalMult needs num_towers + special primes <= 16";
+  } catch (const Error& e) {
+    ev->ks_error = e.msg;
   }
   ctx->ev = ev;
   return *ev;
 }
 
-// Tables and key-switching constants for ciphertexts of Ll towers (Q_l = q_0 .. q_{Ll-1}).
-static LevelState& level(shelfi_ctx* ctx, uint32_t Ll) {
+// NTT + CRT tables of Q_l = q_0 .. q_{Ll-1} (decrypt at a level): built on first use, no
+// key-switching state.
+static const DeviceTables& level_q(shelfi_ctx* ctx, uint32_t Ll) {
   EvalState& ev = eval_state(ctx);
   const Params& P0 = ctx->p;
   if (Ll < 1 || Ll > P0.L) throw Error{SHELFI_ERR_ARG, "tower count out of range for this context"};
   LevelState& l = ev.lv[Ll];
+  if (l.q_built) return l.q;
+  if (Ll == P0.L) {
+    l.q = ctx->dt;
+    l.own_q = false;
+  } else {
+    Params pl = P0;
+    pl.L = Ll;
+    DeviceTables q;
+    try {
+      build_ntt_tables(pl, q);
+    } catch (...) {
+      free_ntt_tables(q);
+      throw;
+    }
+    l.q = q;
+    l.own_q = true;
+    l.q.fft_inv = ctx->dt.fft_inv;  // shared, owned by the context
+    l.q.fft_fwd = ctx->dt.fft_fwd;
+    l.q.cdt = ctx->dt.cdt;
+    l.q.cdt_len = ctx->dt.cdt_len;
+  }
+  l.q_built = true;
+  return l.q;
+}
+
+// Tables and key-switching constants for ciphertexts of Ll towers (Q_l = q_0 .. q_{Ll-1}).
+static LevelState& level(shelfi_ctx* ctx, uint32_t Ll) {
+  EvalState& ev = eval_state(ctx);
+  if (!ev.ks_error.empty()) throw Error{SHELFI_ERR_ARG, ev.ks_error};
+  const Params& P0 = ctx->p;
+  level_q(ctx, Ll);
+  LevelState& l = ev.lv[Ll];
   if (l.built) return l;
   const uint32_t kP = ev.kP, T = Ll + kP, al = ev.alpha, dn = (Ll + al - 1) / al;
   try {
-    if (Ll == P0.L) {
-      l.q = ctx->dt;
-      l.own_q = false;
-    } else {
-      Params pl = P0;
-      pl.L = Ll;
-      build_ntt_tables(pl, l.q);
-      l.own_q = true;
-      l.q.fft_inv = ctx->dt.fft_inv;  // shared, owned by the context
-      l.q.fft_fwd = ctx->dt.fft_fwd;
-      l.q.cdt = ctx->dt.cdt;
-      l.q.cdt_len = ctx->dt.cdt_len;
-    }
     Params pe = P0;
     pe.L = T;
     for (uint32_t m = 0; m < kP; ++m) {
@@ -186,18 +219,19 @@ static LevelState& level(shelfi_ctx* ctx, uint32_t Ll) {
     a.tq = ctx->dt.tc;  // q / Shoup constants only: the context's prefix serves every level
     a.te = l.ext.tc;
   } catch (...) {
-    free_level(l);
+    free_level_ks(l);
     throw;
   }
   l.built = true;
   return l;
 }
 
-// tables of Q_l for decrypt at a level (api.cpp)
-const DeviceTables& level_tables(shelfi_ctx* ctx, uint32_t Ll) { return level(ctx, Ll).q; }
+// tables of Q_l for decrypt at a level (api.cpp): the Q_l tables alone
+const DeviceTables& level_tables(shelfi_ctx* ctx, uint32_t Ll) { return level_q(ctx, Ll); }
 
 static void install_evk(shelfi_ctx* ctx, EvalState& ev, const uint64_t* evk) {
   const Params& p = ctx->p;
+  if (!ev.ks_error.empty()) throw Error{SHELFI_ERR_ARG, ev.ks_error};
   const uint32_t T0 = p.L + ev.kP;
   const size_t TN = (size_t)T0 * p.N, words = 2ull * ev.dnum * TN;
   std::vector<uint64_t> sh(words);
@@ -467,6 +501,13 @@ int shelfi_dev_mult(shelfi_ctx* ctx, const uint64_t* a_dev, const uint64_t* b_de
       throw Error{SHELFI_ERR_STATE, "no evaluation key: call evalMultKeyGen() first"};
     LevelState& l = level(ctx, towers);
     if (!K) return;
+    // out may alias a or b exactly (each workgroup reads its inputs before writing that
+    // ciphertext's output); a shifted overlap would let one chunk's writes corrupt inputs
+    // another has not read yet
+    const uint64_t words = 2ull * towers * ctx->p.N * K;
+    for (const uint64_t* in : {a_dev, b_dev})
+      if (out_dev != in && out_dev < in + words && in < out_dev + words)
+        throw Error{SHELFI_ERR_ARG, "EvalMult output must be an input exactly or not overlap the inputs"};
     const KsArgs& a = l.args;
     const uint32_t N = ctx->p.N;
     hipStream_t s = (hipStream_t)stream;

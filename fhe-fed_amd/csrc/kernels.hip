@@ -195,6 +195,32 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   SHELFI_HIP(hipGetLastError());
 }
 
+// Upload validation of an arena slot (shelfi_dev_arena_put*): every residue of learner
+// `learner`'s slices must be canonical (< q_t) — the carry-free limb sums of wavg_kernel
+// drop bits >= 2^60 and would otherwise return a silently wrong aggregate.  One thread =
+// 2 residues of one 512-residue slice (a block = one chunk row); reads 1/C of the arena.
+__global__ __launch_bounds__(256) void arena_check_kernel(const uint64_t* __restrict__ arena, uint32_t C,
+                                                          uint32_t learner, uint32_t L, uint32_t logN,
+                                                          const TowerConst* __restrict__ tcs,
+                                                          uint32_t* __restrict__ bad) {
+  const uint64_t r = blockIdx.x;  // chunk row: residues [r 512, (r + 1) 512) of the learner's batch
+  const uint32_t t = (uint32_t)(((r * kArenaChunk) >> logN) % L);
+  const uint64_t q = tcs[t].q;
+  const u32x4 v = __builtin_nontemporal_load(
+      reinterpret_cast<const u32x4*>(arena + (r * C + learner) * kArenaChunk + 2u * threadIdx.x));
+  if ((((uint64_t)v.y << 32) | v.x) >= q || (((uint64_t)v.w << 32) | v.z) >= q) atomicOr(bad, 1u);
+}
+
+void launch_arena_check(const uint64_t* arena, uint32_t C, uint32_t learner, uint64_t rows, uint32_t L,
+                        uint32_t logN, const TowerConst* tc, uint32_t* bad, hipStream_t s) {
+  const uint64_t blocks = (rows << logN) / kArenaChunk;
+  if (!blocks) return;
+  if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "arena too large"};
+  hipLaunchKernelGGL(arena_check_kernel, dim3((uint32_t)blocks), dim3(kArenaChunk / 2), 0, s, arena, C,
+                     learner, L, logN, tc, bad);
+  SHELFI_HIP(hipGetLastError());
+}
+
 // A collective's uint64 sum of G <= 15 partial sums (each < q < 2^60) -> [0, q).
 __global__ __launch_bounds__(256) void modq_kernel(uint64_t* buf, uint32_t L, uint32_t logN,
                                                    const TowerConst* __restrict__ tcs) {

@@ -169,7 +169,16 @@ struct shelfi_ctx {
   uint64_t seed = 0;          // 0 -> OS entropy per call
   uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
   uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
-                                 // [2] max decode logError (noise flooding)
+                                 // [2] max decode logError (noise flooding), [3] bytes-API
+                                 // upload residue >= q, [4] arena upload residue >= q
+  // arena slots whose last upload was refused (shelfi_dev_arena_put*): an aggregation
+  // over an arena range holding one fails instead of summing the refused residues
+  struct ArenaRefusal {
+    const uint64_t* arena;
+    size_t words;  // C * K * 2 * L * N of that arena
+    size_t learner;
+  };
+  std::vector<ArenaRefusal> arena_refused;
   int decode_noise = 1;          // shelfi_set_decode_noise (PALISADE floods every decode)
   double decode_m_factor = 1.0;
   int last_log_error = -1;       // of the last flooded decrypt, -1 if none
@@ -215,6 +224,9 @@ void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint3
                             hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
+// flags *bad when a residue of learner `learner`'s slices of an arena of C learners is >= q_t
+void launch_arena_check(const uint64_t* arena, uint32_t C, uint32_t learner, uint64_t rows, uint32_t L,
+                        uint32_t logN, const TowerConst* tc, uint32_t* bad, hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                 const DeviceTables& dt, hipStream_t s);
 void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,

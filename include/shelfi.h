@@ -204,8 +204,22 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
  * shelfi_arena_words() = C*K*2*L*N.  shelfi_dev_arena_put copies learner `learner`'s
  * [K][2][L][N] batch (device memory, or host memory if src_on_host) into its slices. */
 size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K);
+/* Every put validates what landed: one device pass over the learner's slices checks that
+ * each residue is < q_t (the aggregation's carry-free limb sums assume canonical
+ * residues), and the call returns after it (synchronises `stream`).  A refused slot
+ * (SHELFI_ERR_FORMAT) stays marked: shelfi_dev_wavg_arena over a range of that arena
+ * fails with SHELFI_ERR_STATE until a valid put replaces the slot. */
 int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size_t K, size_t learner,
                          size_t C, uint64_t* arena_dev, void* stream);
+/* A learner's upload as it arrives over the wire — a library blob or a PALISADE archive
+ * (ckks.cpp:276-281's per-learner bytes) — placed into its arena slot.  The header is
+ * checked against the context before any byte is copied: ring dimension, towers and
+ * moduli (params_id), the key (key_id / PALISADE keyTag, as EvalAdd refuses other keys,
+ * SURVEY App. B.7), the CKKS-packed encoding and the length; the batch must hold exactly
+ * K ciphertexts.  Refusals are SHELFI_ERR_FORMAT; the residues are then validated as
+ * for shelfi_dev_arena_put. */
+int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t K, size_t learner,
+                              size_t C, uint64_t* arena_dev, void* stream);
 /* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream);

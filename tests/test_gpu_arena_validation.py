@@ -1,0 +1,219 @@
+"""The HBM-resident arena validates every upload (Weak 3).
+
+`Arena.put(bytes)` / `shelfi_dev_arena_put_blob` parse a learner's upload (library blob or
+the reference's PALISADE archive, ckks.cpp:276-281) against the context before any byte is
+copied — ring, towers, moduli, key (PALISADE's EvalAdd refuses other keys),
+length and K — and every put (bytes or device tensor) checks that each placed residue is
+< q_t, since the aggregation's carry-free limb sums assume canonical residues.  A refused
+slot keeps `Arena.wavg` failing until a valid upload replaces it.
+"""
+import ctypes
+import mmap
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import PALISADE_DIR, PALISADE_PYBIND_DIR
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import _lib  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+K = 3
+
+
+@pytest.fixture(scope="module")
+def c2(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("arena_c2")) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    return ck
+
+
+@pytest.fixture(scope="module")
+def c2_other_key(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("arena_c2b")) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=8, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    return ck
+
+
+@pytest.fixture(scope="module")
+def c1():
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42, decodeNoise=False)
+    ck.loadCryptoParams()
+    return ck
+
+
+def _xs(C, n, seed=1000):
+    return [np.random.default_rng(seed + i).uniform(-1, 1, n) for i in range(C)]
+
+
+class GuardedBuffer:
+    """`data` placed so that its last byte is the last byte before a PROT_NONE page: a
+    read past the end faults (the over-read a same-K blob of smaller parameters would cause
+    if the header were not checked before the copy)."""
+
+    def __init__(self, data: bytes):
+        pg = mmap.PAGESIZE
+        self.n = len(data)
+        body = (self.n + pg - 1) // pg * pg
+        self.mm = mmap.mmap(-1, body + pg)
+        self.base = ctypes.addressof(ctypes.c_char.from_buffer(self.mm))
+        libc = ctypes.CDLL(None)
+        libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert libc.mprotect(ctypes.c_void_p(self.base + body), pg, 0) == 0  # PROT_NONE
+        self.off = body - self.n
+        self.mm[self.off:body] = data
+        self.ptr = self.base + self.off
+
+
+def _put_raw(ck, ar, learner, ptr, n):
+    return _lib.load().shelfi_dev_arena_put_blob(ck._ctx, ctypes.c_void_p(ptr), n, ar.K, learner, ar.C,
+                                                 ctypes.c_void_p(ar.buf.data_ptr()),
+                                                 ctypes.c_void_p(D._stream_ptr(ar.buf)))
+
+
+def _err():
+    return _lib.load().shelfi_last_error().decode()
+
+
+def test_valid_blobs_aggregate_like_the_bytes_api(c2):
+    B = c2.info()["batch"]
+    xs = _xs(4, K * B - 77)
+    blobs = [c2.encrypt(x) for x in xs]
+    w = [0.1, 0.2, 0.3, 0.4]
+    ar = D.Arena(c2, 4, K)
+    for i, b in enumerate(blobs):
+        ar.put(i, b)
+    got = ar.wavg(w).cpu().numpy().view(np.uint64)
+    inf = c2.info()
+    ref = m.blob_residues(c2.computeWeightedAverage(blobs, w), inf["ring_dim"], inf["num_towers"])
+    assert np.array_equal(got, ref)
+
+
+def test_same_k_blob_of_smaller_parameters_is_refused_before_any_copy(c2, c1):
+    """A 2^13/L2 blob of K ciphertexts is 8x smaller than a 2^15/L4 slot of K: refused by
+    its header (SHELFI_ERR_FORMAT) with the blob ending at a guard page, so any read past
+    it would fault this process."""
+    small = c1.encrypt(np.linspace(-1, 1, K * 4096))
+    assert m.blob_info(small)["num_cts"] == K
+    ar = D.Arena(c2, 2, K)
+    g = GuardedBuffer(small)
+    rc = _put_raw(c2, ar, 0, g.ptr, g.n)
+    assert rc == _lib.SHELFI_ERR_FORMAT, (rc, _err())
+    assert "parameters" in _err()
+    with pytest.raises(m.ShelfiError, match="parameters"):
+        ar.put(0, small)
+
+
+def test_blob_under_another_key_is_refused(c2, c2_other_key):
+    B = c2.info()["batch"]
+    other = c2_other_key.encrypt(np.linspace(-1, 1, K * B))
+    ar = D.Arena(c2, 2, K)
+    g = GuardedBuffer(other)
+    rc = _put_raw(c2, ar, 1, g.ptr, g.n)
+    assert rc == _lib.SHELFI_ERR_FORMAT and "different key" in _err()
+
+
+def test_wrong_ciphertext_count_and_truncation_are_refused(c2):
+    B = c2.info()["batch"]
+    ar = D.Arena(c2, 2, K)
+    with pytest.raises(m.ShelfiError, match="ciphertexts"):
+        ar.put(0, c2.encrypt(np.zeros((K - 1) * B)))
+    blob = c2.encrypt(np.zeros(K * B))
+    with pytest.raises(m.ShelfiError, match="length"):
+        ar.put(0, blob[:-8])
+    with pytest.raises(ValueError):
+        ar.put(2, blob)  # learner index >= C
+
+
+@pytest.mark.parametrize("where", ["first", "last", "middle_tower"])
+def test_non_canonical_residue_is_refused_and_poisons_the_slot(c2, where):
+    inf = c2.info()
+    N, L, B = inf["ring_dim"], inf["num_towers"], inf["batch"]
+    q = np.array(inf["moduli"], np.uint64)
+    xs = _xs(3, K * B)
+    blobs = [c2.encrypt(x) for x in xs]
+    w = [0.5, 0.25, 0.25]
+    ar = D.Arena(c2, 3, K)
+    for i, b in enumerate(blobs):
+        ar.put(i, b)
+    good = ar.wavg(w).cpu().numpy().view(np.uint64).copy()
+    hdr = _lib.load().shelfi_blob_header_bytes()
+    bad = bytearray(blobs[1])
+    res = np.frombuffer(bad, dtype="<u8", offset=hdr).reshape(K, 2, L, N)
+    k, p, t, j = {"first": (0, 0, 0, 0), "last": (K - 1, 1, L - 1, N - 1), "middle_tower": (1, 1, 2, 4097)}[where]
+    res[k, p, t, j] = q[t]  # == q_t: not canonical
+    with pytest.raises(m.ShelfiError, match="residue"):
+        ar.put(1, bytes(bad))
+    with pytest.raises(m.ShelfiError, match="refused upload for learner 1"):
+        ar.wavg(w)
+    with pytest.raises(m.ShelfiError, match="refused"):
+        ar.wavg(w, k0=1, k1=2)  # any range of that arena
+    ar.put(1, blobs[1])  # a valid upload replaces the slot
+    assert np.array_equal(ar.wavg(w).cpu().numpy().view(np.uint64), good)
+
+
+def test_device_tensor_with_non_canonical_residue_is_refused(c2):
+    B = c2.info()["batch"]
+    cts = [D.encrypt(c2, torch.tensor(x, device="cuda")) for x in _xs(2, K * B)]
+    bad = cts[0].clone()
+    bad[2, 0, 3, 5] = -1  # 2^64 - 1
+    ar = D.Arena(c2, 2, K)
+    ar.put(1, cts[1])
+    with pytest.raises(m.ShelfiError, match="residue"):
+        ar.put(0, bad)
+    with pytest.raises(m.ShelfiError, match="refused"):
+        ar.wavg([0.5, 0.5])
+    ar.put(0, cts[0])
+    out = ar.wavg([0.5, 0.5])
+    inf = c2.info()
+    ref = O.wavg([c.cpu().numpy().view(np.uint64) for c in cts], [0.5, 0.5], np.array(inf["moduli"], np.uint64),
+                 inf["delta"])
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), ref)
+
+
+def test_palisade_archives_are_placed_and_other_keys_refused(c1):
+    """The reference's own wire format: an archive is validated like a blob (keyTag as
+    PALISADE's EvalAdd checks it) and its per-tower runs are gathered into the slot."""
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=43, decodeNoise=False)
+    ck.loadCryptoParams()
+    ck.set_wire_format("palisade")
+    xs = _xs(3, K * 4096 - 5)
+    arch = [ck.encrypt(x) for x in xs]
+    w = [0.2, 0.3, 0.5]
+    ar = D.Arena(ck, 3, K)
+    for i, a in enumerate(arch):
+        ar.put(i, a)
+    got = ar.wavg(w).cpu().numpy().view(np.uint64)
+    _, ref = m.palisade_parse(ck.computeWeightedAverage(arch, w))
+    assert np.array_equal(got, ref)
+    other = m.CKKS("ckks", 4096, 52, PALISADE_PYBIND_DIR, seed=44, decodeNoise=False)
+    other.loadCryptoParams()
+    other.set_wire_format("palisade")
+    with pytest.raises(m.ShelfiError, match="keyTag"):
+        ar.put(0, other.encrypt(xs[0]))
+
+
+def test_device_checks_after_reloading_other_parameters(tmp_path):
+    """the (L, N) cache of the device API follows loadCryptoParams, so an
+    old-shape tensor is refused after the context switched to the PALISADE ring."""
+    d = str(tmp_path) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    old = D.encrypt(ck, torch.zeros(100, dtype=torch.float64, device="cuda"))
+    assert tuple(old.shape) == (1, 2, 4, 32768)
+    ck.cryptodir = PALISADE_DIR
+    ck.loadCryptoParams()
+    assert ck.info()["ring_dim"] == 8192
+    with pytest.raises(ValueError, match="shape"):
+        D.decrypt(ck, old, 100, ck.info()["delta"])
+    with pytest.raises(ValueError, match="shape"):
+        D.wavg(ck, [old], [1.0])
+    new = D.encrypt(ck, torch.zeros(100, dtype=torch.float64, device="cuda"))
+    assert tuple(new.shape) == (1, 2, 2, 8192)
