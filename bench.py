@@ -73,8 +73,12 @@ def parse():
                          "ciphertext ranges to their ranks)")
     ap.add_argument("--combine", choices=["torch", "shelfi"], default="torch",
                     help="learner-sharded combine: torch = pipelined torch.distributed reduce_scatter + "
-                         "modq; shelfi = the library's own RCCL communicator through the C ABI "
-                         "(shelfi_dev_reduce_scatter, one collective after the local wavg)")
+                         "modq; shelfi = the library's own RCCL communicator through the C ABI, the same "
+                         "pipeline in one call (shelfi_dev_combine_arena: wavg pieces on the caller's "
+                         "stream, reduce_scatter pieces on the library's comm stream)")
+    ap.add_argument("--shelfi-fold", action="store_true",
+                    help="--combine shelfi: fold each piece mod q after its collective (default: leave "
+                         "the sums to the consumer, shelfi_dev_decrypt_sum folds them on load)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
     ap.add_argument("--place-output", type=int, default=0,
@@ -109,11 +113,14 @@ def parse():
 
 
 class ShelfiCombine:
-    """Learner-sharded combine through the C ABI (include/shelfi.h): local wavg into a
-    partial padded to a multiple of the world size, then shelfi_dev_reduce_scatter (RCCL
-    uint64 SUM + mod-q fold inside the library).  Same result as PipelinedCombine."""
+    """Learner-sharded step through the C ABI alone (include/shelfi.h), pipelined:
+    shelfi_dev_combine_arena aggregates the local arena piece by piece and runs each piece's
+    RCCL reduce_scatter on the library's own comm stream while the next piece is aggregated
+    (HIP events order them) — the overlap PipelinedCombine gets from torch.distributed, for a
+    host without PyTorch.  fold=False leaves the share as uint64 sums of the W partials: the
+    mod-q fold happens in the consumer (shelfi_dev_decrypt_sum), not in a separate pass."""
 
-    def __init__(self, ck, K, ct_shape, dev):
+    def __init__(self, ck, arena, weights, K, pieces, dev, fold=False):
         import torch
         import torch.distributed as dist
 
@@ -121,19 +128,22 @@ class ShelfiCombine:
 
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
-        self.K, self.per = K, -(-K // self.world)
-        self.partial = torch.zeros((self.per * self.world,) + tuple(ct_shape), dtype=torch.int64, device=dev)
-        self.share = torch.empty((self.per,) + tuple(ct_shape), dtype=torch.int64, device=dev)
         self.comm = SD.Comm(ck, self.rank, self.world)
+        self.arena, self.weights, self.K, self.pieces, self.fold = arena, weights, K, pieces, fold
+        self.Ks = self.comm.share_cts(K)
+        shape = (2, arena.L, arena.N)
+        self.send = torch.empty((self.world * self.Ks,) + shape, dtype=torch.int64, device=dev)
+        self.share = torch.empty((self.Ks,) + shape, dtype=torch.int64, device=dev)
+        self.terms = 1 if fold else self.world  # residues of the share: sums of `terms` residues
 
-    def run(self, compute_piece, fold_share=None):
-        compute_piece(0, self.K, self.partial[:self.K])
-        self.comm.reduce_scatter(self.partial, out=self.share)
-        a, b = self.rank * self.per, min(self.K, (self.rank + 1) * self.per)
+    def run(self, compute_piece=None, fold_share=None):
+        self.comm.combine_arena(self.arena, self.weights, self.K, self.send, self.share, pieces=self.pieces,
+                                fold=self.fold)
+        a, b = self.rank * self.Ks, min(self.K, (self.rank + 1) * self.Ks)
         return [(a, b, self.share[:b - a])] if b > a else []
 
 
-def check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8):
+def check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8, terms=1):
     """Decrypt up to max_cts of the ciphertexts this rank owns and compare with plain
     FedAvg of ALL learners (every rank regenerates any learner's slice from its seed:
     PCG64 draws one 64-bit word per uniform double, so advance() skips to the slice)."""
@@ -154,7 +164,8 @@ def check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8):
             g = np.random.default_rng(1000 + i)
             g.bit_generator.advance(lo)
             exp += w32 * g.uniform(-1, 1, hi - lo).astype(np.float32).astype(np.float64)
-        dec = D.decrypt(ck, share[:b - a], hi - lo, delta * delta).cpu().numpy()
+        dec = (D.decrypt(ck, share[:b - a], hi - lo, delta * delta) if terms == 1 else
+               D.decrypt_sum(ck, share[:b - a], terms, hi - lo, delta * delta)).cpu().numpy()
         err = max(err, float(np.abs(dec - exp).max()))
         n_checked += b - a
     return {"max_abs_err": err, "cts_checked_per_rank": n_checked,
@@ -341,7 +352,9 @@ def main():
         if shard == "learners" and args.combine == "torch":
             comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
         elif shard == "learners":
-            comb = ShelfiCombine(ck, K, (2, L, N), dev)
+            if args.layout != "arena":
+                raise SystemExit("--combine shelfi aggregates the resident arena (--layout arena)")
+            comb = ShelfiCombine(ck, arena, weights, K, args.pieces, dev, fold=args.shelfi_fold)
 
         def kernel_into(dst):
             if args.layout == "arena":
@@ -416,7 +429,8 @@ def main():
         the learners shard) decrypt to plain FedAvg of every learner (max over ranks)."""
         owned = mode["step"]()
         torch.cuda.synchronize()
-        c = check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8)
+        terms = getattr(mode["comb"], "terms", 1)
+        c = check_owned(ck, D, owned, world, Cl, params, batch, delta, max_cts=8, terms=terms)
         if distributed:
             ce = torch.tensor([c["max_abs_err"]], dtype=torch.float64, device=dev)
             dist.all_reduce(ce, op=dist.ReduceOp.MAX)
@@ -438,21 +452,37 @@ def main():
     # never returns must not cost the headline line (the line is then written with the
     # check marked as timed out and every rank exits).
     def c_abi_comm_check():
+        """torch combine (headline) -> the C-ABI communicator's allreduce on the same partial
+        sums must equal the owned shares; C-ABI combine (headline) -> torch.distributed's
+        all_reduce + modq on the same partial sums must equal the (folded) C-ABI shares."""
         try:
             t0 = time.perf_counter()
-            comm = SD.Comm(ck, rank, world)
             full = torch.empty((K, 2, L, N), dtype=torch.int64, device=dev)
             main_mode["piece"](0, K, full)
-            comm.allreduce(full)
+            comb = main_mode["comb"]
+            if args.combine == "torch":
+                comm = SD.Comm(ck, rank, world)
+                comm.allreduce(full)
+                what = "shelfi_dev_allreduce (C ABI, world %d) == torch reduce_scatter shares" % world
+            else:
+                dist.all_reduce(full, op=dist.ReduceOp.SUM)
+                D.modq(ck, full)
+                what = ("pipelined shelfi_dev_combine_arena (C ABI, world %d, %d pieces, fold %s) == "
+                        "torch all_reduce + modq" % (world, args.pieces, "on" if args.shelfi_fold else "in decrypt"))
             owned = main_mode["step"]()
             torch.cuda.synchronize()
-            ok = all(torch.equal(sv, full[a:b]) for a, b, sv in owned)
-            comm.close()
+            ok = True
+            for a, b, sv in owned:
+                sv = sv.clone()
+                if getattr(comb, "terms", 1) > 1:
+                    D.modq(ck, sv)
+                ok = ok and torch.equal(sv, full[a:b])
+            if args.combine == "torch":
+                comm.close()
             okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(okt, op=dist.ReduceOp.MIN)
             del full
-            return {"ok": bool(okt.item()), "seconds": round(time.perf_counter() - t0, 3),
-                    "what": "shelfi_dev_allreduce (C ABI, world %d) == torch reduce_scatter shares" % world}
+            return {"ok": bool(okt.item()), "seconds": round(time.perf_counter() - t0, 3), "what": what}
         except Exception as e:  # reported, never fatal to the headline
             return {"ok": False, "error": repr(e)[:300]}
 
@@ -670,11 +700,17 @@ def main():
                                                    "cts [k0, k1), no collective" % (Cl * world)) if cts_mode else
                                                   (", RCCL reduce_scatter overlapped in %d pieces" % args.pieces
                                                    if args.combine == "torch" else
-                                                   ", RCCL reduce_scatter through shelfi_dev_reduce_scatter")),
+                                                   ", RCCL reduce_scatter overlapped in %d pieces inside libshelfi "
+                                                   "(shelfi_dev_combine_arena, mod-q fold %s)"
+                                                   % (args.pieces, "per piece" if args.shelfi_fold else
+                                                      "in the consumer's decrypt"))),
                    "ring_dim": N, "towers": L, "learners_total": Cl * world, "cts_per_learner": K,
                    "parallelism": ("dp1 (one GPU, no collective)" if not distributed else
                                    "ciphertext-sharded dp%d (no collective)" % world if cts_mode else
-                                   "learner-sharded dp%d + RCCL reduce_scatter over xGMI + modq" % world),
+                                   "learner-sharded dp%d + RCCL reduce_scatter over xGMI + modq" % world
+                                   if args.combine == "torch" or args.shelfi_fold else
+                                   "learner-sharded dp%d + RCCL reduce_scatter over xGMI (C ABI; fold in decrypt)"
+                                   % world),
                    "layout": args.layout, "output_placement": main_mode["placement"]},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(enc_ms, 5),
@@ -746,7 +782,7 @@ def main():
                 emit()
                 os._exit(COMM_HANG_EXIT)  # the line is written, but a hung collective fails the run
         threading.Thread(target=watchdog, daemon=True).start()
-        if main_mode["shard"] == "learners" and args.combine == "torch":
+        if main_mode["shard"] == "learners":
             res["c_abi_comm_check"] = c_abi_comm_check()
     emit()
     if distributed:

@@ -135,6 +135,9 @@ SIGNATURES = {
     "shelfi_dev_reduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
     "shelfi_dev_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "shelfi_dev_reduce_scatter": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "shelfi_combine_share_cts": (C.c_size_t, [C.c_void_p, C.c_size_t]),
+    "shelfi_dev_combine_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                           C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "shelfi_dev_encrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_size_t,
                                      C.c_void_p, C.c_void_p]),
@@ -153,6 +156,8 @@ SIGNATURES = {
     "shelfi_dev_rescale": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt_level": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_double,
                                            C.c_size_t, C.c_void_p, C.c_void_p]),
+    "shelfi_dev_decrypt_sum": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_double,
+                                         C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_save_eval_key": (C.c_int, [C.c_void_p, C.c_char_p]),
     "shelfi_load_eval_key": (C.c_int, [C.c_void_p, C.c_char_p]),
     "shelfi_palisade_evalkey_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.c_void_p, u64p]),

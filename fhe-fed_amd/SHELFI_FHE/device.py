@@ -200,6 +200,20 @@ def decrypt(ckks, ct, n: int, scale: float, out=None):
     return out
 
 
+def decrypt_sum(ckks, ct, terms: int, n: int, scale: float, out=None):
+    """decrypt a multi-GPU combine's unfolded share: every residue is a uint64 sum of `terms`
+    (<= 16) canonical residues (Comm.combine_arena(fold=False)); the mod-q fold happens in
+    decrypt's first pass (shelfi_dev_decrypt_sum)."""
+    torch = _torch()
+    _check_ct(ct, ckks)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=ct.device)
+    check(_lib.load().shelfi_dev_decrypt_sum(ckks._ctx, C.c_void_p(ct.data_ptr()), ct.shape[0], int(terms),
+                                             float(scale), int(n), C.c_void_p(out.data_ptr()),
+                                             C.c_void_p(_stream_ptr(ct))), "dev_decrypt_sum")
+    return out
+
+
 def mult(ckks, a, b, out=None):
     """cc->EvalMult(a, b) for K ciphertext pairs of the same level: tensor product +
     HYBRID relinearization (needs ckks.evalMultKeyGen()).  Scale: scale_a * scale_b."""

@@ -250,6 +250,33 @@ class Comm:
                    C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(out)))
         return out
 
+    def share_cts(self, K: int) -> int:
+        """Ciphertexts of this rank's share of a K-ciphertext combine: ceil(K / world)."""
+        from ._lib import load
+
+        return int(load().shelfi_combine_share_cts(self._ckks._ctx, int(K)))
+
+    def combine_arena(self, arena, weights, K: int, send, share, pieces: int = 8, fold: bool = True):
+        """The whole learner-sharded step in the library (shelfi_dev_combine_arena): this rank's
+        arena aggregated piece by piece on the current stream, each piece reduce-scattered on
+        the library's comm stream while the next is aggregated.  `share` ([share_cts(K)][2][L][N])
+        receives global ciphertexts [rank Ks, (rank+1) Ks); `send` is [world Ks][2][L][N] scratch.
+        fold=False leaves uint64 sums of `world` residues (decrypt them with
+        device.decrypt_sum(..., terms=world))."""
+        import ctypes as C
+        from .device import _check_ct, _stream_ptr
+
+        Ks = self.share_cts(K)
+        _check_ct(share, self._ckks, Ks)
+        _check_ct(send, self._ckks, self.world * Ks)
+        if len(weights) != arena.C or arena.K != K:
+            raise ValueError("one weight per arena learner, and the arena's K")
+        w = (C.c_float * arena.C)(*[float(x) for x in weights])
+        self._call("shelfi_dev_combine_arena", C.c_void_p(arena.buf.data_ptr()), w, arena.C, int(K), int(pieces),
+                   C.c_void_p(send.data_ptr()), C.c_void_p(share.data_ptr()), 1 if fold else 0,
+                   C.c_void_p(_stream_ptr(share)))
+        return share
+
     def close(self):
         if self._ckks is not None and self._ckks._ctx:
             from ._lib import load

@@ -1033,8 +1033,21 @@ static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* c
 // Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
 // chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
 // (stream B), with two device buffer sets.  Writes the payload of the result.
+// Zero-copy uploads (SHELFI_H2D_REGISTER=1, A/B probe switch read per call): each learner's
+// upload is page-locked in place for the call (hipHostRegister) and DMA'd straight from it,
+// instead of being copied into the pinned staging ring first.
+struct HostRegistration {
+  std::vector<void*> ptrs;
+  hipStream_t s = nullptr;
+  ~HostRegistration() {
+    if (s) (void)hipStreamSynchronize(s);  // no DMA may still read a buffer being unpinned
+    for (void* p : ptrs) (void)hipHostUnregister(p);
+  }
+};
+
 static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in,
-                                const float* weights, size_t C, uint64_t K, const CtLayout& dst) {
+                                const float* weights, size_t C, uint64_t K, const CtLayout& dst,
+                                const size_t* lens) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   // chunk: ~64 MiB of input per learner-group buffer, at least 1 ciphertext
@@ -1049,6 +1062,20 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
   std::vector<HostPiece> pcs;
+  HostRegistration reg;
+  const char* zc_env = getenv("SHELFI_H2D_REGISTER");
+  bool zc = zc_env && *zc_env == '1';
+  if (zc) {
+    reg.s = pp.a;
+    for (size_t c = 0; c < C && zc; ++c) {
+      if (hipHostRegister(in[c].base, lens[c], hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        zc = false;  // not registrable (e.g. already pinned elsewhere): the staging ring
+      } else {
+        reg.ptrs.push_back(in[c].base);
+      }
+    }
+  }
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
   const uint64_t nchunks = (K + kc - 1) / kc;
@@ -1060,7 +1087,15 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
-        sr.s.h2dv(inb[b] + c * kn * ct_bytes, pcs.data(), pcs.size(), pp.a);
+        if (zc) {  // DMA straight from the registered upload
+          uint8_t* d = inb[b] + c * kn * ct_bytes;
+          for (const HostPiece& pc : pcs) {
+            SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, pp.a));
+            d += pc.n;
+          }
+        } else {
+          sr.s.h2dv(inb[b] + c * kn * ct_bytes, pcs.data(), pcs.size(), pp.a);
+        }
       }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
@@ -1130,7 +1165,7 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     // residues first (the parallel drains first-touch the fresh pages), framing after
     CtLayout dst = make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, nullptr, &total);
     dst.base = out;
-    if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst);
+    if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst, lens);
     make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, out, &total);
   });
 }
@@ -1340,14 +1375,48 @@ static void arena_validate(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t K,
   }
 }
 
-// An aggregation over arena words [a, a + words) must not read a refused slot.
-static void arena_require_valid(shelfi_ctx* ctx, const uint64_t* a, size_t words) {
-  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+}  // extern "C"
+
+namespace shelfi {
+// An aggregation over arena words [a, a + words) must not read a refused slot (ctx lock held).
+void arena_require_valid_locked(const shelfi_ctx* ctx, const uint64_t* a, size_t words) {
   for (const auto& r : ctx->arena_refused)
     if (a < r.arena + r.words && r.arena < a + words)
       throw Error{SHELFI_ERR_STATE, "the arena holds a refused upload for learner " +
                                         std::to_string(r.learner) + "; put a valid batch first"};
 }
+
+// The arena aggregation itself (ctx lock held, weights checked): C <= 16 learners in one
+// wavg_kernel launch per group of 16, more in one wavg_arena_many pass.
+void wavg_arena_enqueue(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                        uint64_t* out_dev, hipStream_t s) {
+  const Params& p = ctx->p;
+  if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners
+    const int slot = arena_weight_slot(ctx, w, C, s);
+    launch_wavg_arena_many(arena_dev, ctx->wl_dev[slot], (uint32_t)C, (uint64_t)K * 2 * p.L, p.L, p.logN,
+                           ctx->dt.tc, out_dev, s);
+    SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], s));
+    return;
+  }
+  WavgArgs a;
+  std::memset(&a, 0, sizeof(a));
+  fill_weights(a, p, w, C);
+  a.arena = arena_dev;
+  a.arena_learners = (uint32_t)C;
+  a.first_learner = 0;
+  a.out = out_dev;
+  a.rows = (uint64_t)K * 2 * p.L;
+  a.C = (uint32_t)C;
+  a.L = p.L;
+  a.logN = p.logN;
+  a.accumulate = 0;
+  launch_wavg(a, ctx->dt.tc, s);
+}
+
+void check_wavg_weights(const float* w, size_t C, double delta) { check_weights(w, C, delta); }
+}  // namespace shelfi
+
+extern "C" {
 
 int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size_t K, size_t learner,
                          size_t C, uint64_t* arena_dev, void* stream) {
@@ -1397,36 +1466,13 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream) {
   if (!ctx || !out_dev || (C && (!arena_dev || !w))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
     check_weights(w, C, ctx->p.delta);
-    arena_require_valid(ctx, arena_dev, C * K * 2ull * ctx->p.L * ctx->p.N);
+    arena_require_valid_locked(ctx, arena_dev, C * K * 2ull * ctx->p.L * ctx->p.N);
     DeviceGuard g(ctx->device);
-    const Params& p = ctx->p;
-    if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners
-      std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
-      const int slot = arena_weight_slot(ctx, w, C, (hipStream_t)stream);
-      launch_wavg_arena_many(arena_dev, ctx->wl_dev[slot], (uint32_t)C, (uint64_t)K * 2 * p.L, p.L,
-                             p.logN, ctx->dt.tc, out_dev, (hipStream_t)stream);
-      SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], (hipStream_t)stream));
-      return;
-    }
-    for (size_t c0 = 0; c0 < C; c0 += kWavgMaxLearners) {
-      const size_t gc = std::min<size_t>(kWavgMaxLearners, C - c0);
-      WavgArgs a;
-      std::memset(&a, 0, sizeof(a));
-      fill_weights(a, p, w + c0, gc);
-      a.arena = arena_dev;
-      a.arena_learners = (uint32_t)C;
-      a.first_learner = (uint32_t)c0;
-      a.out = out_dev;
-      a.rows = (uint64_t)K * 2 * p.L;
-      a.C = (uint32_t)gc;
-      a.L = p.L;
-      a.logN = p.logN;
-      a.accumulate = c0 ? 1 : 0;
-      launch_wavg(a, ctx->dt.tc, (hipStream_t)stream);
-    }
+    wavg_arena_enqueue(ctx, arena_dev, w, C, K, out_dev, (hipStream_t)stream);
   });
 }
 
@@ -1525,8 +1571,9 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
 }
 
 // decrypt K ciphertexts of `towers` RNS towers (the context's L, or fewer after ModReduce)
+// (sum_in: residues are uint64 sums of <= 16 canonical residues, folded on load)
 static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
-                       size_t n, double* out_dev, void* stream) {
+                       size_t n, double* out_dev, void* stream, bool sum_in = false) {
   if (!ctx || (n && (!ct_dev || !out_dev))) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
@@ -1549,7 +1596,8 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
       const uint64_t kc = std::min(kc_max, Kn - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
       dn.g0 = g0 + k0;
-      launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn);
+      launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
+                     sum_in);
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);
@@ -1564,6 +1612,15 @@ int shelfi_dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, double
 int shelfi_dev_decrypt_level(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
                              size_t n, double* out_dev, void* stream) {
   return dev_decrypt(ctx, ct_dev, K, towers, scale, n, out_dev, stream);
+}
+
+int shelfi_dev_decrypt_sum(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t terms, double scale,
+                           size_t n, double* out_dev, void* stream) {
+  if (terms < 1 || terms > (uint32_t)kMaxCommRanks) {
+    set_error("decrypt_sum: the residues must be sums of 1..16 canonical residues");
+    return SHELFI_ERR_ARG;
+  }
+  return dev_decrypt(ctx, ct_dev, K, ctx ? ctx->p.L : 0, scale, n, out_dev, stream, true);
 }
 
 int shelfi_dev_ntt(shelfi_ctx* ctx, uint64_t* polys_dev, size_t P, int inverse, void* stream) {

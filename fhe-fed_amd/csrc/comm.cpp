@@ -15,6 +15,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -108,12 +109,18 @@ ncclComm_t comm_of(shelfi_ctx* ctx) {
 }  // namespace
 
 void comm_release(shelfi_ctx* ctx) {
-  if (ctx && ctx->comm) {
+  if (!ctx) return;
+  if (ctx->comm_stream) (void)hipStreamSynchronize(ctx->comm_stream);
+  if (ctx->comm) {
     (void)rccl().comm_destroy(reinterpret_cast<ncclComm_t>(ctx->comm));
     ctx->comm = nullptr;
     ctx->comm_rank = 0;
     ctx->comm_world = 0;
   }
+  for (hipEvent_t e : ctx->comm_events) (void)hipEventDestroy(e);
+  ctx->comm_events.clear();
+  if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+  ctx->comm_stream = nullptr;
 }
 
 }  // namespace shelfi
@@ -210,6 +217,70 @@ int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size
     const size_t Ks = K / W, words = Ks * 2ull * p.L * p.N;
     check(rccl().reduce_scatter(partial_dev, out_dev, words, ncclUint64, ncclSum, c, s), "ncclReduceScatter");
     launch_modq(out_dev, (uint64_t)Ks * 2 * p.L, p.L, p.logN, ctx->dt.tc, s);
+  });
+}
+
+size_t shelfi_combine_share_cts(const shelfi_ctx* ctx, size_t K) {
+  if (!ctx || !ctx->comm || ctx->comm_world < 1) return 0;
+  const size_t W = (size_t)ctx->comm_world;
+  return (K + W - 1) / W;
+}
+
+// The pipelined learner-sharded combine (SURVEY §8 e): rank r owns the global ciphertexts
+// [r Ks, (r+1) Ks), Ks = ceil(K / W).  Piece j covers sub-slice j (Kp = ceil(Ks / P)
+// ciphertexts) of EVERY rank's slice: the local arena aggregation of those W runs is written
+// to a [W][kp] send region on the caller's stream, an event hands it to the context's comm
+// stream, and one ncclReduceScatter delivers this rank's sub-slice straight into
+// share[j Kp ..] while piece j+1 is being aggregated.  The share comes out contiguous, as
+// the unpipelined reduce_scatter's would.  fold = 1: the mod-q fold of each piece follows its
+// collective on the comm stream; fold = 0: left to the consumer (shelfi_dev_decrypt_sum).
+int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                             size_t pieces, uint64_t* send_dev, uint64_t* share_dev, int fold, void* stream) {
+  if (!ctx || !w || !C || (K && (!arena_dev || !send_dev || !share_dev))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded_comm([&] {
+    ncclComm_t c = comm_of(ctx);
+    check_wavg_weights(w, C, ctx->p.delta);
+    const Params& p = ctx->p;
+    const size_t ctw = 2ull * p.L * p.N;
+    arena_require_valid_locked(ctx, arena_dev, C * K * ctw);
+    if (!K) return;
+    DevGuard g(ctx->device);
+    const size_t W = (size_t)ctx->comm_world;
+    const size_t Ks = (K + W - 1) / W;
+    const size_t P = std::max<size_t>(1, std::min(pieces ? pieces : 1, Ks));
+    const size_t Kp = (Ks + P - 1) / P;
+    hipStream_t s = (hipStream_t)stream;
+    if (!ctx->comm_stream) SHELFI_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    while (ctx->comm_events.size() < P + 1) {
+      hipEvent_t e = nullptr;
+      SHELFI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->comm_events.push_back(e);
+    }
+    hipStream_t cs = ctx->comm_stream;
+    // the comm stream must not overwrite a share the caller's stream may still be reading
+    SHELFI_HIP(hipEventRecord(ctx->comm_events[P], s));
+    SHELFI_HIP(hipStreamWaitEvent(cs, ctx->comm_events[P], 0));
+    for (size_t j = 0; j < P; ++j) {
+      const size_t kj0 = j * Kp;
+      if (kj0 >= Ks) break;
+      const size_t kn = std::min(Kp, Ks - kj0);
+      uint64_t* send = send_dev + W * kj0 * ctw;  // [W][kn] ciphertexts
+      for (size_t gr = 0; gr < W; ++gr) {
+        const size_t a = gr * Ks + kj0;
+        const size_t cnt = a < K ? std::min(kn, K - a) : 0;
+        if (cnt) wavg_arena_enqueue(ctx, arena_dev + a * ctw * C, w, C, cnt, send + gr * kn * ctw, s);
+        if (cnt < kn)  // padding past K: zero, the additive identity
+          SHELFI_HIP(hipMemsetAsync(send + (gr * kn + cnt) * ctw, 0, (kn - cnt) * ctw * 8, s));
+      }
+      SHELFI_HIP(hipEventRecord(ctx->comm_events[j], s));
+      SHELFI_HIP(hipStreamWaitEvent(cs, ctx->comm_events[j], 0));
+      uint64_t* dst = share_dev + kj0 * ctw;
+      check(rccl().reduce_scatter(send, dst, kn * ctw, ncclUint64, ncclSum, c, cs), "ncclReduceScatter");
+      if (fold) launch_modq(dst, (uint64_t)kn * 2 * p.L, p.L, p.logN, ctx->dt.tc, cs);
+    }
+    SHELFI_HIP(hipEventRecord(ctx->comm_events[P], cs));
+    SHELFI_HIP(hipStreamWaitEvent(s, ctx->comm_events[P], 0));  // the share is ready on `stream`
   });
 }
 

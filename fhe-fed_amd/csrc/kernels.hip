@@ -62,56 +62,73 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
 //    (tools/wavg_variants.py), the gap being DRAM row locality across 16 streams.
 // CHECK (the bytes API, whose inputs are untrusted learner uploads): also flag any input
 // residue >= q_t in *a.bad (the carry-free limb sums assume canonical residues).
-template <bool INTERLEAVED, bool CHECK = false>
+// R rows per block (R = 2 for C <= 8 learners): with few learners one 512-residue row gives
+// a thread only C 16-byte loads in flight; two adjacent rows (same tower: N / 512 is even)
+// double that, and the block's arena region stays one contiguous 2 C x 4 KiB run.
+template <bool INTERLEAVED, bool CHECK = false, int R = 1>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
-  const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
+  const uint64_t row0 = (uint64_t)blockIdx.x * R;
+  const uint64_t base = row0 * kWavgPerBlock;
   const uint32_t t = (uint32_t)((base >> a.logN) % a.L);  // block-uniform tower
   const TowerConst c = tcs[t];
-  const uint64_t e = base + 2u * threadIdx.x;
   const uint32_t M30 = (1u << 30) - 1;
-  // interleaved: this block's chunk, learner slice k at src + k * 512
+  // interleaved: row i's chunk, learner slice k at src + (i C + k) * 512
   const uint64_t* __restrict__ src =
-      INTERLEAVED ? a.arena + ((uint64_t)blockIdx.x * a.arena_learners + a.first_learner) * kWavgPerBlock +
-                        2u * threadIdx.x
+      INTERLEAVED ? a.arena + (row0 * a.arena_learners + a.first_learner) * kWavgPerBlock + 2u * threadIdx.x
                   : nullptr;
+  const uint64_t rstride = INTERLEAVED ? (uint64_t)a.arena_learners * kWavgPerBlock : kWavgPerBlock;
 
-  uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
-  uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
+  uint64_t s[R][8];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[i][j] = 0;
   bool bad = false;
-#pragma unroll 8
+  constexpr int UNR = 8 / R;
+#pragma unroll UNR
   for (uint32_t k = 0; k < a.C; ++k) {
-    const uint64_t* __restrict__ p = INTERLEAVED ? src + (uint64_t)k * kWavgPerBlock : a.ptrs[k] + e;
+    const uint64_t* __restrict__ p = INTERLEAVED ? src + (uint64_t)k * kWavgPerBlock
+                                                 : a.ptrs[k] + base + 2u * threadIdx.x;
     const uint32_t w0 = a.wl[k][t][0], w1 = a.wl[k][t][1];
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    if (CHECK)
-      bad |= (((uint64_t)v.y << 32) | v.x) >= c.q || (((uint64_t)v.w << 32) | v.z) >= c.q;
-    // element a: (v.x, v.y), element b: (v.z, v.w); 30-bit limbs
-    const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
-    const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
-    s00a += (uint64_t)xa0 * w0;
-    s01a += (uint64_t)xa0 * w1;
-    s10a += (uint64_t)xa1 * w0;
-    s11a += (uint64_t)xa1 * w1;
-    s00b += (uint64_t)xb0 * w0;
-    s01b += (uint64_t)xb0 * w1;
-    s10b += (uint64_t)xb1 * w0;
-    s11b += (uint64_t)xb1 * w1;
+    u32x4 v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i * rstride));
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (CHECK)
+        bad |= (((uint64_t)v[i].y << 32) | v[i].x) >= c.q || (((uint64_t)v[i].w << 32) | v[i].z) >= c.q;
+      // element a: (v.x, v.y), element b: (v.z, v.w); 30-bit limbs
+      const uint32_t xa0 = v[i].x & M30, xa1 = (v[i].x >> 30) | (v[i].y << 2);
+      const uint32_t xb0 = v[i].z & M30, xb1 = (v[i].z >> 30) | (v[i].w << 2);
+      s[i][0] += (uint64_t)xa0 * w0;
+      s[i][1] += (uint64_t)xa0 * w1;
+      s[i][2] += (uint64_t)xa1 * w0;
+      s[i][3] += (uint64_t)xa1 * w1;
+      s[i][4] += (uint64_t)xb0 * w0;
+      s[i][5] += (uint64_t)xb0 * w1;
+      s[i][6] += (uint64_t)xb1 * w0;
+      s[i][7] += (uint64_t)xb1 * w1;
+    }
   }
   if (CHECK && bad) atomicOr(a.bad, 1u);
-  uint64_t r0 = wavg_fold(s00a, s01a, s10a, s11a, c);
-  uint64_t r1 = wavg_fold(s00b, s01b, s10b, s11b, c);
-  if (a.accumulate) {  // learners beyond the first 16: fold into the running sum
-    const u32x4 o = *reinterpret_cast<const u32x4*>(a.out + e);
-    r0 = addmod(r0, (uint64_t)o.x | ((uint64_t)o.y << 32), c.q);
-    r1 = addmod(r1, (uint64_t)o.z | ((uint64_t)o.w << 32), c.q);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const uint64_t e = base + (uint64_t)i * kWavgPerBlock + 2u * threadIdx.x;
+    uint64_t r0 = wavg_fold(s[i][0], s[i][1], s[i][2], s[i][3], c);
+    uint64_t r1 = wavg_fold(s[i][4], s[i][5], s[i][6], s[i][7], c);
+    if (a.accumulate) {  // learners beyond the first 16: fold into the running sum
+      const u32x4 o = *reinterpret_cast<const u32x4*>(a.out + e);
+      r0 = addmod(r0, (uint64_t)o.x | ((uint64_t)o.y << 32), c.q);
+      r1 = addmod(r1, (uint64_t)o.z | ((uint64_t)o.w << 32), c.q);
+    }
+    u32x4 o;
+    o.x = (uint32_t)r0;
+    o.y = (uint32_t)(r0 >> 32);
+    o.z = (uint32_t)r1;
+    o.w = (uint32_t)(r1 >> 32);
+    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(a.out + e));
   }
-  u32x4 o;
-  o.x = (uint32_t)r0;
-  o.y = (uint32_t)(r0 >> 32);
-  o.z = (uint32_t)r1;
-  o.w = (uint32_t)(r1 >> 32);
-  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(a.out + e));
 }
 
 // Arena aggregation of any number of learners in one pass: groups of up to 16
@@ -181,17 +198,42 @@ void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint3
   SHELFI_HIP(hipGetLastError());
 }
 
+// Rows per wavg block: with C <= 8 learners a one-row thread has only C 16-byte loads in
+// flight; the arena kernel then takes 4 rows (4 C loads), the separate-buffer one 2.  Measured
+// in one process per shape (tools/wavg_rows_ab.py, profiles/probes/r03_wavg_rows_ab.txt):
+// 8 x 156 (cfg5) 0.729 -> 0.786 of 8 TB/s, 8 x 714 0.718 -> 0.778, 2 x 714 0.646 -> 0.675,
+// 4 x 714 a tie; at 12-16 learners the best row count moved with the shape (16 x 4: 1 row;
+// 12 x 476: 1; 16 x 714: 2), so one row stays there.  SHELFI_WAVG_ROWS=1|2|4 forces one
+// (A/B probe switch, read per launch).
+static int wavg_rows(uint32_t C, bool arena) {
+  const char* env = getenv("SHELFI_WAVG_ROWS");
+  if (env && (*env == '1' || *env == '2' || (*env == '4' && arena))) return *env - '0';
+  return C <= 8 ? (arena ? 4 : 2) : 1;
+}
+
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t total = a.rows << a.logN;
-  const uint64_t blocks = total / kWavgPerBlock;
-  if (!blocks) return;
+  const uint64_t rows = total / kWavgPerBlock;  // always even: N / 512 >= 2 rows per tower
+  if (!rows) return;
+  int R = wavg_rows(a.C, a.arena != nullptr);
+  while (R > 1 && ((1ull << a.logN) / kWavgPerBlock) % R) R >>= 1;  // a block stays in one tower
+  const uint64_t blocks = rows / R;
   if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  if (a.arena)
-    hipLaunchKernelGGL(wavg_kernel<true>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+  const dim3 g((uint32_t)blocks), b(kWavgThreads);
+  if (a.arena && R == 4)
+    hipLaunchKernelGGL((wavg_kernel<true, false, 4>), g, b, 0, s, a, tc);
+  else if (a.arena && R == 2)
+    hipLaunchKernelGGL((wavg_kernel<true, false, 2>), g, b, 0, s, a, tc);
+  else if (a.arena)
+    hipLaunchKernelGGL((wavg_kernel<true, false, 1>), g, b, 0, s, a, tc);
+  else if (a.bad && R == 2)
+    hipLaunchKernelGGL((wavg_kernel<false, true, 2>), g, b, 0, s, a, tc);
   else if (a.bad)
-    hipLaunchKernelGGL((wavg_kernel<false, true>), dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+    hipLaunchKernelGGL((wavg_kernel<false, true, 1>), g, b, 0, s, a, tc);
+  else if (R == 2)
+    hipLaunchKernelGGL((wavg_kernel<false, false, 2>), g, b, 0, s, a, tc);
   else
-    hipLaunchKernelGGL(wavg_kernel<false>, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, a, tc);
+    hipLaunchKernelGGL((wavg_kernel<false, false, 1>), g, b, 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());
 }
 
@@ -514,7 +556,11 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
 // ciphertext batch [K][2][L][N], and the last chunk writes the lazy ([0, 8q)) block to
 // dbuf [K][L][N] from registers for ntt_inv_cols.  Same contract as ntt_inv_blocks with
 // ct != nullptr and scale_ninv = 0.
-template <int BL, int K1, int K2, int K3, int K4>
+// SUM: the ciphertexts are a collective's unfolded uint64 sums of <= 16 canonical residues
+// (shelfi_dev_combine_arena with fold = 0): c0 is reduced on load (red_any, [0, 2q)), c1 needs
+// nothing (the lazy Shoup product takes any 64-bit multiplicand) — the mod-q fold of the
+// combine happens here instead of in a separate pass over the share.
+template <int BL, int K1, int K2, int K3, int K4, bool SUM = false>
 __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restrict__ dbuf, uint32_t L,
                                                              uint32_t logN,
                                                              const ulonglong2* __restrict__ twb,
@@ -530,7 +576,8 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const uint32_t b = bid & ((1u << sstart) - 1);
   const uint32_t poly = bid >> sstart;  // k * L + t
   const uint32_t t = poly % L, k = poly / L;
-  const uint64_t q = tcs[t].q, n4q = tcs[t].n4q, n8q = tcs[t].n8q;
+  const TowerConst& cst = tcs[t];
+  const uint64_t q = cst.q, n4q = cst.n4q, n8q = cst.n8q;
   const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
@@ -542,7 +589,8 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   // first chunk: contiguous sets of 2^K1 (T0 = 0)
   inv_chunk_ct<BL, 0, K1, false>(tb, q, n8q,
                           [&](uint32_t j, uint32_t) {
-                            return csub_neg(c0[j] + shoup_lazy(c1[j], s[j], ss[j], q), n4q);
+                            const uint64_t a0 = SUM ? red_any(c0[j], cst) : c0[j];
+                            return csub_neg(a0 + shoup_lazy(c1[j], s[j], ss[j], q), n4q);
                           },
                           [&](int, uint32_t, uint32_t pj0, auto& x) {
 #pragma unroll
@@ -578,7 +626,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
                                                       int scale_ninv,
                                                       const uint64_t* __restrict__ ct,
                                                       const uint64_t* __restrict__ sk,
-                                                      const uint64_t* __restrict__ sksh) {
+                                                      const uint64_t* __restrict__ sksh, int sum_in) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
   const uint32_t N = 1u << logN, blk = 1u << blkLog;
   const uint32_t sh = logN - blkLog, nb = 1u << sh;
@@ -595,7 +643,9 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
     const ulonglong2* s = reinterpret_cast<const ulonglong2*>(sk + off);
     const ulonglong2* ss = reinterpret_cast<const ulonglong2*>(sksh + off);
     for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
-      const ulonglong2 x0 = c0[p], x1 = c1[p], sv = s[p], sw = ss[p];
+      ulonglong2 x0 = c0[p];
+      const ulonglong2 x1 = c1[p], sv = s[p], sw = ss[p];
+      if (sum_in) x0 = make_ulonglong2(red64(x0.x, q, c.one_shoup), red64(x0.y, q, c.one_shoup));
       lds_put2(sm, p, make_ulonglong2(addmod(x0.x, shoup_mul(x1.x, sv.x, sw.x, q), q),
                                       addmod(x0.y, shoup_mul(x1.y, sv.y, sw.y, q), q)));
     }
@@ -766,7 +816,7 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
                          logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0,
-                         (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr);
+                         (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr, 0);
     if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
@@ -1749,7 +1799,7 @@ size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
 
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s, const DecodeNoise* dn) {
+                    void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in) {
   if (!K) return;
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
@@ -1765,16 +1815,22 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
     const uint32_t xg = xcd_combos(p.L << (logR > 0 ? logR : 0));
-    if (logR > 0 && blkLog == 11 && dt.red_ok)
+    if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
                          s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
-    else if (logR > 0 && blkLog == 12 && dt.red_ok)
+    else if (logR > 0 && blkLog == 11 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+    else if (logR > 0 && blkLog == 12 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+    else if (logR > 0 && blkLog == 12 && dt.red_ok)
+      hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
                          s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
-                         logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh);
+                         logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh, sum_in ? 1 : 0);
     if (logR > 0 && fuse) {
       const uint64_t nbf = K * ((p.N >> logR) / 64);
       NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, logS,

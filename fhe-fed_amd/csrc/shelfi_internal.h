@@ -201,6 +201,8 @@ struct shelfi_ctx {
   // RCCL communicator of the multi-GPU combine (comm.cpp; ncclComm_t, opaque here)
   void* comm = nullptr;
   int comm_rank = 0, comm_world = 0;
+  hipStream_t comm_stream = nullptr;     // the pipelined combine's collectives (comm.cpp)
+  std::vector<hipEvent_t> comm_events;   // piece-ready events of the pipelined combine
 };
 
 namespace shelfi {
@@ -246,12 +248,17 @@ struct DecodeNoise {
 };
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr);
+                    void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr, bool sum_in = false);
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
 void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
                    uint64_t* pk, void* scratch, hipStream_t s);
 size_t keygen_scratch_bytes(const Params& p);
 
+// api.cpp: the arena aggregation (ctx lock held, weights checked), refused-slot check, weights
+void wavg_arena_enqueue(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                        uint64_t* out_dev, hipStream_t s);
+void arena_require_valid_locked(const shelfi_ctx* ctx, const uint64_t* a, size_t words);
+void check_wavg_weights(const float* w, size_t C, double delta);
 // comm.cpp: drop the context's RCCL communicator (if any)
 void comm_release(shelfi_ctx* ctx);
 // eval.cpp: drop the relinearization key (keys_only) or all EvalMult / ModReduce state

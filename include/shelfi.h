@@ -259,6 +259,18 @@ int shelfi_dev_allreduce(shelfi_ctx* ctx, uint64_t* partial_dev, size_t K, void*
  * (K % W == 0): each rank then decrypts its own slice, nothing is gathered */
 int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size_t K,
                               uint64_t* out_dev, void* stream);
+/* The whole learner-sharded step in one call, pipelined: this rank's arena of C learners
+ * (K ciphertexts each) is aggregated piece by piece on `stream`, and each piece's
+ * ncclReduceScatter runs on the context's own comm stream (ordered by HIP events) while the
+ * next piece is aggregated.  Rank r receives the combined aggregate of global ciphertexts
+ * [r Ks, min(K, (r+1) Ks)), Ks = shelfi_combine_share_cts(ctx, K) = ceil(K / W), contiguous in
+ * share_dev (Ks ciphertexts; slots past K are zero).  send_dev is scratch of W * Ks
+ * ciphertexts.  fold = 1 folds each piece into [0, q_t) on the comm stream; fold = 0 leaves
+ * the uint64 sums of W residues for shelfi_dev_decrypt_sum, which folds them on load (no
+ * separate pass).  Returns with the work enqueued: `stream` is ordered after the share. */
+size_t shelfi_combine_share_cts(const shelfi_ctx* ctx, size_t K);
+int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                             size_t pieces, uint64_t* send_dev, uint64_t* share_dev, int fold, void* stream);
 
 /* encode + encrypt n doubles (device) into K = ceil(n/batch) ciphertexts. */
 int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,
@@ -317,6 +329,11 @@ int shelfi_dev_rescale(shelfi_ctx* ctx, const uint64_t* in_dev, size_t K, uint32
 /* shelfi_dev_decrypt for ciphertexts of `towers` <= L towers (after ModReduce). */
 int shelfi_dev_decrypt_level(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t towers, double scale,
                              size_t n, double* out_dev, void* stream);
+/* shelfi_dev_decrypt of a multi-GPU combine's unfolded share: every residue is a uint64 sum of
+ * `terms` (1..16) canonical residues (shelfi_dev_combine_arena with fold = 0); the mod-q fold
+ * happens inside decrypt's first pass. */
+int shelfi_dev_decrypt_sum(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32_t terms, double scale,
+                           size_t n, double* out_dev, void* stream);
 
 /* ---- test hooks (host-visible tables) ------------------------------------- */
 /* CKKS special-FFT twiddles (flat, index lenh + j) as used by the kernels. */

@@ -72,9 +72,15 @@ def test_bench_ciphertext_sharded_path_one_rank():
 
 def test_bench_learner_sharded_c_abi_combine_one_rank():
     """--combine shelfi: the learner-sharded step through the library's own RCCL
-    communicator (shelfi_comm_init / shelfi_dev_reduce_scatter), id broadcast over the
-    torch process group; bench's end-to-end check on the owned aggregate."""
-    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist", "--shard", "learners", "--combine", "shelfi", "--no-alt"] + COMMON)
-    assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
+    communicator, pipelined inside libshelfi (shelfi_dev_combine_arena), id broadcast over the
+    torch process group; bench's end-to-end check decrypts the unfolded share
+    (shelfi_dev_decrypt_sum) and the line records the cross-check against torch's
+    all_reduce + modq on the same partial sums."""
+    for extra in ([], ["--shelfi-fold"]):
+        r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
+                  "--force-dist", "--shard", "learners", "--combine", "shelfi", "--pieces", "3",
+                  "--no-alt"] + extra + COMMON)
+        assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
+        assert r["c_abi_comm_check"]["ok"], r["c_abi_comm_check"]
+        assert "shelfi_dev_combine_arena" in r["config"]["workload"]

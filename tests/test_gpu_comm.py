@@ -97,3 +97,61 @@ def test_combine_of_real_partials_matches_single_gpu_aggregate(ck):
     finally:
         comm.close()
     assert torch.equal(dev, full)
+
+
+@pytest.mark.parametrize("C,K,pieces,fold", [(4, 7, 1, True), (4, 7, 3, True), (5, 9, 8, False),
+                                             (20, 5, 2, True)])
+def test_pipelined_c_abi_combine_one_rank(ck, C, K, pieces, fold):
+    """shelfi_dev_combine_arena (the pipelined C-ABI step: wavg pieces on the caller's
+    stream, ncclReduceScatter pieces on the library's comm stream, HIP events between them)
+    on a one-rank communicator: the share equals the single-GPU arena aggregate bit for bit,
+    and its decryption (decrypt_sum at terms = world) equals the plain decryption."""
+    B = ck.info()["batch"]
+    rng = np.random.default_rng(C * 100 + K)
+    cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B - 3)).cuda()) for _ in range(C)]
+    w = list(rng.dirichlet(np.ones(C)))
+    ar = D.Arena(ck, C, K)
+    for i, c in enumerate(cts):
+        ar.put(i, c)
+    ref = ar.wavg(w)
+    comm = X.Comm(ck, rank=0, world=1)
+    try:
+        Ks = comm.share_cts(K)
+        assert Ks == K
+        send, share = D.empty_ct(ck, Ks), D.empty_ct(ck, Ks)
+        for _ in range(2):  # the events and the comm stream are reused by the next call
+            comm.combine_arena(ar, w, K, send, share, pieces=pieces, fold=fold)
+        torch.cuda.synchronize()
+        assert torch.equal(share, ref)
+        delta = ck.info()["delta"]
+        n = K * B - 3
+        assert torch.equal(D.decrypt_sum(ck, share, 1, n, delta * delta), D.decrypt(ck, ref, n, delta * delta))
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("ring", ["cfg2", "no_columns_pass"])
+def test_decrypt_of_unfolded_sums_equals_decrypt(ck, tmp_path, ring):
+    """Residues x + k q (k <= 15: what a uint64 SUM of 16 ranks' partials holds before the
+    fold) decrypt bit-identically to x through decrypt_sum: the fused fold in the compile-time
+    first INTT pass (2^15) and the generic pass (2^11, no columns pass)."""
+    if ring == "cfg2":
+        c = ck
+    else:
+        c = m.CKKS("ckks", 512, 52, str(tmp_path) + os.sep, ringDim=2048, seed=3, decodeNoise=False)
+        assert c.genCryptoContextAndKeyGen() == 1
+    inf = c.info()
+    q = np.array(inf["moduli"], np.uint64)
+    B, delta = inf["batch"], inf["delta"]
+    x = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, 3 * B)).cuda()
+    ct = D.encrypt(c, x)
+    h = ct.cpu().numpy().view(np.uint64).copy()
+    k = np.random.default_rng(6).integers(0, 16, h.shape, dtype=np.uint64)
+    k[0, 0, 0, :8] = 15
+    lazy = h + k * q[None, None, :, None]
+    assert (lazy >= q[None, None, :, None]).any()
+    lz = torch.from_numpy(lazy.view(np.int64)).cuda()
+    got = D.decrypt_sum(c, lz, 16, 3 * B, delta)
+    assert torch.equal(got, D.decrypt(c, ct, 3 * B, delta))
+    with pytest.raises(ValueError, match="1..16"):
+        D.decrypt_sum(c, lz, 17, 3 * B, delta)

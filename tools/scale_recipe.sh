@@ -2,7 +2,7 @@
 # Multi-GPU launch recipe for bench.py on ONE node (the driver's SCALE protocol):
 # torch.distributed.run starts one child process per GPU (no exec after GPU init).
 #   tools/scale_recipe.sh 8                      # headline: learner-sharded + pipelined RCCL reduce_scatter
-#   tools/scale_recipe.sh 8 --combine shelfi     # the same combine through libshelfi's C-ABI communicator
+#   tools/scale_recipe.sh 8 --combine shelfi     # the same pipelined combine inside libshelfi (C ABI)
 #   tools/scale_recipe.sh 8 --shard cts          # ciphertext-sharded, no collective
 # The default run also cross-checks the C-ABI communicator (c_abi_comm_check in the JSON).
 set -euo pipefail
