@@ -218,6 +218,8 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
       c.red_ok = E >= 40;
       c.red_sh = E >= 32 ? E - 32 : 0;
       c.red_r = c.red_ok ? (uint32_t)(((u128)1 << (32 + E)) / q) : 0;
+      c.crt_sh = E >= 31 ? E - 31 : 0;
+      c.inv_q32 = (float)((double)(1ull << c.crt_sh) / (double)q);
     }
     // twiddles: psi^bitrev(i), psi^-bitrev(i)
     const uint64_t ipsi = invmod(p.psi[t], q);

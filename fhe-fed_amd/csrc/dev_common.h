@@ -104,6 +104,8 @@ __device__ __forceinline__ uint64_t red_any(uint64_t x, const TowerConst& c) {
   const uint64_t r = x + (uint64_t)k * (uint32_t)c.nq + ((uint64_t)(k * (uint32_t)(c.nq >> 32)) << 32);
   return csub_neg(r, c.nq);
 }
+// Towers below this bound skip the forward reductions of the encrypt passes (NORED).
+constexpr uint64_t kNoRedQ = 1ull << 57;
 // Reduction schedule for canonical inputs (bounds in units of q): stage s reduces its x
 // inputs only when its outputs could otherwise reach 16q; fwd_bound(S) bounds the
 // outputs after S stages.
@@ -240,6 +242,67 @@ __device__ __forceinline__ void chacha20_block(const Key8& key, uint64_t counter
 #pragma unroll
   for (int i = 0; i < 8; ++i)
     out[i] = (uint64_t)(x[2 * i] + s[2 * i]) | ((uint64_t)(x[2 * i + 1] + s[2 * i + 1]) << 32);
+}
+
+// The same block as 16 little-endian 32-bit words.
+__device__ __forceinline__ void chacha20_block32(const Key8& key, uint64_t counter, uint64_t nonce,
+                                                 uint32_t out[16]) {
+  uint64_t w[8];
+  chacha20_block(key, counter, nonce, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    out[2 * i] = (uint32_t)w[i];
+    out[2 * i + 1] = (uint32_t)(w[i] >> 32);
+  }
+}
+
+// ---- encrypt sampler v2 (round 3; DESIGN.md §2.3, oracle or_sample_encrypt) ----
+// Stream of ciphertext g (nonce (1 << 56) | g), in ChaCha20 blocks of 16 32-bit words, with
+// N16 = N / 16 and coefficient j = h + N16 i (h < N16, i < 16):
+//   v  : blocks [0, N/64): block h/4, words 4 (h mod 4) .. +3 = a 128-bit U (word 0 lowest);
+//        v_j = trit_i - 1 with trit_i the i-th base-3 digit of U / 2^128 (U <- 3U, the carry
+//        out of bit 128 is the digit): 16 ternary samples per 128 bits (was one 64-bit word
+//        each); the 16-digit pattern is within 3^16 / 2^128 < 2^-102 of uniform.
+//   e0 : block N/64 + h, word i;  e1: block N/64 + N16 + h, word i: a 32-bit word w gives the
+//        sign (w & 1) and the top 31 bits of a 63-bit uniform U63 = (w >> 1) 2^32 + lo32;
+//        |e| = #{t : U63 >= cdt[t]}.  lo32 (word i of block N/64 + 2 N16 + h for e0, + 3 N16
+//        for e1) only matters when w >> 1 equals the top 31 bits of a CDT entry (probability
+//        ~2^-26 per sample) and is generated only then: the distribution is the 63-bit CDT's.
+// The v / e0 / e1 words of a column of 16 coefficients come from 1/4 + 1 + 1 ChaCha blocks
+// instead of 6.
+__device__ __forceinline__ uint32_t trit_next(uint32_t (&u)[4]) {  // U <- 3U mod 2^128, returns the carry
+  uint64_t c = 0;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    c = (uint64_t)u[l] * 3u + c;
+    u[l] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+// Word i of a stream block, out of line: the rare tie path of gauss32 (kept out of the
+// unrolled sampling loops' code).
+__device__ __noinline__ uint32_t chacha20_word(Key8 key, uint64_t counter, uint64_t nonce, uint32_t i) {
+  uint32_t t[16];
+  chacha20_block32(key, counter, nonce, t);
+  uint32_t r = t[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) r = (i == (uint32_t)j) ? t[j] : r;
+  return r;
+}
+// |e| and sign from a 32-bit word, tab_hi / tab_lo = the CDT's top 31 / low 32 bits, padded to
+// 64 entries with 0xFFFFFFFF tops (above every 31-bit value); lo32() fetches the tie word.
+template <class Lo>
+__device__ __forceinline__ int64_t gauss32(uint32_t w, const uint32_t* tab_hi, const uint32_t* tab_lo, Lo lo32) {
+  const uint32_t H = w >> 1;
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) k += (tab_hi[k + step - 1] < H) ? step : 0u;
+  if (tab_hi[k] == H) {  // tie on the top 31 bits: the low half decides (rare, divergent)
+    const uint32_t lo = lo32();
+    while (k < 64 && tab_hi[k] == H && tab_lo[k] <= lo) ++k;
+  }
+  return (w & 1) ? -(int64_t)k : (int64_t)k;
 }
 
 __device__ __forceinline__ int64_t gauss_sample(uint64_t r, const uint64_t* __restrict__ cdt,
@@ -443,7 +506,10 @@ constexpr uint32_t lpad_size(int BL) { return (1u << BL) + (1u << (BL - 3)); }
 // Reduction schedule: the stage at local half-size 2^h reduces its x inputs iff h is
 // even, so the block's last stage (h = 0) always does: inputs below 12q (the columns
 // pass leaves < 8q), outputs below 12q, never above 16q in between (ct_bfly_s).
-template <int BL, int H0, int KC>
+// NORED (towers with q < 2^57, kNoRedQ): no reductions at all — a block's 11 stages add at
+// most 44q to inputs below 17q (enc_cols_fused<..> leaves its NORED towers unreduced too), and
+// 65q < 2^64 for the combine that follows.
+template <int BL, int H0, int KC, bool NORED = false>
 __device__ __forceinline__ void fwd_set_ct(uint64_t (&x)[1 << KC], uint32_t g,
                                            const ulonglong2* __restrict__ tb, uint64_t q,
                                            uint64_t n8q) {
@@ -456,7 +522,7 @@ __device__ __forceinline__ void fwd_set_ct(uint64_t (&x)[1 << KC], uint32_t g,
       const ulonglong2 W = tw[gs];
 #pragma unroll
       for (int mm = 0; mm < hm; ++mm) {
-        if (((H0 - i) & 1) == 0)
+        if (!NORED && ((H0 - i) & 1) == 0)
           ct_bfly_s<true>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
         else
           ct_bfly_s<false>(x[gs * 2 * hm + mm], x[gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
@@ -466,7 +532,7 @@ __device__ __forceinline__ void fwd_set_ct(uint64_t (&x)[1 << KC], uint32_t g,
 }
 // One forward chunk over all 2^(BL-KC) sets of the block (NS per thread): Load(j) gives
 // element j, Store(r, j0, x) receives set r's transformed elements (positions j0 + m 2^dLog).
-template <int BL, int H0, int KC, class Load, class Store>
+template <int BL, int H0, int KC, bool NORED = false, class Load, class Store>
 __device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, uint64_t q,
                                              uint64_t n8q, Load ld, Store st) {
   constexpr int M = 1 << KC, dLog = H0 - KC + 1, NS = (1 << (BL - KC)) / 256;
@@ -480,7 +546,7 @@ __device__ __forceinline__ void fwd_chunk_ct(const ulonglong2* __restrict__ tb, 
     uint64_t x[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) x[m] = ld(j0 + (m << dLog), pj0 + lofs<(1 << dLog)>(m));
-    fwd_set_ct<BL, H0, KC>(x, g, tb, q, n8q);
+    fwd_set_ct<BL, H0, KC, NORED>(x, g, tb, q, n8q);
     st(r, j0, pj0, x);
   }
 }

@@ -25,6 +25,8 @@
 // multiplications use Shoup's precomputed quotient (w' = floor(w 2^64 / q)).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev_common.h"
 #include "shelfi_internal.h"
 
@@ -551,6 +553,120 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
   }
 }
 
+// Persistent, software-pipelined form of ntt_fwd_blocks_enc_ct (round 3), the same idea as
+// ntt_inv_blocks_dec_pp: a workgroup owns one (tower, block) combo and walks ciphertexts
+// k0, k0 + P, ...; the combo's twiddle slice sits in LDS (copied once); each polynomial's
+// first-chunk pbuf words are loaded into registers while the previous polynomial is being
+// transformed, and the public-key words of the combine are requested one polynomial ahead.
+// Same arithmetic and outputs as ntt_fwd_blocks_enc_ct.
+// NR: the launch covers towers [t0, t0 + nt) whose columns pass ran unreduced (q < kNoRedQ,
+// enc_cols_fused's t_split): no reductions in the block stages either (fwd_set_ct).
+template <int BL, int K1, int K2, int K3, int K4, bool NR>
+__global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
+    const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
+    const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk, const uint64_t* __restrict__ pksh,
+    uint64_t* __restrict__ ct, uint32_t K, uint32_t per_combo, uint32_t t0, uint32_t nt) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
+  constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
+  __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sstart = logN - BL;
+  const uint32_t ncombo = nt << sstart;
+  const uint32_t combo = blockIdx.x % ncombo;
+  const uint32_t b = combo & ((1u << sstart) - 1), t = t0 + (combo >> sstart);
+  const TowerConst& cst = tcs[t];
+  const uint64_t q = cst.q, n8q = cst.n8q;
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t LN = (uint64_t)L << logN;
+  {
+    const ulonglong2* __restrict__ src = twb + off;
+    for (uint32_t i = threadIdx.x; i < (1u << BL); i += 256) tws[i] = src[i];
+  }
+  uint64_t pf[NS1][M1];              // the next polynomial's first-chunk words
+  ulonglong2 P[NSL][ML / 2], Ps[NSL][ML / 2];  // the next combine's key words (b or a)
+  uint64_t V[NSL][ML];                // NTT(v) at this thread's last-chunk positions
+  const auto fetch = [&](uint32_t kk, int poly) {
+    const uint64_t* __restrict__ src = pbuf + ((uint64_t)kk * 3 + poly) * LN + off;
+#pragma unroll
+    for (int r = 0; r < NS1; ++r)
+#pragma unroll
+      for (int m = 0; m < M1; ++m) pf[r][m] = __builtin_nontemporal_load(src + threadIdx.x + 256u * r + (m << D1));
+  };
+  const auto fetch_key = [&](int poly) {  // poly 1: b, poly 2: a
+#pragma unroll
+    for (int r = 0; r < NSL; ++r) {
+      const uint64_t e = (poly == 1 ? 0 : LN) + off + ((threadIdx.x + 256u * r) << K4);
+#pragma unroll
+      for (int m = 0; m < ML; m += 2) {
+        P[r][m / 2] = *reinterpret_cast<const ulonglong2*>(pk + e + m);
+        Ps[r][m / 2] = *reinterpret_cast<const ulonglong2*>(pksh + e + m);
+      }
+    }
+  };
+  uint32_t k = blockIdx.x / ncombo;
+  if (k < K) fetch(k, 0);
+  __syncthreads();  // the twiddle slice is in LDS
+  const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
+#pragma unroll 1
+  for (; k < K; k += per_combo) {
+#pragma unroll 1
+    for (int poly = 0; poly < 3; ++poly) {
+      uint64_t x[NS1][M1];
+#pragma unroll
+      for (int r = 0; r < NS1; ++r)
+#pragma unroll
+        for (int m = 0; m < M1; ++m) x[r][m] = pf[r][m];
+      // the next polynomial's words (or the next ciphertext's v) and this one's key words
+      if (poly < 2)
+        fetch(k, poly + 1);
+      else if (k + per_combo < K)
+        fetch(k + per_combo, 0);
+      if (poly > 0) fetch_key(poly);
+#pragma unroll
+      for (int r = 0; r < NS1; ++r) {  // first chunk: one group, block-uniform twiddles
+        fwd_set_ct<BL, BL - 1, K1, NR>(x[r], 0u, tws, q, n8q);
+        const uint32_t p0 = lpad(threadIdx.x + 256u * r);
+#pragma unroll
+        for (int m = 0; m < M1; ++m) sm[p0 + lofs<(1 << D1)>(m)] = x[r][m];
+      }
+      __syncthreads();
+      fwd_chunk_ct<BL, BL - 1 - K1, K2, NR>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
+#pragma unroll
+        for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2))>(m)] = y[m];
+      });
+      __syncthreads();
+      fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3, NR>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
+#pragma unroll
+        for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2 - K3))>(m)] = y[m];
+      });
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < NSL; ++r) {
+        const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4, pj0 = lpad(j0);
+        uint64_t y[ML];
+#pragma unroll
+        for (int m = 0; m < ML; ++m) y[m] = sm[pj0 + m];
+        fwd_set_ct<BL, K4 - 1, K4, NR>(y, g, tws, q, n8q);
+        if (poly == 0) {  // NTT(v), lazy (< 12q): only ever a Shoup multiplicand
+#pragma unroll
+          for (int m = 0; m < ML; ++m) V[r][m] = y[m];
+        } else {  // poly 1: c0 = v*b + (m + e0); poly 2: c1 = v*a + e1
+          uint64_t* __restrict__ dst = ct + ((uint64_t)k * 2 + (poly - 1)) * LN + off + j0;
+#pragma unroll
+          for (int m = 0; m < ML; m += 2) {
+            ulonglong2 c;
+            c.x = red_any(shoup_lazy(V[r][m], P[r][m / 2].x, Ps[r][m / 2].x, q) + y[m], cst);
+            c.y = red_any(shoup_lazy(V[r][m + 1], P[r][m / 2].y, Ps[r][m / 2].y, q) + y[m + 1], cst);
+            *reinterpret_cast<ulonglong2*>(dst + m) = c;
+          }
+        }
+      }
+      __syncthreads();  // LDS is refilled by the next polynomial
+    }
+  }
+}
+
 // Decrypt's first INTT pass at compile-time shape (chunks K1..K4, sum BL; needs
 // logN > BL): c0 + c1*s is formed straight into the first chunk's registers from the
 // ciphertext batch [K][2][L][N], and the last chunk writes the lazy ([0, 8q)) block to
@@ -612,6 +728,136 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
 #pragma unroll
     for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = x[m];
   });
+}
+
+// Persistent, software-pipelined form of ntt_inv_blocks_dec_ct (round 3).  The one-shot
+// kernel loads its whole first chunk from HBM and only then computes, and all its workgroups
+// start together: measured 0.48 of the VALU issue peak and ~3.6 TB/s, neither bound reached.
+// Here a workgroup owns one (tower, block) combo and walks ciphertexts k0, k0 + P, ...:
+//  * the combo's 2^BL twiddle pairs are copied into LDS once (32 KiB), so the per-chunk
+//    twiddle reads leave the vector-memory queue (whose in-order vmcnt would otherwise make
+//    every twiddle wait drain the prefetch below);
+//  * the secret-key words s, s' of the first chunk's elements stay in registers;
+//  * ciphertext k + P's c0 / c1 words are loaded into registers right after ciphertext k's
+//    have been consumed, so their HBM latency hides behind k's stages.
+// Same arithmetic, same lazy bounds and same dbuf contents as ntt_inv_blocks_dec_ct.
+template <int BL, int K1, int K2, int K3, int K4, bool SUM = false>
+__global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restrict__ dbuf, uint32_t L,
+                                                             uint32_t logN,
+                                                             const ulonglong2* __restrict__ twb,
+                                                             const TowerConst* __restrict__ tcs,
+                                                             const uint64_t* __restrict__ ct,
+                                                             const uint64_t* __restrict__ sk,
+                                                             const uint64_t* __restrict__ sksh, uint32_t K,
+                                                             uint32_t per_combo) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256;
+  __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
+  __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  const uint32_t sstart = logN - BL;
+  const uint32_t ncombo = L << sstart;
+  const uint32_t combo = blockIdx.x % ncombo;
+  const uint32_t b = combo & ((1u << sstart) - 1), t = combo >> sstart;
+  const TowerConst& cst = tcs[t];
+  const uint64_t q = cst.q, n4q = cst.n4q, n8q = cst.n8q;
+  const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
+  const uint64_t LN = (uint64_t)L << logN;
+  {
+    const ulonglong2* __restrict__ src = twb + off;
+    for (uint32_t i = threadIdx.x; i < (1u << BL); i += 256) tws[i] = src[i];
+  }
+  // first chunk (T0 = 0): set r of this thread = elements (tid + 256 r) 2^K1 + m
+  uint64_t sv[NS1][M1], sw[NS1][M1], p0[NS1][M1], p1[NS1][M1];
+#pragma unroll
+  for (int r = 0; r < NS1; ++r)
+#pragma unroll
+    for (int m = 0; m < M1; ++m) {
+      const uint32_t j = ((threadIdx.x + 256u * r) << K1) + m;
+      sv[r][m] = sk[off + j];
+      sw[r][m] = sksh[off + j];
+    }
+  uint32_t k = blockIdx.x / ncombo;
+  const auto fetch = [&](uint32_t kk) {
+    const uint64_t* __restrict__ c0 = ct + (uint64_t)kk * 2 * LN + off;
+#pragma unroll
+    for (int r = 0; r < NS1; ++r)
+#pragma unroll
+      for (int m = 0; m < M1; ++m) {
+        const uint32_t j = ((threadIdx.x + 256u * r) << K1) + m;
+        p0[r][m] = __builtin_nontemporal_load(c0 + j);
+        p1[r][m] = __builtin_nontemporal_load(c0 + LN + j);
+      }
+  };
+  if (k < K) fetch(k);
+  __syncthreads();  // the twiddle slice is in LDS
+  const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
+#pragma unroll 1
+  for (; k < K; k += per_combo) {
+    uint64_t x[NS1][M1];
+#pragma unroll
+    for (int r = 0; r < NS1; ++r)
+#pragma unroll
+      for (int m = 0; m < M1; ++m) {
+        const uint64_t a0 = SUM ? red_any(p0[r][m], cst) : p0[r][m];
+        x[r][m] = csub_neg(a0 + shoup_lazy(p1[r][m], sv[r][m], sw[r][m], q), n4q);
+      }
+    if (k + per_combo < K) fetch(k + per_combo);  // lands while this ciphertext is transformed
+#pragma unroll
+    for (int r = 0; r < NS1; ++r) {  // first chunk: stages i < K1 of the contiguous sets
+      const uint32_t g = threadIdx.x + 256u * r;
+#pragma unroll
+      for (int i = 0; i < K1; ++i) {
+        const int hm = 1 << i;
+        const ulonglong2* tw = tws + (1u << (BL - 1 - i)) + (g << (K1 - 1 - i));
+#pragma unroll
+        for (int gs = 0; gs < (M1 >> (i + 1)); ++gs) {
+          const ulonglong2 W = tw[gs];
+#pragma unroll
+          for (int mm = 0; mm < hm; ++mm) {
+            if (gs_in8<false>(i, mm))
+              gs_bfly_b<true>(x[r][gs * 2 * hm + mm], x[r][gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+            else
+              gs_bfly_b<false>(x[r][gs * 2 * hm + mm], x[r][gs * 2 * hm + mm + hm], W.x, W.y, q, n8q);
+          }
+        }
+      }
+      const uint32_t pj0 = lpad(g << K1);
+#pragma unroll
+      for (int m = 0; m < M1; ++m) sm[pj0 + lofs<1>(m)] = x[r][m];
+    }
+    __syncthreads();
+    inv_chunk_ct<BL, K1, K2, true>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
+#pragma unroll
+      for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << K1)>(m)] = y[m];
+    });
+    __syncthreads();
+    inv_chunk_ct<BL, K1 + K2, K3, true>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
+#pragma unroll
+      for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (K1 + K2))>(m)] = y[m];
+    });
+    __syncthreads();
+    uint64_t* __restrict__ dst = dbuf + (uint64_t)k * LN + off;
+    inv_chunk_ct<BL, BL - K4, K4, true>(tws, q, n8q, lds_ld, [&](int, uint32_t j0, uint32_t, auto& y) {
+#pragma unroll
+      for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = y[m];
+    });
+    __syncthreads();  // sm is rewritten by the next ciphertext's first chunk
+  }
+}
+
+// Workgroups of the persistent decrypt / encrypt block passes: LDS-bound residency per CU
+// times the CUs, spread evenly over the (tower, block) combos (at least one each).
+static uint32_t pp_per_combo(uint32_t ncombo, uint64_t K, uint32_t per_cu) {
+  static const uint32_t cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return (uint32_t)n;
+  }();
+  uint64_t pc = (uint64_t)cus * per_cu / ncombo;
+  if (pc < 1) pc = 1;
+  if (pc > K) pc = K;
+  return (uint32_t)pc;
 }
 
 // Inverse blocks pass: small half-sizes first (LDS), then the top LOGR stages on
@@ -975,12 +1221,20 @@ __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ 
 
 
 // -------------------------------------------------------------- encrypt ----
-// One thread = ChaCha20 block bb of each sampled polynomial, which feeds the 8
-// coefficients j = bb + u N/8 (u = 0..7), so every store is a coalesced row.
+// One thread = sample group h of a ciphertext: the 16 coefficients j = h + (N/16) i of the
+// v2 sampler stream (dev_common.h), so every store is a coalesced row.
 // m_j = llround(FFTinv(x)[bitrev(i)] / S * Delta) at j = i*gap (real part) and
 // N/2 + i*gap (imaginary part) (CKKSPackedEncoding::Encode layout).  Output is the
 // compact per-coefficient record {int64 m + e0, int16 (e1 << 8) | (uint8)v} — 10 bytes
 // instead of the 3 L residues the NTT needs, which ntt_fwd_cols_enc expands per tower.
+__device__ __forceinline__ void load_cdt32(const uint64_t* __restrict__ cdt, int T, uint32_t* hi, uint32_t* lo) {
+  if (threadIdx.x < 64) {
+    const uint64_t v = (int)threadIdx.x < T ? cdt[threadIdx.x] : ~0ull;
+    hi[threadIdx.x] = (int)threadIdx.x < T ? (uint32_t)(v >> 32) : 0xFFFFFFFFu;
+    lo[threadIdx.x] = (uint32_t)v;
+  }
+}
+
 __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
                                                        uint64_t K, uint32_t logN, uint32_t logS,
                                                        double delta,
@@ -989,27 +1243,28 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
                                                        int64_t* __restrict__ me0,
                                                        int16_t* __restrict__ ve,
                                                        uint32_t* __restrict__ flag) {
-  const uint32_t N = 1u << logN, S = 1u << logS, E = N >> 3;
-  __shared__ uint64_t tab[64];
-  if (threadIdx.x < 64) tab[threadIdx.x] = (int)threadIdx.x < T ? cdt[threadIdx.x] : ~0ull;
+  const uint32_t N = 1u << logN, S = 1u << logS, N16 = N >> 4, V0 = N >> 6;
+  __shared__ uint32_t thi[64], tlo[64];
+  load_cdt32(cdt, T, thi, tlo);
   __syncthreads();
   const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const uint64_t k = gid >> (logN - 3);
+  const uint64_t k = gid >> (logN - 4);
   if (k >= K) return;
-  const uint32_t bb = (uint32_t)(gid & (E - 1));
+  const uint32_t h = (uint32_t)(gid & (N16 - 1));
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
   const double dS = (double)S;
   const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
-  uint64_t w[8];
-  int32_t vv[8];
-  chacha20_block(key, bb, nonce, w);
+  uint32_t w[16];
+  chacha20_block32(key, h >> 2, nonce, w);
+  uint32_t u[4] = {w[4 * (h & 3)], w[4 * (h & 3) + 1], w[4 * (h & 3) + 2], w[4 * (h & 3) + 3]};
+  int32_t vv[16];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) vv[u] = (int32_t)ternary_sample(w[u]);
-  chacha20_block(key, E + bb, nonce, w);
+  for (int i = 0; i < 16; ++i) vv[i] = (int32_t)trit_next(u) - 1;
+  chacha20_block32(key, V0 + h, nonce, w);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const uint32_t j = bb + u * E;
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t j = h + N16 * i;
     const uint32_t jj = j < half ? j : j - half;
     int64_t m = 0;
     if ((jj & ((1u << gapLog) - 1)) == 0) {
@@ -1018,13 +1273,14 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
       if (!(fabs(val) <= lim)) atomicOr(flag, 1u);  // also catches NaN / inf
       m = round_half_away(val);
     }
-    me0[(k << logN) + j] = m + gauss_sample_lds(w[u], tab);
+    me0[(k << logN) + j] = m + gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 2 * N16 + h, nonce, i); });
   }
-  chacha20_block(key, 2 * E + bb, nonce, w);
+  chacha20_block32(key, V0 + N16 + h, nonce, w);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int32_t e1 = (int32_t)gauss_sample_lds(w[u], tab);
-    ve[(k << logN) + bb + u * E] = (int16_t)((e1 << 8) | (vv[u] & 0xFF));
+  for (int i = 0; i < 16; ++i) {
+    const int32_t e1 =
+        (int32_t)gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 3 * N16 + h, nonce, i); });
+    ve[(k << logN) + h + N16 * i] = (int16_t)((e1 << 8) | (vv[i] & 0xFF));
   }
 }
 
@@ -1094,12 +1350,11 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 
 // Encode + sampling + the columns pass in one kernel (enc_prep_kernel followed by the three
 // ntt_fwd_cols_enc launches, without the 10-byte-per-coefficient record in between):
-// thread = column c of ciphertext k, coefficients j = c + BLK r (r < R = 2^LOGR).  With
-// E8 = N/8 = BLK 2^(LOGR-3) (LOGR >= 3), ChaCha20 block bb feeds coefficients bb + E8 w
-// (w < 8), so the blocks bb = c + BLK u (u < 2^(LOGR-3)) of each stream hold exactly this
-// column: row r = u + 2^(LOGR-3) w.  Same stream words, same samples, same rounding as
-// enc_prep_kernel, then for every tower the columns stages of v, m + e0 and e1 and the
-// lazy stores into pbuf that ntt_fwd_blocks_enc_ct reads.
+// thread = column c of ciphertext k, coefficients j = c + BLK r (r < R = 2^LOGR).  In the v2
+// sampler stream (dev_common.h) coefficient j = h + (N/16) i: the column's rows are the sample
+// indices i = i0 + (16/R) r of group h = c mod N/16 (i0 = c div N/16; LOGR = 4: the whole group).
+// Same samples and rounding as enc_prep_kernel, then for every tower the columns stages of v,
+// m + e0 and e1 and the lazy stores into pbuf that the blocks pass reads.
 template <int LOGR>
 __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
@@ -1109,24 +1364,28 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
                                                       const uint64_t* __restrict__ tw,
                                                       const uint64_t* __restrict__ twp,
                                                       uint64_t* __restrict__ out,
-                                                      uint32_t* __restrict__ flag) {
-  constexpr int R = 1 << LOGR, NB = 1 << (LOGR - 3);
-  static_assert(LOGR >= 3, "a column must own whole ChaCha20 blocks");
-  __shared__ uint64_t tab[64];
-  if (threadIdx.x < 64) tab[threadIdx.x] = (int)threadIdx.x < T ? cdt[threadIdx.x] : ~0ull;
+                                                      uint32_t* __restrict__ flag, uint32_t t_split) {
+  constexpr int R = 1 << LOGR, IS = 16 / R;
+  static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
+  __shared__ uint32_t thi[64], tlo[64];
+  load_cdt32(cdt, T, thi, tlo);
   __syncthreads();
-  const uint32_t N = 1u << logN, BLK = N >> LOGR, E8 = N >> 3, half = N >> 1;
+  const uint32_t N = 1u << logN, BLK = N >> LOGR, N16 = N >> 4, V0 = N >> 6;
   const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = gid >> (logN - LOGR);
   if (k >= K) return;
   const uint32_t c = (uint32_t)(gid & (BLK - 1));
+  const uint32_t h = c & (N16 - 1), i0 = c >> (logN - 4);
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   const uint32_t S = 1u << logS, gapLog = logN - 1 - logS;
   const double invS = 1.0 / (double)S;  // a power of two: x * (1/S) == x / S exactly
   const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
   const uint64_t LN = (uint64_t)L << logN;
   // columns stages of one polynomial of tower t (values x[r] < q) and its lazy store
-  auto cols = [&](uint64_t (&x)[R], uint32_t t, const TowerConst& cst, int poly) {
+  // (towers with q < kNoRedQ run unreduced (NORED, fwd_set_ct): no stage reductions, no
+  // store reduction; the blocks pass knows)
+  auto cols = [&](uint64_t (&x)[R], uint32_t t, const TowerConst& cst, int poly, auto nored) __attribute__((always_inline)) {
+    constexpr bool NR = decltype(nored)::value;
     const uint64_t q = cst.q;
     const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
     const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
@@ -1139,7 +1398,7 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
 #pragma unroll
         for (int jj = 0; jj < tr; ++jj) {
           const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
-          if (fwd_red_at(s))
+          if (!NR && fwd_red_at(s))
             ct_bfly_s<true>(x[r0], x[r1], W, Wp, q, cst.n8q);
           else
             ct_bfly_s<false>(x[r0], x[r1], W, Wp, q, cst.n8q);
@@ -1148,46 +1407,63 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
     }
     uint64_t* __restrict__ o = out + (k * 3 + poly) * LN + ((uint64_t)t << logN) + c;
 #pragma unroll
-    for (int r = 0; r < R; ++r) o[(uint64_t)r * BLK] = fwd_bound(LOGR) > 8 ? csub_neg(x[r], cst.n8q) : x[r];
+    for (int r = 0; r < R; ++r)
+      o[(uint64_t)r * BLK] = (!NR && fwd_bound(LOGR) > 8) ? csub_neg(x[r], cst.n8q) : x[r];
   };
-  // phase 1: v (stream blocks [0, E8)) and e1 ([2 E8, 3 E8)), packed (e1 << 8) | (uint8) v
+  // phase 1: v (16 digits of a 128-bit word group) and e1, packed (e1 << 8) | (uint8) v
   {
     int32_t sv[R];
+    {
+      uint32_t wv[16];
+      chacha20_block32(key, h >> 2, nonce, wv);
+      uint32_t u[4] = {wv[4 * (h & 3)], wv[4 * (h & 3) + 1], wv[4 * (h & 3) + 2], wv[4 * (h & 3) + 3]};
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      uint64_t w[8];
-      chacha20_block(key, c + BLK * u, nonce, w);
-#pragma unroll
-      for (int ww = 0; ww < 8; ++ww) sv[u + NB * ww] = (int32_t)ternary_sample(w[ww]) & 0xFF;
-    }
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      uint64_t w[8];
-      chacha20_block(key, 2 * E8 + c + BLK * u, nonce, w);
-#pragma unroll
-      for (int ww = 0; ww < 8; ++ww) sv[u + NB * ww] |= (int32_t)gauss_sample_lds(w[ww], tab) << 8;
-    }
-#pragma unroll 1
-    for (uint32_t t = 0; t < L; ++t) {
-      const TowerConst cst = tcs[t];
-#pragma unroll 1
-      for (int poly = 0; poly < 3; poly += 2) {
-        uint64_t x[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = small_mod(poly == 0 ? (int32_t)(int8_t)(sv[r] & 0xFF) : (sv[r] >> 8), cst.q);
-        cols(x, t, cst, poly);
+      for (int i = 0; i < 16; ++i) {
+        const int32_t d = (int32_t)trit_next(u) - 1;
+        if (IS == 1) {
+          sv[i] = d & 0xFF;
+        } else if ((i % IS) == 0) {
+          if (i0 == 0) sv[i / IS] = d & 0xFF;
+        } else if (i0 == 1) {
+          sv[i / IS] = d & 0xFF;
+        }
       }
     }
+    {
+      uint32_t we[16];
+      chacha20_block32(key, V0 + N16 + h, nonce, we);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t i = IS == 1 ? (uint32_t)r : i0 + IS * r;
+        const uint32_t wi = IS == 1 ? we[r] : (i0 ? we[IS * r + 1] : we[IS * r]);  // no dynamic register index
+        sv[r] |= (int32_t)gauss32(wi, thi, tlo, [&] { return chacha20_word(key, V0 + 3 * N16 + h, nonce, i); }) << 8;
+      }
+    }
+    // towers [0, t_split) reduced, [t_split, L) unreduced (q < kNoRedQ; the blocks pass knows)
+    const auto small_polys = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
+#pragma unroll 1
+      for (uint32_t t = ta; t < tb; ++t) {
+        const TowerConst cst = tcs[t];
+#pragma unroll 1
+        for (int poly = 0; poly < 3; poly += 2) {
+          uint64_t x[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            x[r] = small_mod(poly == 0 ? (int32_t)(int8_t)(sv[r] & 0xFF) : (sv[r] >> 8), cst.q);
+          cols(x, t, cst, poly, nored);
+        }
+      }
+    };
+    small_polys(0, t_split, std::false_type{});
+    small_polys(t_split, L, std::true_type{});
   }
-  // phase 2: m + e0 (blocks [E8, 2 E8)); rows r and r + R/2 read one slot
+  // phase 2: m + e0; rows r and r + R/2 are the real and imaginary parts of one slot
   int64_t me[R];
+  {
+    uint32_t we[16];
+    chacha20_block32(key, V0 + h, nonce, we);
 #pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    uint64_t w[8];
-    chacha20_block(key, E8 + c + BLK * u, nonce, w);
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const int r = u + NB * ww;
+    for (int r = 0; r < R / 2; ++r) {
       const uint32_t jj = c + BLK * r;  // < N/2
       int64_t mre = 0, mim = 0;
       if ((jj & ((1u << gapLog) - 1)) == 0) {
@@ -1198,22 +1474,31 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
         mre = round_half_away(vr);
         mim = round_half_away(vi);
       }
-      me[r] = mre + gauss_sample_lds(w[ww], tab);
-      me[r + R / 2] = mim + gauss_sample_lds(w[ww + 4], tab);
-    }
-  }
-#pragma unroll 1
-  for (uint32_t t = 0; t < L; ++t) {
-    const TowerConst cst = tcs[t];
-    uint64_t x[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      x[r] = mod_signed_dev(me[r], cst);
-      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+      for (int part = 0; part < 2; ++part) {
+        const int rr = r + part * (R / 2);
+        const uint32_t i = IS == 1 ? (uint32_t)rr : i0 + IS * rr;
+        const uint32_t wi = IS == 1 ? we[rr] : (i0 ? we[IS * rr + 1] : we[IS * rr]);
+        me[rr] = (part ? mim : mre) +
+                 gauss32(wi, thi, tlo, [&] { return chacha20_word(key, V0 + 2 * N16 + h, nonce, i); });
+      }
     }
-    cols(x, t, cst, 1);
   }
-  (void)half;
+  const auto message_poly = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
+#pragma unroll 1
+    for (uint32_t t = ta; t < tb; ++t) {
+      const TowerConst cst = tcs[t];
+      uint64_t x[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        x[r] = mod_signed_dev(me[r], cst);
+        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+      }
+      cols(x, t, cst, 1, nored);
+    }
+  };
+  message_poly(0, t_split, std::false_type{});
+  message_poly(t_split, L, std::true_type{});
 }
 
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
@@ -1252,19 +1537,30 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const bool fused = (nlogR == 3 || nlogR == 4) && !(env && *env == '0');
   int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
   int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
+  // NORED towers (fwd_set_ct): q < kNoRedQ, run unreduced through both passes — only with the
+  // persistent blocks pass, and only as a suffix of the chain (q_0 the 60-bit tower, the rest
+  // near 2^scale_bits); t_split = L turns it off
+  const char* ppenv = getenv("SHELFI_ENC_PP");  // A/B probe switch (read per launch)
+  const bool pp = fused && nblkLog == 11 && dt.red_ok && !(ppenv && *ppenv == '0');
+  uint32_t t_split = 0;
+  while (t_split < p.L && p.q[t_split] >= kNoRedQ) ++t_split;
+  for (uint32_t t = t_split; t < p.L; ++t)
+    if (p.q[t] >= kNoRedQ) t_split = p.L;
+  const char* nrenv = getenv("SHELFI_ENC_NORED");  // A/B probe switch (read per launch)
+  if (!pp || (nrenv && *nrenv == '0')) t_split = p.L;
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
     const uint64_t nb = (K << (p.logN - nlogR)) / 256;
     if (nlogR == 3)
       hipLaunchKernelGGL((enc_cols_fused<3>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
-                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag);
+                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split);
     else
       hipLaunchKernelGGL((enc_cols_fused<4>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
-                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag);
+                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split);
     SHELFI_HIP(hipGetLastError());
   } else {
     // 2. encode (scale/round) + sampling -> compact record
-    const uint64_t threads = K * (p.N / 8);
+    const uint64_t threads = K * (p.N / 16);  // one per v2 sample group
     hipLaunchKernelGGL(enc_prep_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, fbuf,
                        K, p.logN, logS, p.delta, dt.cdt, dt.cdt_len, k8, g0, me0, ve, flag);
     SHELFI_HIP(hipGetLastError());
@@ -1295,7 +1591,21 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint64_t nbb = K * p.L << nlogR;
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
   const uint32_t xg = xcd_combos(p.L << nlogR);
-  if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
+  if (pp) {  // one launch per tower class, each spread over all CUs
+    if (t_split > 0) {
+      const uint32_t ncombo = t_split << nlogR;
+      const uint32_t pc = pp_per_combo(ncombo, K, 3);
+      hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
+                         p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
+    }
+    if (t_split < p.L) {
+      const uint32_t ncombo = (p.L - t_split) << nlogR;
+      const uint32_t pc = pp_per_combo(ncombo, K, 3);
+      hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
+                         p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
+                         p.L - t_split);
+    }
+  } else if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
@@ -1321,6 +1631,12 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
 // (y_t = a + b 2^30; every column is a sum of <= 2L products below 2^60 plus k times a
 // 30-bit limb, below 2^64 without carries: one v_mad_u64_u32 per product), then one carry
 // pass; X is exact either way, so the two paths give the same bits.
+//
+// k (round 3): sum_t y_t / q_t = k + X / Q exactly, and X / Q is within 2^-17 of 0 for every X
+// this decode can represent (|X| < 2^127 << Q / 2, the 128-bit read below), so k needs no
+// double precision: binary32 terms (y_t >> s_t) * (2^s_t / q_t) with y_t >> s_t < 2^32
+// (TowerConst::crt_sh), each within 2^-31 + 2^-23 of y_t / q_t, round half up.  The oracle's CRT is exact (multi-word centring); the two agree wherever the
+// decode is defined.  For L <= 7, k <= L fits a 32-bit limb multiplier.
 template <class YF>
 __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst* __restrict__ tcs,
                                             uint64_t Qlo, uint64_t Qhi, double inv_scale) {
@@ -1329,11 +1645,13 @@ __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst*
   if (L <= 7) {
     constexpr uint32_t M30 = (1u << 30) - 1;
     uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+    float f = 0.f;
 #pragma unroll 1
     for (uint32_t t = 0; t < L; ++t) {
       const TowerConst& c = tcs[t];
       const uint64_t y = yf(t);
-      frac += (double)y * c.inv_q;
+      const uint32_t ytop = __builtin_amdgcn_alignbit((uint32_t)(y >> 32), (uint32_t)y, c.crt_sh);
+      f = __fadd_rn(f, __fmul_rn((float)ytop, c.inv_q32));
       const uint32_t a = (uint32_t)y & M30, b = (uint32_t)(y >> 30);
       s0 += (uint64_t)a * c.crt30[0];
       s1 += (uint64_t)a * c.crt30[1] + (uint64_t)b * c.crt30[0];
@@ -1341,13 +1659,13 @@ __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst*
       s3 += (uint64_t)a * c.crt30[3] + (uint64_t)b * c.crt30[2];
       s4 += (uint64_t)a * c.crt30[4] + (uint64_t)b * c.crt30[3];
     }
-    const uint64_t kk = (uint64_t)(frac + 0.5);  // <= L
+    const uint32_t kk = (uint32_t)__fadd_rn(f, 0.5f);  // <= L
     const uint32_t* nq = tcs[0].nq30;
-    s0 += kk * nq[0];
-    s1 += kk * nq[1] + (s0 >> 30);
-    s2 += kk * nq[2] + (s1 >> 30);
-    s3 += kk * nq[3] + (s2 >> 30);
-    s4 += kk * nq[4] + (s3 >> 30);
+    s0 += (uint64_t)kk * nq[0];
+    s1 += (uint64_t)kk * nq[1] + (s0 >> 30);
+    s2 += (uint64_t)kk * nq[2] + (s1 >> 30);
+    s3 += (uint64_t)kk * nq[3] + (s2 >> 30);
+    s4 += (uint64_t)kk * nq[4] + (s3 >> 30);
     xlo = (s0 & M30) | ((s1 & M30) << 30) | (s2 << 60);
     xhi = ((s2 & M30) >> 4) | ((s3 & M30) << 26) | (s4 << 56);
   } else {
@@ -1815,7 +2133,18 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
     const uint32_t xg = xcd_combos(p.L << (logR > 0 ? logR : 0));
-    if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
+    const char* ppenv = getenv("SHELFI_DEC_PP");  // A/B probe switch (read per launch)
+    const bool pp = logR > 0 && blkLog == 11 && dt.red_ok && !(ppenv && *ppenv == '0');
+    if (pp) {
+      const uint32_t ncombo = p.L << logR;
+      const uint32_t pc = pp_per_combo(ncombo, K, 3);
+      if (sum_in)
+        hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, true>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc);
+      else
+        hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc);
+    } else if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
                          s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
     else if (logR > 0 && blkLog == 11 && dt.red_ok)

@@ -93,7 +93,12 @@ struct TowerConst {
   uint64_t nq, n4q, n8q;      // 2^64 - q, - 4q, - 8q (borrow-free conditional subtractions)
   // any u64 x -> [0, 2q): k = (x_hi * red_r) >> (32 + red_sh), x - k q (red_any; needs
   // q >= 2^40, red_ok): red_r = floor(2^(32 + E) / q) < 2^32, E = bitlength(q) - 1
-  uint32_t red_r, red_sh, red_ok, pad32;
+  uint32_t red_r, red_sh, red_ok;
+  // the CRT's k in binary32 (crt_value): y_t >> crt_sh < 2^32 (crt_sh = max(0, E - 31)) times
+  // inv_q32 = 2^crt_sh / q
+  uint32_t crt_sh;
+  float inv_q32;
+  uint32_t pad32;
   uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
   // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^128 and (2^128 - Q) mod 2^128
   // (the same in every tower), limbs 0..3 of 30 bits and limb 4 of 8 bits

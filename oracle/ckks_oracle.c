@@ -849,13 +849,21 @@ static inline int64_t gauss_from_word(uint64_t r, const uint64_t* cdt, int T) {
 }
 static inline int64_t ternary_from_word(uint64_t r) { return (int64_t)(r % 3) - 1; }
 
-/* Encrypt randomness for global ciphertext index g: nonce = (1<<56)|g; the v, e0,
- * e1 polynomials use stream words [0,N), [N,2N), [2N,3N).  Coefficient j of a
- * polynomial takes word widx(j) = (j mod N/8) * 8 + j div (N/8) of its range, i.e.
- * ChaCha block b feeds coefficients b, b + N/8, ..., b + 7N/8. */
-static inline uint32_t enc_word_index(uint32_t j, uint32_t N) {
-  const uint32_t e = N / 8;
-  return (j % e) * 8 + j / e;
+/* Encrypt randomness for global ciphertext index g (sampler v2, round 3; the product's
+ * kernels/dev_common.h states the same).  nonce = (1<<56)|g, ChaCha20 blocks of 16 32-bit
+ * words; N16 = N/16, coefficient j = h + N16 i (h < N16, i < 16):
+ *   v : block h/4 of [0, N/64), words 4(h%4)..+3 -> U = w0 + w1 2^32 + w2 2^64 + w3 2^96;
+ *       trit_i = the i-th base-3 digit of U / 2^128 (U <- 3U mod 2^128, the carry out is
+ *       the digit); v_j = trit_i - 1.
+ *   e0: block N/64 + h, word i; e1: block N/64 + N16 + h, word i.  A word w: sign w & 1,
+ *       U63 = (w >> 1) 2^32 + lo32, |e| = #{t : U63 >= cdt[t]}, where lo32 = word i of block
+ *       N/64 + 2 N16 + h (e0) / N/64 + 3 N16 + h (e1) (the product reads it only when the
+ *       top 31 bits tie with a table entry; here it is always read: same value). */
+static inline int64_t gauss_from_split(uint32_t w, uint32_t lo, const uint64_t* cdt, int T) {
+  const uint64_t u = ((uint64_t)(w >> 1) << 32) | lo;
+  int64_t k = 0;
+  for (int t = 0; t < T; ++t) k += (u >= cdt[t]);
+  return (w & 1) ? -k : k;
 }
 void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int64_t* v,
                        int64_t* e0, int64_t* e1) {
@@ -863,15 +871,30 @@ void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int6
   or_seed_to_key(seed, key);
   uint64_t cdt[64];
   int T = or_gauss_cdt(sigma, cdt, 64);
-  uint64_t* w = malloc(sizeof(uint64_t) * 3 * N);
-  or_stream_words(key, (1ull << 56) | g, 0, 3ull * N, w);
-  for (uint32_t j = 0; j < N; ++j) {
-    const uint32_t k = enc_word_index(j, N);
-    v[j] = ternary_from_word(w[k]);
-    e0[j] = gauss_from_word(w[N + k], cdt, T);
-    e1[j] = gauss_from_word(w[2ull * N + k], cdt, T);
+  const uint64_t nonce = (1ull << 56) | g;
+  const uint32_t N16 = N / 16, V0 = N / 64;
+  for (uint32_t h = 0; h < N16; ++h) {
+    uint32_t vb[16], b0[16], b1[16], t0[16], t1[16];
+    or_chacha20_block(key, h / 4, nonce, vb);
+    or_chacha20_block(key, V0 + h, nonce, b0);
+    or_chacha20_block(key, V0 + N16 + h, nonce, b1);
+    or_chacha20_block(key, V0 + 2ull * N16 + h, nonce, t0);
+    or_chacha20_block(key, V0 + 3ull * N16 + h, nonce, t1);
+    const uint32_t* w4 = vb + 4 * (h % 4);
+    u128 U = (u128)w4[0] | ((u128)w4[1] << 32) | ((u128)w4[2] << 64) | ((u128)w4[3] << 96);
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint32_t j = h + N16 * i;
+      /* 3U = 2U + U; the digit is the carry out of bit 128 */
+      const u128 U2 = U << 1;
+      uint32_t carry = (uint32_t)(U >> 127);
+      const u128 U3 = U2 + U;
+      carry += (U3 < U2);
+      U = U3;
+      v[j] = (int64_t)carry - 1;
+      e0[j] = gauss_from_split(b0[i], t0[i], cdt, T);
+      e1[j] = gauss_from_split(b1[i], t1[i], cdt, T);
+    }
   }
-  free(w);
 }
 
 /* uniform residue mod q from two words (bias < 2^-67) */

@@ -19,14 +19,15 @@ def main():
     var = os.environ["VAR"]
     batch, depth = int(os.environ.get("BATCH", "16384")), int(os.environ.get("DEPTH", "3"))
     K = int(os.environ.get("K", "238"))
-    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, seed=7)
+    flood = os.environ.get("FLOOD", "0") == "1"  # exact decode (comparable across variants) by default
+    ck = m.CKKS("ckks", batch, 52, "", multDepth=depth, seed=7, decodeNoise=flood)
     assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
     B = inf["batch"]
     g = torch.Generator(device="cuda").manual_seed(3)
     x = (torch.rand(K * B, generator=g, device="cuda", dtype=torch.float64) * 2 - 1)
     vals = os.environ.get("VALS", "0,1").split(",")
-    outs = {}
+    outs, decs = {}, {}
     times = {v: [] for v in vals}
     dtimes = {v: [] for v in vals}
     for rep in range(3):
@@ -53,10 +54,12 @@ def main():
                 ds.append(time.perf_counter() - t0)
             dtimes[v].append(sorted(ds)[2] * 1e3 / K)
             outs[v] = out.clone()
+            decs[v] = dec.clone()
     same = all(torch.equal(outs[vals[0]], outs[v]) for v in vals)
+    same_dec = flood or all(torch.equal(decs[vals[0]], decs[v]) for v in vals)
     err = float((dec - x).abs().max())
-    print("%s N=%d L=%d K=%d identical=%s max|dec-x|=%.2e" % (var, inf["ring_dim"], inf["num_towers"], K,
-                                                             same, err))
+    print("%s N=%d L=%d K=%d identical=%s decrypt_identical=%s max|dec-x|=%.2e" % (
+        var, inf["ring_dim"], inf["num_towers"], K, same, same_dec, err))
     for v in vals:
         print("  %s=%-4s encrypt ms/ct %s   decrypt ms/ct %s" % (
             var, v, " ".join("%.5f" % t for t in times[v]), " ".join("%.5f" % t for t in dtimes[v])),
