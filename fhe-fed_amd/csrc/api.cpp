@@ -1238,6 +1238,23 @@ int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
   return SHELFI_OK;
 }
 
+// Towers the decode needs: the shortest prefix of q_0 .. q_{towers-1} whose product exceeds
+// 2^130.  The decode reads the centred CRT value X mod 2^128 as a signed integer (crt_value),
+// exact for |X| < 2^127; over a prefix modulus Q' > 2^130 the centred residue of X is X itself
+// and |X| / Q' < 2^-3 keeps k's estimate clear of its rounding boundary, so the towers past the
+// prefix change no output bit.  2^15 / L4 (60 + 3 x 52 bits): 3 of 4 towers.
+// SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe switch, read per call).
+static uint32_t decode_towers(const Params& p, uint32_t towers) {
+  const char* env = getenv("SHELFI_DEC_ALL_TOWERS");
+  if (env && *env == '1') return towers;
+  uint32_t bits = 0;
+  for (uint32_t t = 0; t < towers; ++t) {
+    bits += 63 - (uint32_t)__builtin_clzll(p.q[t]);  // q_t >= 2^floor(log2 q_t)
+    if (bits > 130) return t + 1;
+  }
+  return towers;
+}
+
 int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, double* out) {
   if (!ctx || (n && !out)) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
@@ -1248,6 +1265,9 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     const CtLayout h = open_cts(ctx, blob, len);
     if (n > h.K * (uint64_t)p.batch)
       throw Error{SHELFI_ERR_ARG, "decrypt: data_dimensions exceeds the slots in the ciphertexts"};
+    Params pd = p;  // the decode's tower prefix (decode_towers); the upload carries every tower
+    pd.L = decode_towers(p, p.L);
+    const DeviceTables& dtd = pd.L == p.L ? ctx->dt : level_tables(ctx, pd.L);
     if (!n) return;
     // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
     const uint64_t K = (n + p.batch - 1) / p.batch;
@@ -1258,7 +1278,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout));
     uint8_t* cb[2] = {io, io + cin};
     uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
-    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc));
+    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(pd, kc));
     Pipe pp(ctx);
     StageRun sr(stager(ctx));
     advise_huge(out, n * 8);
@@ -1276,8 +1296,8 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       dn.g0 += (ci ? kc : 0);
-      launch_decrypt(p, ctx->dt, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
-                     scratch, pp.b, &dn);
+      launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
+                     scratch, pp.b, &dn, false, p.L);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
       sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
@@ -1583,15 +1603,15 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
     DeviceGuard g(ctx->device);
     if (towers < 1 || towers > ctx->p.L) throw Error{SHELFI_ERR_ARG, "tower count out of range for this context"};
     Params p = ctx->p;
-    p.L = towers;  // Q_l = q_0 .. q_{towers-1}; the secret key's first towers
-    const DeviceTables& dt = towers == ctx->p.L ? ctx->dt : level_tables(ctx, towers);
+    p.L = decode_towers(ctx->p, towers);  // Q' = q_0 .. q_{p.L-1}; the secret key's first towers
+    const DeviceTables& dt = p.L == ctx->p.L ? ctx->dt : level_tables(ctx, p.L);
     if (n > (uint64_t)K * p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
     hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
     const uint64_t Kn = (n + p.batch - 1) / p.batch;
     if (!Kn) return;
     const uint64_t kc_max = dev_chunk(Kn, decrypt_scratch_bytes(p, 1));
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
-    const size_t ct_words = 2ull * p.L * p.N;
+    const size_t ct_words = 2ull * towers * p.N;
     DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
     const uint64_t g0 = dn.g0;
     for (uint64_t k0 = 0; k0 < Kn; k0 += kc_max) {
@@ -1599,7 +1619,7 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
       dn.g0 = g0 + k0;
       launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
-                     sum_in);
+                     sum_in, towers);
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);

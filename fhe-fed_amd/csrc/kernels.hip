@@ -204,20 +204,23 @@ void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint3
 // flight; the arena kernel then takes 4 rows (4 C loads), the separate-buffer one 2.  Measured
 // in one process per shape (tools/wavg_rows_ab.py, profiles/probes/r03_wavg_rows_ab.txt):
 // 8 x 156 (cfg5) 0.729 -> 0.786 of 8 TB/s, 8 x 714 0.718 -> 0.778, 2 x 714 0.646 -> 0.675,
-// 4 x 714 a tie; at 12-16 learners the best row count moved with the shape (16 x 4: 1 row;
-// 12 x 476: 1; 16 x 714: 2), so one row stays there.  SHELFI_WAVG_ROWS=1|2|4 forces one
-// (A/B probe switch, read per launch).
-static int wavg_rows(uint32_t C, bool arena) {
+// 4 x 714 a tie.  At 16 learners two rows win once the launch has >= 16384 rows (16 x 714:
+// 0.705 -> 0.757 there, and through bench.py 0.810 -> 0.822, r03_wavg_rows_bench.txt; 16 x 32
+// at 2^16 / L6: 0.717 -> 0.750) and lose on the small cfg2 launch (16 x 4: 0.767 -> 0.715);
+// 12 x 476 kept one row best (0.778 vs 0.759).  SHELFI_WAVG_ROWS=1|2|4 forces one (A/B probe
+// switch, read per launch).
+static int wavg_rows(uint32_t C, bool arena, uint64_t rows) {
   const char* env = getenv("SHELFI_WAVG_ROWS");
   if (env && (*env == '1' || *env == '2' || (*env == '4' && arena))) return *env - '0';
-  return C <= 8 ? (arena ? 4 : 2) : 1;
+  if (C <= 8) return arena ? 4 : 2;
+  return C >= 16 && rows >= 16384 ? 2 : 1;
 }
 
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t total = a.rows << a.logN;
   const uint64_t rows = total / kWavgPerBlock;  // always even: N / 512 >= 2 rows per tower
   if (!rows) return;
-  int R = wavg_rows(a.C, a.arena != nullptr);
+  int R = wavg_rows(a.C, a.arena != nullptr, rows);
   while (R > 1 && ((1ull << a.logN) / kWavgPerBlock) % R) R >>= 1;  // a block stays in one tower
   const uint64_t blocks = rows / R;
   if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
@@ -684,7 +687,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
                                                              const uint64_t* __restrict__ ct,
                                                              const uint64_t* __restrict__ sk,
                                                              const uint64_t* __restrict__ sksh,
-                                                             uint32_t xg) {
+                                                             uint32_t xg, uint32_t ctL) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
   const uint32_t sstart = logN - BL;
@@ -697,8 +700,9 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
   const ulonglong2* __restrict__ tb = twb + ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t off = ((uint64_t)t << logN) + ((uint64_t)b << BL);
   const uint64_t LN = (uint64_t)L << logN;
-  const uint64_t* __restrict__ c0 = ct + (uint64_t)k * 2 * LN + off;
-  const uint64_t* __restrict__ c1 = c0 + LN;
+  const uint64_t CLN = (uint64_t)ctL << logN;  // the ciphertexts' towers (>= L, decode_towers)
+  const uint64_t* __restrict__ c0 = ct + (uint64_t)k * 2 * CLN + off;
+  const uint64_t* __restrict__ c1 = c0 + CLN;
   const uint64_t* __restrict__ s = sk + off;
   const uint64_t* __restrict__ ss = sksh + off;
   const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
@@ -749,7 +753,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
                                                              const uint64_t* __restrict__ ct,
                                                              const uint64_t* __restrict__ sk,
                                                              const uint64_t* __restrict__ sksh, uint32_t K,
-                                                             uint32_t per_combo) {
+                                                             uint32_t per_combo, uint32_t ctL) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256;
   __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
@@ -777,15 +781,16 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
       sw[r][m] = sksh[off + j];
     }
   uint32_t k = blockIdx.x / ncombo;
+  const uint64_t CLN = (uint64_t)ctL << logN;  // the ciphertexts' towers (>= L, decode_towers)
   const auto fetch = [&](uint32_t kk) {
-    const uint64_t* __restrict__ c0 = ct + (uint64_t)kk * 2 * LN + off;
+    const uint64_t* __restrict__ c0 = ct + (uint64_t)kk * 2 * CLN + off;
 #pragma unroll
     for (int r = 0; r < NS1; ++r)
 #pragma unroll
       for (int m = 0; m < M1; ++m) {
         const uint32_t j = ((threadIdx.x + 256u * r) << K1) + m;
         p0[r][m] = __builtin_nontemporal_load(c0 + j);
-        p1[r][m] = __builtin_nontemporal_load(c0 + LN + j);
+        p1[r][m] = __builtin_nontemporal_load(c0 + CLN + j);
       }
   };
   if (k < K) fetch(k);
@@ -872,7 +877,8 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
                                                       int scale_ninv,
                                                       const uint64_t* __restrict__ ct,
                                                       const uint64_t* __restrict__ sk,
-                                                      const uint64_t* __restrict__ sksh, int sum_in) {
+                                                      const uint64_t* __restrict__ sksh, int sum_in,
+                                                      uint32_t ctL) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
   const uint32_t N = 1u << logN, blk = 1u << blkLog;
   const uint32_t sh = logN - blkLog, nb = 1u << sh;
@@ -884,8 +890,8 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks(uint64_t* __restrict__ pol
   uint64_t* __restrict__ a = polys + poly * N + ((uint64_t)b << blkLog);
   if (ct) {
     const uint64_t kk = poly / L, off = ((uint64_t)t << logN) + ((uint64_t)b << blkLog);
-    const ulonglong2* c0 = reinterpret_cast<const ulonglong2*>(ct + (kk * 2 * L << logN) + off);
-    const ulonglong2* c1 = reinterpret_cast<const ulonglong2*>(ct + ((kk * 2 + 1) * L << logN) + off);
+    const ulonglong2* c0 = reinterpret_cast<const ulonglong2*>(ct + (kk * 2 * ctL << logN) + off);
+    const ulonglong2* c1 = reinterpret_cast<const ulonglong2*>(ct + ((kk * 2 + 1) * ctL << logN) + off);
     const ulonglong2* s = reinterpret_cast<const ulonglong2*>(sk + off);
     const ulonglong2* ss = reinterpret_cast<const ulonglong2*>(sksh + off);
     for (uint32_t p = threadIdx.x; p < blk / 2; p += 256) {
@@ -1062,7 +1068,7 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), lds, s, polys, L,
                          logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, logR == 0 ? 1 : 0,
-                         (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr, 0);
+                         (const uint64_t*)nullptr, (const uint64_t*)nullptr, (const uint64_t*)nullptr, 0, L);
     if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, polys, L, logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
@@ -2117,8 +2123,10 @@ size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
 
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in) {
+                    void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in, uint32_t ct_L) {
   if (!K) return;
+  if (!ct_L) ct_L = p.L;
+  if (ct_L < p.L) throw Error{SHELFI_ERR_ARG, "decrypt: fewer ciphertext towers than decoded towers"};
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
@@ -2140,26 +2148,26 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
       if (sum_in)
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, true>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc);
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc);
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
     } else if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 11 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
-                         logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh, sum_in ? 1 : 0);
+                         logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh, sum_in ? 1 : 0, ct_L);
     if (logR > 0 && fuse) {
       const uint64_t nbf = K * ((p.N >> logR) / 64);
       NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, logS,

@@ -253,7 +253,8 @@ struct DecodeNoise {
 };
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr, bool sum_in = false);
+                    void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr, bool sum_in = false,
+                    uint32_t ct_L = 0);  // ct_L: towers of the ciphertexts (0 = p.L; >= p.L)
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
 void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
                    uint64_t* pk, void* scratch, hipStream_t s);

@@ -14,7 +14,7 @@ import statistics
 
 ENCRYPT = ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
            "ntt_fwd_blocks_enc")
-DECRYPT = ("ntt_inv_blocks_dec_ct", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
+DECRYPT = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
            "fft_fwd_blocks<false>", "fft_fwd_cols")
 
 
