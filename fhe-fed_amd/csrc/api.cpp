@@ -219,6 +219,7 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
       c.red_sh = E >= 32 ? E - 32 : 0;
       c.red_r = c.red_ok ? (uint32_t)(((u128)1 << (32 + E)) / q) : 0;
       c.crt_sh = E >= 31 ? E - 31 : 0;
+      c.bq62 = ((1ull << 62) / q) * q;
       c.inv_q32 = (float)((double)(1ull << c.crt_sh) / (double)q);
     }
     // twiddles: psi^bitrev(i), psi^-bitrev(i)
@@ -770,15 +771,23 @@ struct CtLayout {
   uint64_t level = 0;
   double scale = 0.0;
   std::vector<size_t> off;  // PALISADE tower offsets [K][2][L]
-  void pieces(uint64_t k0, uint64_t kn, const Params& p, std::vector<HostPiece>& out) const {
+  // ciphertexts [k0, k0 + kn) as host pieces in [K][2][L][N] order; with Lu < L only each
+  // polynomial's first Lu towers (the decode's prefix, decode_towers): [kn][2][Lu][N]
+  void pieces(uint64_t k0, uint64_t kn, const Params& p, std::vector<HostPiece>& out, uint32_t Lu = 0) const {
     out.clear();
-    const size_t ct_bytes = 2ull * p.L * p.N * 8;
+    if (!Lu) Lu = p.L;
+    const size_t poly_bytes = (size_t)p.L * p.N * 8, ct_bytes = 2 * poly_bytes;
     if (!pal) {
-      out.push_back(HostPiece{base + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes});
+      if (Lu == p.L) {
+        out.push_back(HostPiece{base + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes});
+        return;
+      }
+      for (uint64_t i = 2 * k0; i < 2 * (k0 + kn); ++i)
+        out.push_back(HostPiece{base + sizeof(BlobHeader) + i * poly_bytes, (size_t)Lu * p.N * 8});
       return;
     }
-    for (uint64_t i = k0 * 2 * p.L; i < (k0 + kn) * 2 * p.L; ++i)
-      out.push_back(HostPiece{base + off[i], (size_t)p.N * 8});
+    for (uint64_t i = 2 * k0; i < 2 * (k0 + kn); ++i)
+      for (uint32_t t = 0; t < Lu; ++t) out.push_back(HostPiece{base + off[i * p.L + t], (size_t)p.N * 8});
   }
 };
 
@@ -1265,13 +1274,13 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     const CtLayout h = open_cts(ctx, blob, len);
     if (n > h.K * (uint64_t)p.batch)
       throw Error{SHELFI_ERR_ARG, "decrypt: data_dimensions exceeds the slots in the ciphertexts"};
-    Params pd = p;  // the decode's tower prefix (decode_towers); the upload carries every tower
+    Params pd = p;  // the decode's tower prefix (decode_towers): only those towers are uploaded
     pd.L = decode_towers(p, p.L);
     const DeviceTables& dtd = pd.L == p.L ? ctx->dt : level_tables(ctx, pd.L);
     if (!n) return;
     // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
     const uint64_t K = (n + p.batch - 1) / p.batch;
-    const size_t ct_bytes = 2ull * p.L * p.N * 8;
+    const size_t ct_bytes = 2ull * pd.L * p.N * 8;  // only the decode's towers travel
     uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
     kc = std::min<uint64_t>(kc, K);
     const size_t cin = kc * ct_bytes, dout = kc * p.batch * 8;
@@ -1290,14 +1299,14 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
-      h.pieces(k0, kn, p, pcs);
+      h.pieces(k0, kn, p, pcs, pd.L);
       sr.s.h2dv(cb[b], pcs.data(), pcs.size(), pp.a);
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       dn.g0 += (ci ? kc : 0);
       launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
-                     scratch, pp.b, &dn, false, p.L);
+                     scratch, pp.b, &dn);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
       sr.s.d2h(out + o0, ob[b], on * 8, pp.c);

@@ -256,6 +256,56 @@ __device__ __forceinline__ void chacha20_block32(const Key8& key, uint64_t count
   }
 }
 
+// One block computed by the 4 lanes of a quad: lane j = lane mod 4 runs column j's quarter
+// rounds, and the diagonal rounds rotate rows 1..3 across the quad (DPP quad_perm), as SIMD
+// ChaCha implementations rotate vector lanes; a quad transpose at the end hands lane j words
+// 4j .. 4j + 3 of the block (the same words chacha20_block32 gives).  A quarter of the
+// instructions of chacha20_block32 per lane.  Every lane of the quad must be active and pass
+// the same counter and nonce.
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void chacha20_quad(const Key8& key, uint64_t counter, uint64_t nonce,
+                                              uint32_t out[4]) {
+  constexpr int ROT1 = 0x39, ROT2 = 0x4E, ROT3 = 0x93, XOR1 = 0xB1;  // lane j <- lane (j + r) mod 4
+  const uint32_t j = threadIdx.x & 3;
+  const bool j1 = j & 1, j2 = j & 2;
+  const auto pick = [&](uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+    return j2 ? (j1 ? v3 : v2) : (j1 ? v1 : v0);
+  };
+  const uint32_t sa = pick(0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u);
+  const uint32_t sb = pick(key.k[0], key.k[1], key.k[2], key.k[3]);
+  const uint32_t sc = pick(key.k[4], key.k[5], key.k[6], key.k[7]);
+  const uint32_t sd = pick((uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce, (uint32_t)(nonce >> 32));
+  uint32_t a = sa, b = sb, c = sc, d = sd;
+#pragma unroll 2
+  for (int i = 0; i < 10; ++i) {
+    CH_QR(a, b, c, d);  // column j
+    b = quad_perm<ROT1>(b);
+    c = quad_perm<ROT2>(c);
+    d = quad_perm<ROT3>(d);
+    CH_QR(a, b, c, d);  // diagonal j: x[j], x[4 + (j+1)%4], x[8 + (j+2)%4], x[12 + (j+3)%4]
+    b = quad_perm<ROT3>(b);
+    c = quad_perm<ROT2>(c);
+    d = quad_perm<ROT1>(d);
+  }
+  // lane j holds x[j], x[4 + j], x[8 + j], x[12 + j]: transpose the quad's 4 x 4 words
+  uint32_t X[4] = {a + sa, b + sb, c + sc, d + sd};
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {  // swap the off-diagonal 2 x 2 blocks (lanes j ^ 2)
+    const uint32_t r = quad_perm<ROT2>(j2 ? X[p] : X[p + 2]);
+    if (j2) X[p] = r; else X[p + 2] = r;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; p += 2) {  // transpose each 2 x 2 block (lanes j ^ 1)
+    const uint32_t r = quad_perm<XOR1>(j1 ? X[p] : X[p + 1]);
+    if (j1) X[p] = r; else X[p + 1] = r;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[i] = X[i];
+}
+
 // ---- encrypt sampler v2 (round 3; DESIGN.md §2.3, oracle or_sample_encrypt) ----
 // Stream of ciphertext g (nonce (1 << 56) | g), in ChaCha20 blocks of 16 32-bit words, with
 // N16 = N / 16 and coefficient j = h + N16 i (h < N16, i < 16):

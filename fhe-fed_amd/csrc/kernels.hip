@@ -1420,9 +1420,9 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
   {
     int32_t sv[R];
     {
-      uint32_t wv[16];
-      chacha20_block32(key, h >> 2, nonce, wv);
-      uint32_t u[4] = {wv[4 * (h & 3)], wv[4 * (h & 3) + 1], wv[4 * (h & 3) + 2], wv[4 * (h & 3) + 3]};
+      // block h/4 is shared by the quad of lanes h & ~3 .. h | 3 (h mod 4 = lane mod 4)
+      uint32_t u[4];
+      chacha20_quad(key, h >> 2, nonce, u);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int32_t d = (int32_t)trit_next(u) - 1;
@@ -1490,15 +1490,27 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
       }
     }
   }
+  // The first columns stage pairs rows r and r + R/2 and reads the upper row only through its
+  // lazy Shoup product, which takes any 64-bit multiplicand: rows >= R/2 enter as
+  // u = m + e0 + floor(2^62 / q) q (in [0, 2^63), congruent), and only rows < R/2 are reduced
+  // (red_any, q >= 2^40).  The canonical ciphertext is the same; only lazy intermediates differ.
   const auto message_poly = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
     for (uint32_t t = ta; t < tb; ++t) {
       const TowerConst cst = tcs[t];
       uint64_t x[R];
+      if (cst.red_ok) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        x[r] = mod_signed_dev(me[r], cst);
-        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+        for (int r = 0; r < R; ++r) {
+          const uint64_t u = (uint64_t)me[r] + cst.bq62;
+          x[r] = r < R / 2 ? red_any(u, cst) : u;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          x[r] = mod_signed_dev(me[r], cst);
+          if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
+        }
       }
       cols(x, t, cst, 1, nored);
     }

@@ -99,6 +99,7 @@ struct TowerConst {
   uint32_t crt_sh;
   float inv_q32;
   uint32_t pad32;
+  uint64_t bq62;  // floor(2^62 / q) q: v + bq62 in [0, 2^63) for |v| <= 2^61 + 2^7 (encrypt's m + e0)
   uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
   // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^128 and (2^128 - Q) mod 2^128
   // (the same in every tower), limbs 0..3 of 30 bits and limb 4 of 8 bits
