@@ -98,7 +98,7 @@ def parse():
     ap.add_argument("--f4-cts", type=int, default=256,
                     help="ciphertext pairs for the §8 f4 sample (EvalMult + relinearization, ModReduce; "
                          "rank 0, 2^15/L4 workloads); 0 = skip")
-    ap.add_argument("--f4-counters-json", default=os.path.join(ROOT, "profiles", "r02_f4_counters.json"),
+    ap.add_argument("--f4-counters-json", default=os.path.join(ROOT, "profiles", "r03_f4_counters.json"),
                     help="PMC VALU instructions and HBM bytes per ciphertext of one EvalMult / ModReduce "
                          "(tools/profile_f4.sh)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
@@ -750,6 +750,8 @@ def main():
                                        "achieved": round(ach, 1), "peak": round(peak, 1),
                                        "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
                                        "source": os.path.relpath(args.encdec_valu_json, ROOT)}
+                if "before_r02" in ev[name]:  # the round-2 code's count (profiles/encdec_valu_r02.json)
+                    res[name + "_valu"]["wave_instr_per_ct_r02"] = ev[name]["before_r02"]
     except (OSError, ValueError, KeyError):
         pass
     if check:

@@ -27,5 +27,5 @@ python3 tools/encdec_traffic.py "$out/efetch_counter_collection.csv" "$out/ewrit
   -o "$out/encdec_traffic.json" > /dev/null
 bash tools/pmc_sq_encdec.sh "$tag"
 cp gpurun_out/sq_$tag/summary.txt "$out/${tag}_sq_encdec.txt"
-python3 tools/encdec_valu.py gpurun_out/sq_$tag/sq_counter_collection.csv --before profiles/r02_encdec_valu.json \
+python3 tools/encdec_valu.py gpurun_out/sq_$tag/sq_counter_collection.csv --before profiles/encdec_valu_r02.json \
   -o "$out/encdec_valu.json" > /dev/null
