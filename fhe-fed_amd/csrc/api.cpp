@@ -147,6 +147,7 @@ static void free_tables(shelfi_ctx* ctx) {
   dfree_t(ctx->dt.fft_inv);
   dfree_t(ctx->dt.fft_fwd);
   dfree_t(ctx->dt.cdt);
+  dfree_t(ctx->dt.enc_tab);
 }
 
 static void free_keys(shelfi_ctx* ctx) {
@@ -291,6 +292,35 @@ static void build_tables(shelfi_ctx* ctx) {
   ctx->dt.cdt_len = gauss_cdt(p.sigma, cdt, 63);
   if (ctx->dt.cdt_len < 0) throw Error{SHELFI_ERR_ARG, "Gaussian table too large"};
   ctx->dt.cdt = upload(cdt, (size_t)ctx->dt.cdt_len);
+  // enc_cols_fused's small-polynomial tables: the columns pass's first twiddles are
+  // psi_rev[1] = psi^(N/2) (stage 0) and psi_rev[2], psi_rev[3] = psi^(N/4), psi^(3N/4) (stage 1)
+  {
+    std::vector<uint64_t> et((size_t)p.L * kEncTab);
+    for (uint32_t t = 0; t < p.L; ++t) {
+      const uint64_t q = p.q[t];
+      const uint64_t W0 = powmod(p.psi[t], p.N / 2, q), W1 = powmod(p.psi[t], p.N / 4, q),
+                     W2 = powmod(p.psi[t], 3ull * p.N / 4, q);
+      const auto mul = [q](uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % q); };
+      const auto sm = [q](int v) { return v < 0 ? q - (uint64_t)(-v) : (uint64_t)v; };  // |v| < q
+      const auto add = [q](uint64_t a, uint64_t b) { return (uint64_t)(((u128)a + b) % q); };
+      const auto sub = [q](uint64_t a, uint64_t b) { return a >= b ? a - b : a + q - b; };
+      uint64_t* T = et.data() + (size_t)t * kEncTab;
+      for (int idx = 0; idx < 81; ++idx) {
+        const uint64_t a = sm(idx % 3 - 1), b = sm(idx / 3 % 3 - 1), c = sm(idx / 9 % 3 - 1), d = sm(idx / 27 - 1);
+        const uint64_t u = add(a, mul(W0, c)), v = add(b, mul(W0, d));  // stage 0 (pairs a-c, b-d)
+        const uint64_t u2 = sub(a, mul(W0, c)), v2 = sub(b, mul(W0, d));
+        T[0 * 81 + idx] = add(u, mul(W1, v));  // stage 1 (pairs a'-b' with W1, c'-d' with W2)
+        T[1 * 81 + idx] = sub(u, mul(W1, v));
+        T[2 * 81 + idx] = add(u2, mul(W2, v2));
+        T[3 * 81 + idx] = sub(u2, mul(W2, v2));
+      }
+      for (int e = -64; e < 64; ++e) {
+        const uint64_t m = mul(W0, sm(e < 0 ? -e : e));
+        T[kEncVTab + 64 + e] = e < 0 ? (m ? q - m : 0) : m;
+      }
+    }
+    ctx->dt.enc_tab = upload(et.data(), et.size());
+  }
   ctx->params_id = compute_params_id(p);
 }
 
@@ -1251,7 +1281,7 @@ int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
 // 2^130.  The decode reads the centred CRT value X mod 2^128 as a signed integer (crt_value),
 // exact for |X| < 2^127; over a prefix modulus Q' > 2^130 the centred residue of X is X itself
 // and |X| / Q' < 2^-3 keeps k's estimate clear of its rounding boundary, so the towers past the
-// prefix change no output bit (DESIGN.md §2.5).  2^15 / L4 (60 + 3 x 52 bits): 3 of 4 towers.
+// prefix change no output bit (DESIGN.md §2.7).  2^15 / L4 (60 + 3 x 52 bits): 3 of 4 towers.
 // SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe switch, read per call).
 static uint32_t decode_towers(const Params& p, uint32_t towers) {
   const char* env = getenv("SHELFI_DEC_ALL_TOWERS");

@@ -1361,7 +1361,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 // indices i = i0 + (16/R) r of group h = c mod N/16 (i0 = c div N/16; LOGR = 4: the whole group).
 // Same samples and rounding as enc_prep_kernel, then for every tower the columns stages of v,
 // m + e0 and e1 and the lazy stores into pbuf that the blocks pass reads.
-template <int LOGR>
+template <int LOGR, bool TAB>
 __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
                                                       double delta, const uint64_t* __restrict__ cdt,
@@ -1370,10 +1370,12 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
                                                       const uint64_t* __restrict__ tw,
                                                       const uint64_t* __restrict__ twp,
                                                       uint64_t* __restrict__ out,
-                                                      uint32_t* __restrict__ flag, uint32_t t_split) {
-  constexpr int R = 1 << LOGR, IS = 16 / R;
+                                                      uint32_t* __restrict__ flag, uint32_t t_split,
+                                                      const uint64_t* __restrict__ enc_tab) {
+  constexpr int R = 1 << LOGR, IS = 16 / R, G = R / 4;
   static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
   __shared__ uint32_t thi[64], tlo[64];
+  __shared__ uint64_t tabs[kEncTab];  // this tower's DeviceTables::enc_tab slice
   load_cdt32(cdt, T, thi, tlo);
   __syncthreads();
   const uint32_t N = 1u << logN, BLK = N >> LOGR, N16 = N >> 4, V0 = N >> 6;
@@ -1390,13 +1392,15 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
   // columns stages of one polynomial of tower t (values x[r] < q) and its lazy store
   // (towers with q < kNoRedQ run unreduced (NORED, fwd_set_ct): no stage reductions, no
   // store reduction; the blocks pass knows)
-  auto cols = [&](uint64_t (&x)[R], uint32_t t, const TowerConst& cst, int poly, auto nored) __attribute__((always_inline)) {
+  // (first: the stage the values enter at; the small polynomials skip stages their tables did)
+  auto cols = [&](uint64_t (&x)[R], uint32_t t, const TowerConst& cst, int poly, auto nored, auto first)
+                  __attribute__((always_inline)) {
     constexpr bool NR = decltype(nored)::value;
     const uint64_t q = cst.q;
     const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
     const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
 #pragma unroll
-    for (int s = 0; s < LOGR; ++s) {
+    for (int s = decltype(first)::value; s < LOGR; ++s) {
       const int m = 1 << s, tr = R >> (s + 1);
 #pragma unroll
       for (int i = 0; i < m; ++i) {
@@ -1445,18 +1449,53 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
         sv[r] |= (int32_t)gauss32(wi, thi, tlo, [&] { return chacha20_word(key, V0 + 3 * N16 + h, nonce, i); }) << 8;
       }
     }
+    // v's first two column stages are table lookups: rows g, g + R/4, g + R/2, g + 3R/4 (g < R/4)
+    // form a radix-4 group whose 4 outputs depend only on its 4 ternary inputs (81 patterns,
+    // DeviceTables::enc_tab, canonical); e1's stage 0 reads W0 e from the table (|e| <= 63).
+    // The canonical ciphertext is the same; only lazy intermediates differ (smaller bounds).
+    uint32_t vidx[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const auto tr = [&](int r) { return (uint32_t)((int32_t)(int8_t)(sv[r] & 0xFF) + 1); };
+      vidx[g] = tr(g) + 3 * tr(g + G) + 9 * tr(g + 2 * G) + 27 * tr(g + 3 * G);
+    }
     // towers [0, t_split) reduced, [t_split, L) unreduced (q < kNoRedQ; the blocks pass knows)
     const auto small_polys = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
       for (uint32_t t = ta; t < tb; ++t) {
         const TowerConst cst = tcs[t];
+        if constexpr (!TAB) {  // A/B reference: every stage as butterflies (SHELFI_ENC_TAB=0)
 #pragma unroll 1
-        for (int poly = 0; poly < 3; poly += 2) {
+          for (int poly = 0; poly < 3; poly += 2) {
+            uint64_t x[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+              x[r] = small_mod(poly == 0 ? (int32_t)(int8_t)(sv[r] & 0xFF) : (sv[r] >> 8), cst.q);
+            cols(x, t, cst, poly, nored, std::integral_constant<int, 0>{});
+          }
+          continue;
+        }
+        __syncthreads();  // the previous tower's lookups are done (every thread runs every tower)
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kEncTab; i += 256) tabs[i] = enc_tab[(size_t)t * kEncTab + i];
+        __syncthreads();
+        {
           uint64_t x[R];
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-            x[r] = small_mod(poly == 0 ? (int32_t)(int8_t)(sv[r] & 0xFF) : (sv[r] >> 8), cst.q);
-          cols(x, t, cst, poly, nored);
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) x[g + kk * G] = tabs[kk * 81 + vidx[g]];
+          cols(x, t, cst, 0, nored, std::integral_constant<int, 2>{});
+        }
+        {
+          uint64_t x[R];
+#pragma unroll
+          for (int r = 0; r < R / 2; ++r) {
+            const uint64_t xa = small_mod(sv[r] >> 8, cst.q);
+            const uint64_t tt = tabs[kEncVTab + 64 + (sv[r + R / 2] >> 8)];  // W0 e mod q
+            x[r] = xa + tt;                   // < 2q
+            x[r + R / 2] = xa + cst.q - tt;   // (0, 2q)
+          }
+          cols(x, t, cst, 2, nored, std::integral_constant<int, 1>{});
         }
       }
     };
@@ -1512,7 +1551,7 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
           if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound reductions in flight
         }
       }
-      cols(x, t, cst, 1, nored);
+      cols(x, t, cst, 1, nored, std::integral_constant<int, 0>{});
     }
   };
   message_poly(0, t_split, std::false_type{});
@@ -1552,7 +1591,7 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint32_t nblkLog = ntt_block_log(p.logN);
   const int nlogR = (int)(p.logN - nblkLog);
   const char* env = getenv("SHELFI_ENC_FUSED_COLS");  // A/B probe switch (read per launch)
-  const bool fused = (nlogR == 3 || nlogR == 4) && !(env && *env == '0');
+  const bool fused = (nlogR == 3 || nlogR == 4) && dt.enc_tab && !(env && *env == '0');
   int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
   int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
   // NORED towers (fwd_set_ct): q < kNoRedQ, run unreduced through both passes — only with the
@@ -1569,12 +1608,21 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
     const uint64_t nb = (K << (p.logN - nlogR)) / 256;
-    if (nlogR == 3)
-      hipLaunchKernelGGL((enc_cols_fused<3>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
-                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split);
+    const char* tabenv = getenv("SHELFI_ENC_TAB");  // A/B probe switch (read per launch)
+    const bool tab = !(tabenv && *tabenv == '0');
+#define ENC_COLS(LR, TB)                                                                                        \
+  hipLaunchKernelGGL((enc_cols_fused<LR, TB>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L, \
+                     p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split,  \
+                     dt.enc_tab)
+    if (nlogR == 3 && tab)
+      ENC_COLS(3, true);
+    else if (nlogR == 3)
+      ENC_COLS(3, false);
+    else if (tab)
+      ENC_COLS(4, true);
     else
-      hipLaunchKernelGGL((enc_cols_fused<4>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L,
-                         p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split);
+      ENC_COLS(4, false);
+#undef ENC_COLS
     SHELFI_HIP(hipGetLastError());
   } else {
     // 2. encode (scale/round) + sampling -> compact record

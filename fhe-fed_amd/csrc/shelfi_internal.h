@@ -106,6 +106,8 @@ struct TowerConst {
   uint32_t crt30[5], nq30[5], pad30[2];
 };
 
+constexpr int kEncVTab = 4 * 81, kEncETab = 128, kEncTab = kEncVTab + kEncETab;
+
 struct DeviceTables {
   TowerConst* tc = nullptr;         // [L]
   uint64_t* psi_rev = nullptr;      // [L][N]  psi^bitrev(i)
@@ -121,6 +123,10 @@ struct DeviceTables {
   double2* fft_inv = nullptr;       // [B] flat special-FFT twiddles (FFTSpecialInv)
   double2* fft_fwd = nullptr;       // [B] (FFTSpecial)
   uint64_t* cdt = nullptr;          // Gaussian CDT [64]
+  // encrypt's first column stages of its small polynomials (enc_cols_fused), per tower
+  // [L][kEncTab]: the radix-4 outputs of 4 ternary inputs (stages 0-1, 4 x 81) and W0 e for e1's
+  // stage 0 (e + 64, |e| <= 63), all canonical
+  uint64_t* enc_tab = nullptr;
   int cdt_len = 0;
   uint64_t qmod128_lo = 0, qmod128_hi = 0;  // Q mod 2^128
 };
