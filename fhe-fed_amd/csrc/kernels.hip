@@ -1171,6 +1171,84 @@ __global__ __launch_bounds__(256) void fft_inv_blocks(const double* __restrict__
   for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
 }
 
+// Compile-time forms of the FFT block passes (round 3): the same butterflies, in the same order
+// per element, as fft_fwd_blocks / fft_inv_blocks, but run as register chunks of 2^KC
+// elements (a set j0 + m 2^A, m < 2^KC, covers the stages of half-size 2^A .. 2^(A+KC-1)) with
+// the LDS block exchanged only between chunks: 3 barriers instead of 10-11, the first chunk
+// loaded and the last chunk stored straight from registers.  Bit-identical outputs.
+template <int KC, int A>
+__device__ __forceinline__ void fft_dit_set(double2 (&v)[1 << KC], uint32_t l, const double2* __restrict__ tw) {
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {  // half-size 2^(A+i), ascending (DIT)
+#pragma unroll
+    for (int m0 = 0; m0 < (1 << KC); ++m0) {
+      if (m0 & (1 << i)) continue;
+      const int m1 = m0 + (1 << i);
+      const double2 W = tw[(1u << (A + i)) + l + ((uint32_t)(m0 & ((1 << i) - 1)) << A)];
+      const double2 u = v[m0];
+      const double2 w = cmul(v[m1], W);
+      v[m0] = cadd(u, w);
+      v[m1] = csub(u, w);
+    }
+  }
+}
+template <int KC, int A>
+__device__ __forceinline__ void fft_dif_set(double2 (&v)[1 << KC], uint32_t l, const double2* __restrict__ tw) {
+#pragma unroll
+  for (int i = KC - 1; i >= 0; --i) {  // half-size 2^(A+i), descending (DIF)
+#pragma unroll
+    for (int m0 = 0; m0 < (1 << KC); ++m0) {
+      if (m0 & (1 << i)) continue;
+      const int m1 = m0 + (1 << i);
+      const double2 W = tw[(1u << (A + i)) + l + ((uint32_t)(m0 & ((1 << i) - 1)) << A)];
+      const double2 a0 = v[m0], a1 = v[m1];
+      v[m0] = cadd(a0, a1);
+      v[m1] = cmul(csub(a0, a1), W);
+    }
+  }
+}
+// One chunk over all 2^(BL-KC) sets of a block, 2^(BL-3) threads: ld(j) / st(j, v) take block
+// offsets.
+template <int BL, int KC, int A, bool DIT, class Load, class Store>
+__device__ __forceinline__ void fft_chunk(const double2* __restrict__ tw, Load ld, Store st) {
+  constexpr int T = 1 << (BL - 3), NS = (1 << (BL - KC)) / T;
+  static_assert(NS >= 1, "chunk plan");
+#pragma unroll
+  for (int r = 0; r < NS; ++r) {
+    const uint32_t s = threadIdx.x + (uint32_t)T * r;
+    const uint32_t l = s & ((1u << A) - 1), j0 = ((s >> A) << (A + KC)) | l;
+    double2 v[1 << KC];
+#pragma unroll
+    for (int m = 0; m < (1 << KC); ++m) v[m] = ld(j0 + ((uint32_t)m << A));
+    if (DIT)
+      fft_dit_set<KC, A>(v, l, tw);
+    else
+      fft_dif_set<KC, A>(v, l, tw);
+#pragma unroll
+    for (int m = 0; m < (1 << KC); ++m) st(j0 + ((uint32_t)m << A), v[m]);
+  }
+}
+// FFTSpecialInv's second pass (encode, after fft_inv_cols): DIF half-sizes 2^(BL-1) .. 1.
+template <int BL, int K1, int K2, int K3, int K4>
+__global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __restrict__ buf, uint32_t logS,
+                                                                  const double2* __restrict__ tw) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan");
+  __shared__ __attribute__((aligned(16))) double2 sm[1 << BL];
+  const uint32_t S = 1u << logS, sh = logS - BL;
+  const uint64_t k = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  double2* __restrict__ g = buf + k * S + ((uint64_t)b << BL);
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  const auto lds_st = [&](uint32_t j, double2 v) { sm[j] = v; };
+  fft_chunk<BL, K1, BL - K1, false>(tw, [&](uint32_t j) { return g[j]; }, lds_st);
+  __syncthreads();
+  fft_chunk<BL, K2, BL - K1 - K2, false>(tw, lds_ld, lds_st);
+  __syncthreads();
+  fft_chunk<BL, K3, BL - K1 - K2 - K3, false>(tw, lds_ld, lds_st);
+  __syncthreads();
+  fft_chunk<BL, K4, 0, false>(tw, lds_ld, [&](uint32_t j, double2 v) { g[j] = v; });
+}
+
 // FFTSpecial (decode): input already bit-reversed by crt_decode's scatter; DIT
 // stages len = 2..S with twiddle ffwd[len/2 + (x mod len)].  Small len in LDS
 // blocks, the top LOGR stages on register columns; the last pass writes the real
@@ -1579,8 +1657,17 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t nb = K * ((p.batch >> logR) / 256);
     FFT_DISPATCH(logR, fft_inv_cols, dim3((uint32_t)nb), dim3(256), 0, s, x, n, fbuf, logS,
                  dt.fft_inv);
-    hipLaunchKernelGGL(fft_inv_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, x, n, fbuf,
-                       logS, blkLog, 0, dt.fft_inv);
+    const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switch (read per launch)
+    const bool fct = !(fenv && *fenv == '0');
+    if (fct && blkLog == 10)
+      hipLaunchKernelGGL((fft_inv_blocks_ct<10, 3, 3, 2, 2>), dim3((uint32_t)(K << logR)), dim3(128), 0, s, fbuf,
+                         logS, dt.fft_inv);
+    else if (fct && blkLog == 11)
+      hipLaunchKernelGGL((fft_inv_blocks_ct<11, 3, 3, 3, 2>), dim3((uint32_t)(K << logR)), dim3(256), 0, s, fbuf,
+                         logS, dt.fft_inv);
+    else
+      hipLaunchKernelGGL(fft_inv_blocks, dim3((uint32_t)(K << logR)), dim3(256), lds, s, x, n, fbuf,
+                         logS, blkLog, 0, dt.fft_inv);
   } else {
     hipLaunchKernelGGL(fft_inv_blocks, dim3((uint32_t)K), dim3(256), lds, s, x, n, fbuf, logS,
                        blkLog, 1, dt.fft_inv);
@@ -2099,6 +2186,29 @@ struct FloodArgs {
 // stages follow on register columns (fft_fwd_cols).  A single pass writes the real parts
 // of the first `n` slots straight into the caller's output vector.  FLOOD: the decode
 // noise is added while loading (see decode_stats_kernel).
+// Ciphertext k's flooding scale from decode_stats_kernel's partial sums: the noise's standard
+// deviation in slot units (the first block of each ciphertext records the precision failure and
+// logError).
+__device__ __forceinline__ double flood_nsd(const FloodArgs& fa, uint64_t k, uint32_t b, uint32_t S) {
+  double s1 = 0.0, s2 = 0.0;
+  for (uint32_t g = 0; g < fa.G; ++g) {
+    const double2 v = fa.part[k * fa.G + g];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  const double var = (s2 - s1 * (s1 / (double)S)) / (double)(S - 1);
+  double sigma_p = 0.5 * sqrt(var > 0.0 ? var : 0.0) * fa.two_p;
+  const bool fail = !(log2(sigma_p) <= fa.p_bits - 5.0);
+  const double floor_sd = 0.125 * sqrt((double)(1u << fa.logN));
+  if (sigma_p < floor_sd) sigma_p = floor_sd;
+  const double stddev_p = sqrt(fa.m_factor + 1.0) * sigma_p;
+  if (b == 0 && threadIdx.x == 0) {
+    if (fail) atomicOr(&fa.flags[1], 1u);
+    atomicMax((int*)&fa.flags[2], (int)rint(log2(stddev_p * sqrt(2.0 * (double)S))));
+  }
+  return stddev_p / fa.two_p;
+}
+
 template <bool FLOOD>
 __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf, uint32_t logS,
                                                       uint32_t blkLog, const double2* __restrict__ tw,
@@ -2111,23 +2221,7 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
   const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint64_t off = k * S + ((uint64_t)b << blkLog);
   if (FLOOD) {
-    double s1 = 0.0, s2 = 0.0;
-    for (uint32_t g = 0; g < fa.G; ++g) {
-      const double2 v = fa.part[k * fa.G + g];
-      s1 += v.x;
-      s2 += v.y;
-    }
-    const double var = (s2 - s1 * (s1 / (double)S)) / (double)(S - 1);
-    double sigma_p = 0.5 * sqrt(var > 0.0 ? var : 0.0) * fa.two_p;
-    const bool fail = !(log2(sigma_p) <= fa.p_bits - 5.0);
-    const double floor_sd = 0.125 * sqrt((double)(1u << fa.logN));
-    if (sigma_p < floor_sd) sigma_p = floor_sd;
-    const double stddev_p = sqrt(fa.m_factor + 1.0) * sigma_p;
-    if (b == 0 && threadIdx.x == 0) {
-      if (fail) atomicOr(&fa.flags[1], 1u);
-      atomicMax((int*)&fa.flags[2], (int)rint(log2(stddev_p * sqrt(2.0 * (double)S))));
-    }
-    const double nsd = stddev_p / fa.two_p;
+    const double nsd = flood_nsd(fa, k, b, S);
     const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
     const double4* src = reinterpret_cast<const double4*>(buf + off);
     for (uint32_t m = threadIdx.x; m < blk / 8; m += 256) {  // positions 8m .. 8m + 7
@@ -2170,6 +2264,42 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
   }
 }
 
+// FFTSpecial's first pass (decode, not the final pass): block b of ciphertext k, DIT half-sizes
+// 1 .. 2^(BL-1); K1 = 3, so the first chunk's set is 8 consecutive positions = one ChaCha block
+// of the flooding stream.
+template <int BL, int K1, int K2, int K3, int K4, bool FLOOD>
+__global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __restrict__ buf, uint32_t logS,
+                                                                  const double2* __restrict__ tw, FloodArgs fa) {
+  static_assert(K1 == 3 && K1 + K2 + K3 + K4 == BL, "chunk plan");
+  __shared__ __attribute__((aligned(16))) double2 sm[1 << BL];
+  const uint32_t S = 1u << logS, sh = logS - BL;
+  const uint64_t k = blockIdx.x >> sh;
+  const uint32_t b = blockIdx.x & ((1u << sh) - 1);
+  double2* __restrict__ g = buf + k * S + ((uint64_t)b << BL);
+  const auto lds_ld = [&](uint32_t j) { return sm[j]; };
+  const auto lds_st = [&](uint32_t j, double2 v) { sm[j] = v; };
+  if (FLOOD) {
+    const double nsd = flood_nsd(fa, k, b, S);
+    const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
+    // set s = positions 8s .. 8s + 7 = ChaCha block (b 2^BL) / 8 + s; position 8s + i takes word i
+    uint64_t w[8];
+    chacha20_block(fa.key, (((uint64_t)b << BL) >> 3) + threadIdx.x, nonce, w);
+    fft_chunk<BL, K1, 0, true>(tw, [&](uint32_t j) {
+      double z0, z1;
+      flood_pair(w[j & 7], z0, z1);
+      const double2 v = g[j];
+      return make_double2(v.x + nsd * z0, v.y + nsd * z1);
+    }, lds_st);
+  } else {
+    fft_chunk<BL, K1, 0, true>(tw, [&](uint32_t j) { return g[j]; }, lds_st);
+  }
+  __syncthreads();
+  fft_chunk<BL, K2, K1, true>(tw, lds_ld, lds_st);
+  __syncthreads();
+  fft_chunk<BL, K3, K1 + K2, true>(tw, lds_ld, lds_st);
+  __syncthreads();
+  fft_chunk<BL, K4, K1 + K2 + K3, true>(tw, lds_ld, [&](uint32_t j, double2 v) { g[j] = v; });
+}
 static uint32_t flood_groups(uint32_t S) {
   const uint32_t half = S / 2;
   return half >= kFloodPairsPerWg ? half / kFloodPairsPerWg : 1;
@@ -2271,11 +2401,22 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     }
     SHELFI_HIP(hipGetLastError());
   }
-  if (fused_flood)
-    hipLaunchKernelGGL(fft_fwd_blocks<true>, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
+  const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switch (read per launch)
+  const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && !(fenv && *fenv == '0');
+  const dim3 fg((uint32_t)(K << flogR));
+  if (fct && fblkLog == 10 && fused_flood)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
+  else if (fct && fblkLog == 10)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
+  else if (fct && fused_flood)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<11, 3, 3, 3, 2, true>), fg, dim3(256), 0, s, fbuf, logS, dt.fft_fwd, fa);
+  else if (fct)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<11, 3, 3, 3, 2, false>), fg, dim3(256), 0, s, fbuf, logS, dt.fft_fwd, fa);
+  else if (fused_flood)
+    hipLaunchKernelGGL(fft_fwd_blocks<true>, fg, dim3(256), lds, s, fbuf, logS,
                        fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
   else
-    hipLaunchKernelGGL(fft_fwd_blocks<false>, dim3((uint32_t)(K << flogR)), dim3(256), lds, s, fbuf, logS,
+    hipLaunchKernelGGL(fft_fwd_blocks<false>, fg, dim3(256), lds, s, fbuf, logS,
                        fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
   SHELFI_HIP(hipGetLastError());
   if (flogR > 0) {
