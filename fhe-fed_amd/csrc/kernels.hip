@@ -1125,7 +1125,8 @@ __global__ __launch_bounds__(256) void fft_inv_cols(const double* __restrict__ x
     for (int r0 = 0; r0 < R; ++r0) {
       if ((r0 / trr) % 2) continue;
       const int r1 = r0 + trr;
-      const uint32_t j = (col + (uint32_t)r0 * BLK) & (len - 1);
+      // (col + r0 BLK) mod len, written so rows sharing a twiddle share its load
+      const uint32_t j = col + (uint32_t)(r0 & ((R >> s) - 1)) * BLK;
       const double2 W = tw[lenh + j];
       const double2 u = cadd(v[r0], v[r1]);
       const double2 d = csub(v[r0], v[r1]);
@@ -1271,13 +1272,13 @@ __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ 
   for (int r = 0; r < R; ++r) v[r] = buf[k * S + col + (uint64_t)r * BLK];
 #pragma unroll
   for (int s = 0; s < LOGR; ++s) {
-    const uint32_t lenh = BLK << s, len = lenh << 1;
+    const uint32_t lenh = BLK << s;
     const int tr = 1 << s;
 #pragma unroll
     for (int r0 = 0; r0 < R; ++r0) {
       if ((r0 >> s) & 1) continue;
       const int r1 = r0 + tr;
-      const uint32_t j = (col + (uint32_t)r0 * BLK) & (len - 1);
+      const uint32_t j = col + (uint32_t)(r0 & ((2 << s) - 1)) * BLK;  // (col + r0 BLK) mod len
       const double2 W = tw[lenh + j];
       const double2 u = v[r0];
       const double2 w = cmul(v[r1], W);
