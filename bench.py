@@ -635,6 +635,14 @@ def main():
                          "SHELFI_FHE.CKKS.computeWeightedAverage (H2D + wavg + D2H)" % (Cl, Ka),
                "ms_per_call": round(dt_api * 1e3, 2),
                "input_GB_per_s": round(Cl * Ka * 2 * L * N * 8 / dt_api / 1e9, 2)}
+        # the aggregate back through decrypt(bytes) (H2D of the decode's tower prefix + decrypt + D2H)
+        ck.decrypt(res_blob, Ka * batch)  # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ck.decrypt(res_blob, Ka * batch)
+        dt_dec = (time.perf_counter() - t0) / reps
+        api["decrypt"] = {"ms_per_call": round(dt_dec * 1e3, 2), "cts_per_s": round(Ka / dt_dec, 1),
+                          "blob_GB_per_s": round(len(res_blob) / dt_dec / 1e9, 2)}
         del blobs, res_blob
         # the same in the reference's own wire format (PALISADE cereal archives, §8 f1):
         # the learners' uploads encrypted with set_wire_format("palisade")
