@@ -81,10 +81,11 @@ def parse():
                          "the sums to the consumer, shelfi_dev_decrypt_sum folds them on load)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
-    ap.add_argument("--place-output", type=int, default=0,
+    ap.add_argument("--place-output", type=int, default=8,
                     help="arena layout, no collective: time this many candidate output buffers before "
-                         "the timed region and keep the fastest placement (default 0 = one plain "
-                         "torch.empty buffer, the headline since round 2)")
+                         "the timed region and keep the fastest placement (Arena.place_output; the "
+                         "plain torch.empty buffer's launch is reported as roofline.untuned_output); "
+                         "0 = one plain buffer")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
