@@ -1,5 +1,5 @@
 """Decrypt decodes with the shortest tower prefix whose modulus exceeds 2^130 (api.cpp
-decode_towers, DESIGN.md §2.5): for every value the 128-bit decode represents (|X| < 2^127)
+decode_towers, DESIGN.md §2.7): for every value the 128-bit decode represents (|X| < 2^127)
 the centred CRT over that prefix is X itself, so the dropped towers change no output bit.
 Checked here bit for bit against the all-tower decode (SHELFI_DEC_ALL_TOWERS=1, read per call)
 on fresh ciphertexts, a depth-2 aggregate (scale Delta^2), the bytes API, a decrypt of
