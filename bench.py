@@ -345,7 +345,11 @@ def main():
         if args.layout == "arena" and shard != "learners" and args.place_output > 0:
             # where the aggregate lands in HBM relative to the arena moves the launch time by
             # up to 12%: keep the fastest of a few candidate buffers
-            out, cand_ms = arena.place_output(weights, candidates=args.place_output)
+            # candidate 0 is a plain torch.empty buffer allocated first (on some boxes every
+            # buffer allocated next to the others ran slower than it)
+            plain0 = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
+            out, cand_ms = arena.place_output(weights, candidates=args.place_output, include=[plain0])
+            del plain0
             placement = {"candidates": len(cand_ms), "candidate_launch_ms": cand_ms,
                          "chosen": cand_ms.index(min(cand_ms))}
         else:
@@ -378,7 +382,10 @@ def main():
                 return [(k_lo, k_hi, out)]
             return comb.run(piece, lambda s_: D.modq(ck, s_))
 
+        # the launch's input bytes: the packed arena or C uint64 batches
+        in_bytes = arena.buf.numel() * 8 if args.layout == "arena" else C_loc * K_loc * 2 * L * N * 8
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
+                "in_bytes": in_bytes,
                 "enc_times": enc_times, "kernel": kernel, "kernel_into": kernel_into, "step": step, "piece": piece, "comb": comb, "weights": weights,
                 "cts": cts, "placement": placement}
 
@@ -663,20 +670,25 @@ def main():
         finally:
             ck.set_wire_format("shelfi")
 
-    # roofline of the dominant kernel: algorithmic bytes = (C + 1) * K * 2 * L * N * 8
-    bytes_per_launch = (C_loc + 1) * K_loc * 2 * L * N * 8
+    # roofline of the dominant kernel: algorithmic bytes = the C learners' packed residues
+    # (K * 2 * N * sum_t B_t / 8 each, B_t = 4 ceil(bitlength(q_t) / 4)) read once
+    # + the uint64 aggregate K * 2 * L * N * 8 written once
+    bytes_per_launch = main_mode["in_bytes"] + K_loc * 2 * L * N * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == args.workload and tj.get("learners") == C_loc and K_loc == K:
+        kname = "wavg_packed" if args.layout == "arena" else "wavg_kernel"
+        if (tj.get("workload") == args.workload and tj.get("learners") == C_loc and K_loc == K
+                and str(tj.get("kernel", "")).startswith(kname)):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "wavg_kernel", "bytes_per_launch": bytes_per_launch,
+                "kernel": "wavg_packed" if args.layout == "arena" else "wavg_kernel",
+                "bytes_per_launch": bytes_per_launch,
                 "launch_ms_avg": round(kern_avg_ms, 4), "launch_ms_min": round(kern_ms[0], 4)}
     if untuned is not None:
         roofline["untuned_output"] = {"launch_ms_avg": round(untuned, 4),

@@ -82,10 +82,12 @@ def wavg(ckks, cts: Sequence, weights: Sequence[float], out=None):
 
 
 class Arena:
-    """The aggregator's resident layout for C learners' K ciphertexts: one HBM buffer
-    [K*2*L*N/512][C][512] (learner slices side by side), filled once per round with
-    put(); wavg() then reads one contiguous C x 4 KiB region per block (6.35 vs 5.80
-    TB/s for separate per-learner buffers at C = 16)."""
+    """The aggregator's resident layout for C learners' K ciphertexts: one HBM buffer of
+    rows of 512 residues (the [K][2][L][N] order), each row holding the C learners' slices
+    side by side, every residue of tower t packed to B_t = 4 ceil(bitlength(q_t) / 4) bits
+    (60 / 52 / 52 / 52 at 2^15 / L4: 216 of 256 bits per coefficient).  put()
+    packs and validates each learner's batch once per round; wavg() then reads one
+    contiguous C-slice region per row and writes the [K][2][L][N] uint64 aggregate."""
 
     def __init__(self, ckks, num_learners: int, K: int, device=None):
         torch = _torch()
@@ -94,7 +96,9 @@ class Arena:
         self.L, self.N = inf["num_towers"], inf["ring_dim"]
         if device is None:
             device = "cuda:%d" % inf["device"]
-        words = _lib.load().shelfi_arena_words(ckks._ctx, self.C, self.K)
+        lib = _lib.load()
+        self.ct_words = lib.shelfi_arena_words(ckks._ctx, self.C, 1)  # packed words per ciphertext
+        words = lib.shelfi_arena_words(ckks._ctx, self.C, self.K)
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
 
     def put(self, learner: int, ct):
@@ -133,22 +137,26 @@ class Arena:
         _check_ct(out, self.ckks, Kr)
         w = (C.c_float * self.C)(*[float(x) for x in weights])
         # ciphertexts [k0, k1) of an arena are themselves an arena of k1-k0 ciphertexts
-        base = self.buf.data_ptr() + k0 * 2 * self.L * self.N * self.C * 8
+        base = self.buf.data_ptr() + k0 * self.ct_words * 8
         check(_lib.load().shelfi_dev_wavg_arena(self.ckks._ctx, C.c_void_p(base), w, self.C, Kr,
                                                 C.c_void_p(out.data_ptr()),
                                                 C.c_void_p(_stream_ptr(out))), "dev_wavg_arena")
         return out
 
 
-    def place_output(self, weights: Sequence[float], candidates: int = 8, launches: int = 2):
+    def place_output(self, weights: Sequence[float], candidates: int = 8, launches: int = 2, include=()):
         """A [K][2][L][N] output buffer placed well for this arena.  The launch time
         depends on where the output lands in physical HBM relative to the arena (up to
         12%, reproducible per buffer pair), so `candidates` buffers are
         allocated side by side, timed (shelfi_dev_wavg_arena_pick_output) and all but the
-        fastest released.  Returns (buffer, per-candidate ms)."""
+        fastest released; buffers in `include` (already allocated [K][2][L][N] tensors) are
+        candidates too, ahead of the new ones.  Returns (buffer, per-candidate ms)."""
         torch = _torch()
-        cands = [torch.empty((self.K, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
-                 for _ in range(max(1, int(candidates)))]
+        cands = list(include)
+        for c in cands:
+            _check_ct(c, self.ckks, self.K)
+        cands += [torch.empty((self.K, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
+                  for _ in range(max(1 if not cands else 0, int(candidates)))]
         ptrs = (C.c_void_p * len(cands))(*[t.data_ptr() for t in cands])
         w = (C.c_float * self.C)(*[float(x) for x in weights])
         best = C.c_size_t()

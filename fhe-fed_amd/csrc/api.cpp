@@ -475,7 +475,7 @@ static void fill_weights(WavgArgs& a, const Params& p, const float* w, size_t n)
   }
 }
 
-// Weight limbs [C][L][2] of wavg_arena_many in a device buffer: a ring of slots, the
+// Weight limbs [C][L][2] of wavg_packed in a device buffer: a ring of slots, the
 // last one reused while the weights repeat (every step of a round), a slot rewritten
 // only after the kernels that read it have completed.
 static int arena_weight_slot(shelfi_ctx* ctx, const float* w, size_t C, hipStream_t s) {
@@ -1407,19 +1407,35 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
 
 size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K) {
   if (!ctx) return 0;
-  return C * K * 2ull * ctx->p.L * ctx->p.N;
+  return (size_t)arena_ct_words(ctx->p, C) * K;
 }
 
-// Validation of a freshly placed arena slot: one read of the learner's slices for residues
-// >= q_t (~0.2 ms of HBM per 1.4 GiB, against ~30 ms of PCIe for the upload), then the
-// slot's refusal mark is set or cleared.  Synchronises `s`.  Called under the ctx lock.
-static void arena_validate(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t K, size_t learner, size_t C,
-                           hipStream_t s) {
+}  // extern "C"
+
+namespace shelfi {
+// Placement of a learner's batch into its packed slices (arena_pack_kernel: the canonical-residue
+// check of every residue rides along, ~0.3 ms of HBM per 1.4 GiB against ~30 ms of PCIe for the
+// upload), then the slot's refusal mark is set or cleared.  `rows_of(k0, kn, dst)` makes
+// ciphertexts [k0, k0 + kn) available as contiguous [kn][2][L][N] device residues and returns
+// them (a device batch: the caller's pointer; host data: staged through `dst`, the context's
+// scratch, `chunk` ciphertexts at a time).  Synchronises `s`.  Called under the ctx lock.
+template <class RowsOf>
+static void arena_place(shelfi_ctx* ctx, size_t K, size_t learner, size_t C, uint64_t* arena_dev, hipStream_t s,
+                        size_t chunk, bool staged, RowsOf rows_of) {
   const Params& p = ctx->p;
+  const ArenaPack ap = arena_pack(p);
   uint32_t* bad = ctx->dev_flag + 4;
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, s));
-  launch_arena_check(arena_dev, (uint32_t)C, (uint32_t)learner, (uint64_t)K * 2 * p.L, p.L, p.logN,
-                     ctx->dt.tc, bad, s);
+  const uint64_t ct_rows = 2ull * p.L * (p.N / kArenaChunk);
+  uint64_t* dst = nullptr;
+  if (staged)
+    dst = (uint64_t*)ensure(ctx->scratch, ctx->scratch_bytes, std::min(chunk, K) * 2ull * p.L * p.N * 8);
+  for (size_t k0 = 0; k0 < K; k0 += chunk) {
+    const size_t kn = std::min(chunk, K - k0);
+    const uint64_t* src = rows_of(k0, kn, dst);
+    launch_arena_pack(src, k0 * ct_rows, kn * ct_rows, (uint32_t)C, (uint32_t)learner, p.L, p.logN, ap,
+                      ctx->dt.tc, arena_dev, bad, s);
+  }
   uint32_t flag = 0;
   SHELFI_HIP(hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, s));
   SHELFI_HIP(hipStreamSynchronize(s));
@@ -1428,17 +1444,37 @@ static void arena_validate(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t K,
     if (R[i].arena == arena_dev && R[i].learner == learner) R.erase(R.begin() + (long)i);
     else ++i;
   if (flag) {
-    R.push_back({arena_dev, C * K * 2ull * p.L * p.N, learner});
+    R.push_back({arena_dev, (size_t)arena_ct_words(p, C) * K, learner});
     throw Error{SHELFI_ERR_FORMAT,
                 "learner " + std::to_string(learner) +
                     ": ciphertext residue >= its tower modulus (malformed upload; the arena slot is "
                     "marked refused until a valid upload replaces it)"};
   }
 }
+// Host uploads are staged through the scratch in pieces of about 64 MiB.
+static size_t arena_stage_cts(const Params& p) {
+  return std::max<size_t>(1, (64ull << 20) / (2ull * p.L * p.N * 8));
+}
 
-}  // extern "C"
+// Packed widths of the resident arena: B_t = 4 ceil(bitlength(q_t) / 4), at least 32.
+ArenaPack arena_pack(const Params& p) {
+  ArenaPack ap;
+  std::memset(&ap, 0, sizeof(ap));
+  for (uint32_t t = 0; t < p.L; ++t) {
+    const uint32_t bits = 64 - (uint32_t)__builtin_clzll(p.q[t]);
+    const uint32_t B = std::max(32u, (bits + 3) & ~3u);
+    if (B > 60) throw Error{SHELFI_ERR_ARG, "arena: modulus above 2^60"};
+    ap.w[t] = B;
+    ap.pre[t] = ap.sum;
+    ap.sum += B;
+  }
+  return ap;
+}
+// uint64 words per ciphertext of a C-learner arena: 2 N sum_t B_t / 64 per learner
+uint64_t arena_ct_words(const Params& p, uint64_t C) {
+  return C * 2ull * (p.N / kArenaChunk) * 8ull * arena_pack(p).sum;
+}
 
-namespace shelfi {
 // An aggregation over arena words [a, a + words) must not read a refused slot (ctx lock held).
 void arena_require_valid_locked(const shelfi_ctx* ctx, const uint64_t* a, size_t words) {
   for (const auto& r : ctx->arena_refused)
@@ -1447,31 +1483,15 @@ void arena_require_valid_locked(const shelfi_ctx* ctx, const uint64_t* a, size_t
                                         std::to_string(r.learner) + "; put a valid batch first"};
 }
 
-// The arena aggregation itself (ctx lock held, weights checked): C <= 16 learners in one
-// wavg_kernel launch per group of 16, more in one wavg_arena_many pass.
+// The arena aggregation itself (ctx lock held, weights checked): one wavg_packed pass over any
+// number of learners (groups of 16 folded into a running sum), weight limbs from the device ring.
 void wavg_arena_enqueue(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
                         uint64_t* out_dev, hipStream_t s) {
   const Params& p = ctx->p;
-  if (C > (size_t)kWavgMaxLearners) {  // one pass over any number of learners
-    const int slot = arena_weight_slot(ctx, w, C, s);
-    launch_wavg_arena_many(arena_dev, ctx->wl_dev[slot], (uint32_t)C, (uint64_t)K * 2 * p.L, p.L, p.logN,
-                           ctx->dt.tc, out_dev, s);
-    SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], s));
-    return;
-  }
-  WavgArgs a;
-  std::memset(&a, 0, sizeof(a));
-  fill_weights(a, p, w, C);
-  a.arena = arena_dev;
-  a.arena_learners = (uint32_t)C;
-  a.first_learner = 0;
-  a.out = out_dev;
-  a.rows = (uint64_t)K * 2 * p.L;
-  a.C = (uint32_t)C;
-  a.L = p.L;
-  a.logN = p.logN;
-  a.accumulate = 0;
-  launch_wavg(a, ctx->dt.tc, s);
+  const int slot = arena_weight_slot(ctx, w, C, s);
+  launch_wavg_packed(arena_dev, ctx->wl_dev[slot], (uint32_t)C, (uint64_t)K * 2 * p.L, p.L, p.logN, arena_pack(p),
+                     ctx->dt.tc, out_dev, s);
+  SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], s));
 }
 
 void check_wavg_weights(const float* w, size_t C, double delta) { check_weights(w, C, delta); }
@@ -1485,14 +1505,21 @@ int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     DeviceGuard g(ctx->device);
-    const size_t total = K * 2ull * ctx->p.L * ctx->p.N;  // residues per learner
-    if (!total) return;
-    const size_t rows = total / kArenaChunk, row_bytes = kArenaChunk * 8;
-    SHELFI_HIP(hipMemcpy2DAsync(arena_dev + learner * kArenaChunk, C * row_bytes, src, row_bytes,
-                                row_bytes, rows,
-                                src_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
-                                (hipStream_t)stream));
-    arena_validate(ctx, arena_dev, K, learner, C, (hipStream_t)stream);
+    if (!K) return;
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t ct_words = 2ull * p.L * p.N;
+    if (!src_on_host) {
+      arena_place(ctx, K, learner, C, arena_dev, s, K, false, [&](size_t k0, size_t, uint64_t*) {
+        return (const uint64_t*)src + k0 * ct_words;
+      });
+      return;
+    }
+    arena_place(ctx, K, learner, C, arena_dev, s, arena_stage_cts(p), true, [&](size_t k0, size_t kn, uint64_t* dst) {
+      SHELFI_HIP(hipMemcpyAsync(dst, (const uint64_t*)src + k0 * ct_words, kn * ct_words * 8,
+                                hipMemcpyHostToDevice, s));
+      return (const uint64_t*)dst;
+    });
   });
 }
 
@@ -1510,17 +1537,17 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
     hipStream_t s = (hipStream_t)stream;
-    const size_t row_bytes = kArenaChunk * 8;
     std::vector<HostPiece> pcs;
-    v.pieces(0, K, p, pcs);  // a blob: one payload run; an archive: 2 L tower runs per ciphertext
-    size_t r0 = 0;           // first chunk row of the next piece
-    for (const HostPiece& pc : pcs) {
-      const size_t rows = pc.n / row_bytes;
-      SHELFI_HIP(hipMemcpy2DAsync(arena_dev + (r0 * C + learner) * kArenaChunk, C * row_bytes, pc.p,
-                                  row_bytes, row_bytes, rows, hipMemcpyHostToDevice, s));
-      r0 += rows;
-    }
-    arena_validate(ctx, arena_dev, K, learner, C, s);
+    arena_place(ctx, K, learner, C, arena_dev, s, arena_stage_cts(p), true, [&](size_t k0, size_t kn, uint64_t* dst) {
+      // a blob: one payload run; an archive: 2 L tower runs per ciphertext
+      v.pieces(k0, kn, p, pcs);
+      uint8_t* d = (uint8_t*)dst;
+      for (const HostPiece& pc : pcs) {
+        SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, s));
+        d += pc.n;
+      }
+      return (const uint64_t*)dst;
+    });
   });
 }
 
@@ -1531,7 +1558,7 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
   return guarded([&] {
     if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
     check_weights(w, C, ctx->p.delta);
-    arena_require_valid_locked(ctx, arena_dev, C * K * 2ull * ctx->p.L * ctx->p.N);
+    arena_require_valid_locked(ctx, arena_dev, (size_t)arena_ct_words(ctx->p, C) * K);
     DeviceGuard g(ctx->device);
     wavg_arena_enqueue(ctx, arena_dev, w, C, K, out_dev, (hipStream_t)stream);
   });

@@ -243,7 +243,8 @@ int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const f
     check_wavg_weights(w, C, ctx->p.delta);
     const Params& p = ctx->p;
     const size_t ctw = 2ull * p.L * p.N;
-    arena_require_valid_locked(ctx, arena_dev, C * K * ctw);
+    const size_t acw = (size_t)arena_ct_words(p, C);  // arena words per ciphertext (packed, all learners)
+    arena_require_valid_locked(ctx, arena_dev, acw * K);
     if (!K) return;
     DevGuard g(ctx->device);
     const size_t W = (size_t)ctx->comm_world;
@@ -269,7 +270,7 @@ int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const f
       for (size_t gr = 0; gr < W; ++gr) {
         const size_t a = gr * Ks + kj0;
         const size_t cnt = a < K ? std::min(kn, K - a) : 0;
-        if (cnt) wavg_arena_enqueue(ctx, arena_dev + a * ctw * C, w, C, cnt, send + gr * kn * ctw, s);
+        if (cnt) wavg_arena_enqueue(ctx, arena_dev + a * acw, w, C, cnt, send + gr * kn * ctw, s);
         if (cnt < kn)  // padding past K: zero, the additive identity
           SHELFI_HIP(hipMemsetAsync(send + (gr * kn + cnt) * ctw, 0, (kn - cnt) * ctw * 8, s));
       }

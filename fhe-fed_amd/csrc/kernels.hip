@@ -56,18 +56,14 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
   return addmod(addmod(a, b, c.q), d, c.q);
 }
 
-// Two input layouts, one kernel body:
-//  * SEPARATE: each learner's batch is its own buffer (ptrs[k] + e);
-//  * INTERLEAVED (the aggregator's resident layout, shelfi_dev_arena_*): one arena
-//    [chunk][learner][512 residues]; a block then reads one contiguous C x 4 KiB
-//    region instead of C separate streams — measured 6.35 vs 5.80 TB/s at C = 16
-//    (tools/wavg_variants.py), the gap being DRAM row locality across 16 streams.
+// Separate per-learner batches (ptrs[k] + e): the bytes API's staged uploads and
+// shelfi_dev_wavg.  The aggregator's resident layout is the packed arena below.
 // CHECK (the bytes API, whose inputs are untrusted learner uploads): also flag any input
 // residue >= q_t in *a.bad (the carry-free limb sums assume canonical residues).
 // R rows per block (R = 2 for C <= 8 learners): with few learners one 512-residue row gives
 // a thread only C 16-byte loads in flight; two adjacent rows (same tower: N / 512 is even)
-// double that, and the block's arena region stays one contiguous 2 C x 4 KiB run.
-template <bool INTERLEAVED, bool CHECK = false, int R = 1>
+// double that.
+template <bool CHECK = false, int R = 1>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
   const uint64_t row0 = (uint64_t)blockIdx.x * R;
@@ -75,11 +71,6 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   const uint32_t t = (uint32_t)((base >> a.logN) % a.L);  // block-uniform tower
   const TowerConst c = tcs[t];
   const uint32_t M30 = (1u << 30) - 1;
-  // interleaved: row i's chunk, learner slice k at src + (i C + k) * 512
-  const uint64_t* __restrict__ src =
-      INTERLEAVED ? a.arena + (row0 * a.arena_learners + a.first_learner) * kWavgPerBlock + 2u * threadIdx.x
-                  : nullptr;
-  const uint64_t rstride = INTERLEAVED ? (uint64_t)a.arena_learners * kWavgPerBlock : kWavgPerBlock;
 
   uint64_t s[R][8];
 #pragma unroll
@@ -90,12 +81,11 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   constexpr int UNR = 8 / R;
 #pragma unroll UNR
   for (uint32_t k = 0; k < a.C; ++k) {
-    const uint64_t* __restrict__ p = INTERLEAVED ? src + (uint64_t)k * kWavgPerBlock
-                                                 : a.ptrs[k] + base + 2u * threadIdx.x;
+    const uint64_t* __restrict__ p = a.ptrs[k] + base + 2u * threadIdx.x;
     const uint32_t w0 = a.wl[k][t][0], w1 = a.wl[k][t][1];
     u32x4 v[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i * rstride));
+    for (int i = 0; i < R; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + i * kWavgPerBlock));
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (CHECK)
@@ -133,51 +123,227 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
   }
 }
 
-// Arena aggregation of any number of learners in one pass: groups of up to 16
-// learners accumulate carry-free as above, each group is folded and mod-added into a
-// running sum, and the output is written once (no read-modify-write per group).
-// Weight limbs come from a device buffer wl[C][L][2] (block-uniform scalar loads).
-__global__ __launch_bounds__(kWavgThreads) void wavg_arena_many(const uint64_t* __restrict__ arena,
-                                                                const uint32_t* __restrict__ wl,
-                                                                uint32_t C, uint32_t L,
-                                                                uint32_t logN,
-                                                                const TowerConst* __restrict__ tcs,
-                                                                uint64_t* __restrict__ out) {
-  const uint64_t base = (uint64_t)blockIdx.x * kWavgPerBlock;
-  const uint32_t t = (uint32_t)((base >> logN) % L);
-  const TowerConst c = tcs[t];
-  const uint32_t M30 = (1u << 30) - 1;
-  const uint64_t* __restrict__ src = arena + (uint64_t)blockIdx.x * C * kWavgPerBlock + 2u * threadIdx.x;
-  uint64_t r0 = 0, r1 = 0;
+// ------------------------------------------------------------ packed arena ----
+// The aggregator's resident layout (round 3; ArenaPack in shelfi_internal.h).  A residue of
+// tower t carries bitlength(q_t) bits of information; storing it in 64 wastes 4 of them for a
+// 60-bit q_0 and 12 for the 52-bit towers of the reference parameters (ckks.cpp:26-33:
+// scaleFactorBits 52, first modulus 60).  wavg is HBM-bound and reads every learner's residues
+// once, so the arena keeps each tower at B_t = 4 ceil(bitlength(q_t) / 4) bits: at 2^15 / L4
+// (B = 60, 52, 52, 52) a client ciphertext is 216 / 256 of its uint64 size, and the launch moves
+// 16 x 216 + 1 x 256 instead of 17 x 256 bits per coefficient (the aggregate is written as
+// uint64 [K][2][L][N] for decrypt and the collectives).
+//
+// Geometry: rows of 512 residues (one (ct, poly, tower) polynomial has N / 512 rows) in the
+// natural [K][2][L][N] order; a row holds C learner slices side by side; a slice is
+// 512 B_t bits = 16 B_t dwords.  One wave handles one row: lane l owns the 8 residues
+// 2l + (j & 1) + 128 (j >> 1), j < 8 — so the uint64 output of a row is 4 coalesced 16-byte
+// stores per lane — and its 8 B_t-bit fields, concatenated low bit first, are B_t / 4 dwords
+// d = 0 .. D-1 stored as planes: d < 4 N4 in N4 16-byte planes (plane p: lane l's dwords
+// 4p .. 4p+3 at dword p 256 + 4 l of the slice), then an 8-byte plane (if D mod 4 >= 2) and a
+// 4-byte plane (if D is odd).  Every load and store of a plane is a contiguous wave access.
+template <int B>
+struct PackShape {
+  static_assert(B % 4 == 0 && B >= 32 && B <= 60, "packed width");
+  static constexpr int D = B / 4;                 // dwords per lane (8 residues)
+  static constexpr int N4 = D / 4;                // 16-byte planes
+  static constexpr int H2 = (D % 4) >= 2 ? 1 : 0; // an 8-byte plane
+  static constexpr int H1 = D & 1;                // a 4-byte plane
+  static constexpr int O2 = N4 * 256, O1 = O2 + H2 * 128;
+  static constexpr int SLICE = 16 * B;            // dwords per learner slice
+};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int B>
+__device__ __forceinline__ void pk_load(const uint32_t* __restrict__ sl, uint32_t lane, uint32_t (&w)[B / 4]) {
+  using S = PackShape<B>;
+#pragma unroll
+  for (int p = 0; p < S::N4; ++p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sl + p * 256 + 4 * lane));
+    w[4 * p] = v.x;
+    w[4 * p + 1] = v.y;
+    w[4 * p + 2] = v.z;
+    w[4 * p + 3] = v.w;
+  }
+  if (S::H2) {
+    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(sl + S::O2 + 2 * lane));
+    w[4 * S::N4] = v.x;
+    w[4 * S::N4 + 1] = v.y;
+  }
+  if (S::H1) w[S::D - 1] = __builtin_nontemporal_load(sl + S::O1 + lane);
+}
+template <int B>
+__device__ __forceinline__ void pk_store(uint32_t* __restrict__ sl, uint32_t lane, const uint32_t (&w)[B / 4]) {
+  using S = PackShape<B>;
+#pragma unroll
+  for (int p = 0; p < S::N4; ++p) {
+    u32x4 v;
+    v.x = w[4 * p];
+    v.y = w[4 * p + 1];
+    v.z = w[4 * p + 2];
+    v.w = w[4 * p + 3];
+    *reinterpret_cast<u32x4*>(sl + p * 256 + 4 * lane) = v;
+  }
+  if (S::H2) {
+    u32x2 v;
+    v.x = w[4 * S::N4];
+    v.y = w[4 * S::N4 + 1];
+    *reinterpret_cast<u32x2*>(sl + S::O2 + 2 * lane) = v;
+  }
+  if (S::H1) sl[S::O1 + lane] = w[S::D - 1];
+}
+// Bits [o, o + nb) of a lane's field stream (o, nb compile-time after unrolling, nb <= 30):
+// one v_bfe_u32 inside a dword, v_alignbit_b32 + mask across two.
+template <int D>
+__device__ __forceinline__ uint32_t pk_bits(const uint32_t (&w)[D], int o, int nb) {
+  const int i = o >> 5, s = o & 31;
+  const uint32_t m = (1u << nb) - 1;
+  if (s + nb <= 32) return (w[i] >> s) & m;
+  return __builtin_amdgcn_alignbit(w[i + 1], w[i], (uint32_t)s) & m;
+}
+
+// Row geometry of a packed arena, wave-uniform: the row's learner-0 slice (dwords from the
+// arena base), its tower and width.
+struct PackedRow {
+  uint64_t base;
+  uint32_t t, B;
+};
+__device__ __forceinline__ PackedRow packed_row(uint64_t r, uint32_t C, uint32_t L, uint32_t logN,
+                                                const ArenaPack& ap) {
+  const uint32_t lr = logN - 9;  // rows per tower polynomial: N / 512
+  const uint64_t tp = r >> lr;   // (ct, poly, tower) index
+  const uint32_t t = (uint32_t)(tp % L);
+  const uint64_t g = tp / L;     // (ct, poly) index
+  const uint32_t chunk = (uint32_t)(r & ((1u << lr) - 1));
+  const uint32_t B = ap.w[t];
+  const uint64_t base =
+      16ull * C * (((g * ap.sum + ap.pre[t]) << lr) + (uint64_t)chunk * B);
+  return {base, t, B};
+}
+
+// One wave = one row: sum_c W_c x_c mod q_t over the row's C learner slices (carry-free limb
+// sums per group of 16 learners, as wavg_kernel), the row's 512 uint64 results stored.
+template <int B>
+__device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl, uint32_t C,
+                                                const uint32_t* __restrict__ wlt, uint32_t wl_stride,
+                                                const TowerConst& c, uint64_t* __restrict__ out,
+                                                uint32_t lane) {
+  using S = PackShape<B>;
+  uint64_t r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = 0;
   for (uint32_t k0 = 0; k0 < C; k0 += kWavgMaxLearners) {
     const uint32_t k1 = min(C, k0 + (uint32_t)kWavgMaxLearners);
-    uint64_t s00a = 0, s01a = 0, s10a = 0, s11a = 0;
-    uint64_t s00b = 0, s01b = 0, s10b = 0, s11b = 0;
-#pragma unroll 8
+    uint64_t s[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[j][i] = 0;
+#pragma unroll 2
     for (uint32_t k = k0; k < k1; ++k) {
-      const uint32_t w0 = wl[(k * L + t) * 2], w1 = wl[(k * L + t) * 2 + 1];
-      const u32x4 v = __builtin_nontemporal_load(
-          reinterpret_cast<const u32x4*>(src + (uint64_t)k * kWavgPerBlock));
-      const uint32_t xa0 = v.x & M30, xa1 = (v.x >> 30) | (v.y << 2);
-      const uint32_t xb0 = v.z & M30, xb1 = (v.z >> 30) | (v.w << 2);
-      s00a += (uint64_t)xa0 * w0;
-      s01a += (uint64_t)xa0 * w1;
-      s10a += (uint64_t)xa1 * w0;
-      s11a += (uint64_t)xa1 * w1;
-      s00b += (uint64_t)xb0 * w0;
-      s01b += (uint64_t)xb0 * w1;
-      s10b += (uint64_t)xb1 * w0;
-      s11b += (uint64_t)xb1 * w1;
+      uint32_t w[S::D];
+      pk_load<B>(sl + (uint64_t)k * S::SLICE, lane, w);
+      const uint32_t w0 = wlt[k * wl_stride], w1 = wlt[k * wl_stride + 1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t x0 = pk_bits(w, j * B, 30), x1 = pk_bits(w, j * B + 30, B - 30);
+        s[j][0] += (uint64_t)x0 * w0;
+        s[j][1] += (uint64_t)x0 * w1;
+        s[j][2] += (uint64_t)x1 * w0;
+        s[j][3] += (uint64_t)x1 * w1;
+      }
     }
-    r0 = addmod(r0, wavg_fold(s00a, s01a, s10a, s11a, c), c.q);
-    r1 = addmod(r1, wavg_fold(s00b, s01b, s10b, s11b, c), c.q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t f = wavg_fold(s[j][0], s[j][1], s[j][2], s[j][3], c);
+      r[j] = k0 ? addmod(r[j], f, c.q) : f;
+    }
   }
-  u32x4 o;
-  o.x = (uint32_t)r0;
-  o.y = (uint32_t)(r0 >> 32);
-  o.z = (uint32_t)r1;
-  o.w = (uint32_t)(r1 >> 32);
-  __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + base + 2u * threadIdx.x));
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u32x4 o;
+    o.x = (uint32_t)r[2 * g];
+    o.y = (uint32_t)(r[2 * g] >> 32);
+    o.z = (uint32_t)r[2 * g + 1];
+    o.w = (uint32_t)(r[2 * g + 1] >> 32);
+    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + 128 * g + 2 * lane));
+  }
+}
+
+constexpr int kPackedRowsPerBlock = 4;  // 4 waves, one row each
+
+__global__ __launch_bounds__(64 * kPackedRowsPerBlock) void wavg_packed(const uint32_t* __restrict__ arena,
+                                                                       const uint32_t* __restrict__ wl,
+                                                                       uint32_t C, uint64_t rows, uint32_t L,
+                                                                       uint32_t logN, ArenaPack ap,
+                                                                       const TowerConst* __restrict__ tcs,
+                                                                       uint64_t* __restrict__ out) {
+  const uint64_t r = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedRowsPerBlock + (threadIdx.x >> 6));
+  if (r >= rows) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const PackedRow pr = packed_row(r, C, L, logN, ap);
+  const TowerConst c = tcs[pr.t];
+  const uint32_t* __restrict__ sl = arena + pr.base;
+  const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
+  uint64_t* __restrict__ o = out + r * kArenaChunk;
+  switch (pr.B) {
+#define WPR(BB) \
+  case BB: wavg_packed_row<BB>(sl, C, wlt, 2 * L, c, o, lane); break;
+    WPR(32) WPR(36) WPR(40) WPR(44) WPR(48) WPR(52) WPR(56) WPR(60)
+#undef WPR
+    default: break;
+  }
+}
+
+// Upload of one learner's rows into its packed slices, with the canonical-residue check of
+// every residue (the limb sums above assume x < q_t; a refused slot is never aggregated).
+template <int B>
+__device__ __forceinline__ bool pack_row(const uint64_t* __restrict__ src, uint32_t* __restrict__ sl, uint64_t q,
+                                         uint32_t lane) {
+  using S = PackShape<B>;
+  uint64_t x[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 128 * g + 2 * lane));
+    x[2 * g] = ((uint64_t)v.y << 32) | v.x;
+    x[2 * g + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+  bool bad = false;
+  uint32_t w[S::D];
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) w[d] = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bad |= x[j] >= q;
+    const uint64_t v = x[j] & ((1ull << B) - 1);
+    const int o = j * B, i = o >> 5, s = o & 31;
+    w[i] |= (uint32_t)(v << s);
+    if (s + B > 32) w[i + 1] |= (uint32_t)(v >> (32 - s));
+    if (s + B > 64) w[i + 2] |= (uint32_t)(v >> (64 - s));
+  }
+  pk_store<B>(sl, lane, w);
+  return bad;
+}
+
+__global__ __launch_bounds__(64 * kPackedRowsPerBlock) void arena_pack_kernel(
+    const uint64_t* __restrict__ src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner, uint32_t L,
+    uint32_t logN, ArenaPack ap, const TowerConst* __restrict__ tcs, uint32_t* __restrict__ arena,
+    uint32_t* __restrict__ bad) {
+  const uint64_t i = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedRowsPerBlock + (threadIdx.x >> 6));
+  if (i >= rows) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const PackedRow pr = packed_row(row0 + i, C, L, logN, ap);
+  const uint64_t q = tcs[pr.t].q;
+  const uint64_t* __restrict__ s = src + i * kArenaChunk;
+  uint32_t* __restrict__ sl = arena + pr.base + (uint64_t)learner * 16 * pr.B;
+  bool b = false;
+  switch (pr.B) {
+#define PKR(BB) \
+  case BB: b = pack_row<BB>(s, sl, q, lane); break;
+    PKR(32) PKR(36) PKR(40) PKR(44) PKR(48) PKR(52) PKR(56) PKR(60)
+#undef PKR
+    default: b = true; break;
+  }
+  if (b) atomicOr(bad, 1u);
 }
 
 // Host side of xcd_block: the combo count G when the block passes may deal (tower, block)
@@ -189,30 +355,36 @@ static uint32_t xcd_combos(uint64_t G) {
   return (G % 8 == 0 && G <= 0xFFFFFFFFull) ? (uint32_t)G : 0;
 }
 
-void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,
-                            uint32_t L, uint32_t logN, const TowerConst* tc, uint64_t* out,
-                            hipStream_t s) {
-  const uint64_t blocks = (rows << logN) / kWavgPerBlock;
-  if (!blocks) return;
-  if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  hipLaunchKernelGGL(wavg_arena_many, dim3((uint32_t)blocks), dim3(kWavgThreads), 0, s, arena, wl_dev,
-                     C, L, logN, tc, out);
+void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows, uint32_t L,
+                        uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* out, hipStream_t s) {
+  const uint64_t nrows = (rows << logN) / kArenaChunk;
+  if (!nrows) return;
+  const uint64_t blocks = (nrows + kPackedRowsPerBlock - 1) / kPackedRowsPerBlock;
+  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  hipLaunchKernelGGL(wavg_packed, dim3((uint32_t)blocks), dim3(64 * kPackedRowsPerBlock), 0, s,
+                     reinterpret_cast<const uint32_t*>(arena), wl_dev, C, nrows, L, logN, ap, tc, out);
+  SHELFI_HIP(hipGetLastError());
+}
+
+void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner,
+                       uint32_t L, uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* arena,
+                       uint32_t* bad, hipStream_t s) {
+  if (!rows) return;
+  const uint64_t blocks = (rows + kPackedRowsPerBlock - 1) / kPackedRowsPerBlock;
+  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "arena too large"};
+  hipLaunchKernelGGL(arena_pack_kernel, dim3((uint32_t)blocks), dim3(64 * kPackedRowsPerBlock), 0, s, src, row0,
+                     rows, C, learner, L, logN, ap, tc, reinterpret_cast<uint32_t*>(arena), bad);
   SHELFI_HIP(hipGetLastError());
 }
 
 // Rows per wavg block: with C <= 8 learners a one-row thread has only C 16-byte loads in
-// flight; the arena kernel then takes 4 rows (4 C loads), the separate-buffer one 2.  Measured
-// in one process per shape (tools/wavg_rows_ab.py, profiles/probes/r03_wavg_rows_ab.txt):
-// 8 x 156 (cfg5) 0.729 -> 0.786 of 8 TB/s, 8 x 714 0.718 -> 0.778, 2 x 714 0.646 -> 0.675,
-// 4 x 714 a tie.  At 16 learners two rows win once the launch has >= 16384 rows (16 x 714:
-// 0.705 -> 0.757 there, and through bench.py 0.810 -> 0.822, r03_wavg_rows_bench.txt; 16 x 32
-// at 2^16 / L6: 0.717 -> 0.750) and lose on the small cfg2 launch (16 x 4: 0.767 -> 0.715);
-// 12 x 476 kept one row best (0.778 vs 0.759).  SHELFI_WAVG_ROWS=1|2|4 forces one (A/B probe
-// switch, read per launch).
-static int wavg_rows(uint32_t C, bool arena, uint64_t rows) {
+// flight; the kernel then takes 2 rows.  Measured in one process per shape (tools/wavg_rows_ab.py,
+// profiles/probes/r03_wavg_rows_ab.txt).  SHELFI_WAVG_ROWS=1|2 forces one (A/B probe switch, read
+// per launch).
+static int wavg_rows(uint32_t C, uint64_t rows) {
   const char* env = getenv("SHELFI_WAVG_ROWS");
-  if (env && (*env == '1' || *env == '2' || (*env == '4' && arena))) return *env - '0';
-  if (C <= 8) return arena ? 4 : 2;
+  if (env && (*env == '1' || *env == '2')) return *env - '0';
+  if (C <= 8) return 2;
   return C >= 16 && rows >= 16384 ? 2 : 1;
 }
 
@@ -220,51 +392,19 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t total = a.rows << a.logN;
   const uint64_t rows = total / kWavgPerBlock;  // always even: N / 512 >= 2 rows per tower
   if (!rows) return;
-  int R = wavg_rows(a.C, a.arena != nullptr, rows);
+  int R = wavg_rows(a.C, rows);
   while (R > 1 && ((1ull << a.logN) / kWavgPerBlock) % R) R >>= 1;  // a block stays in one tower
   const uint64_t blocks = rows / R;
   if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   const dim3 g((uint32_t)blocks), b(kWavgThreads);
-  if (a.arena && R == 4)
-    hipLaunchKernelGGL((wavg_kernel<true, false, 4>), g, b, 0, s, a, tc);
-  else if (a.arena && R == 2)
-    hipLaunchKernelGGL((wavg_kernel<true, false, 2>), g, b, 0, s, a, tc);
-  else if (a.arena)
-    hipLaunchKernelGGL((wavg_kernel<true, false, 1>), g, b, 0, s, a, tc);
-  else if (a.bad && R == 2)
-    hipLaunchKernelGGL((wavg_kernel<false, true, 2>), g, b, 0, s, a, tc);
+  if (a.bad && R == 2)
+    hipLaunchKernelGGL((wavg_kernel<true, 2>), g, b, 0, s, a, tc);
   else if (a.bad)
-    hipLaunchKernelGGL((wavg_kernel<false, true, 1>), g, b, 0, s, a, tc);
+    hipLaunchKernelGGL((wavg_kernel<true, 1>), g, b, 0, s, a, tc);
   else if (R == 2)
-    hipLaunchKernelGGL((wavg_kernel<false, false, 2>), g, b, 0, s, a, tc);
+    hipLaunchKernelGGL((wavg_kernel<false, 2>), g, b, 0, s, a, tc);
   else
-    hipLaunchKernelGGL((wavg_kernel<false, false, 1>), g, b, 0, s, a, tc);
-  SHELFI_HIP(hipGetLastError());
-}
-
-// Upload validation of an arena slot (shelfi_dev_arena_put*): every residue of learner
-// `learner`'s slices must be canonical (< q_t) — the carry-free limb sums of wavg_kernel
-// drop bits >= 2^60 and would otherwise return a silently wrong aggregate.  One thread =
-// 2 residues of one 512-residue slice (a block = one chunk row); reads 1/C of the arena.
-__global__ __launch_bounds__(256) void arena_check_kernel(const uint64_t* __restrict__ arena, uint32_t C,
-                                                          uint32_t learner, uint32_t L, uint32_t logN,
-                                                          const TowerConst* __restrict__ tcs,
-                                                          uint32_t* __restrict__ bad) {
-  const uint64_t r = blockIdx.x;  // chunk row: residues [r 512, (r + 1) 512) of the learner's batch
-  const uint32_t t = (uint32_t)(((r * kArenaChunk) >> logN) % L);
-  const uint64_t q = tcs[t].q;
-  const u32x4 v = __builtin_nontemporal_load(
-      reinterpret_cast<const u32x4*>(arena + (r * C + learner) * kArenaChunk + 2u * threadIdx.x));
-  if ((((uint64_t)v.y << 32) | v.x) >= q || (((uint64_t)v.w << 32) | v.z) >= q) atomicOr(bad, 1u);
-}
-
-void launch_arena_check(const uint64_t* arena, uint32_t C, uint32_t learner, uint64_t rows, uint32_t L,
-                        uint32_t logN, const TowerConst* tc, uint32_t* bad, hipStream_t s) {
-  const uint64_t blocks = (rows << logN) / kArenaChunk;
-  if (!blocks) return;
-  if (blocks > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "arena too large"};
-  hipLaunchKernelGGL(arena_check_kernel, dim3((uint32_t)blocks), dim3(kArenaChunk / 2), 0, s, arena, C,
-                     learner, L, logN, tc, bad);
+    hipLaunchKernelGGL((wavg_kernel<false, 1>), g, b, 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());
 }
 

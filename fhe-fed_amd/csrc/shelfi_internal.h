@@ -187,7 +187,7 @@ struct shelfi_ctx {
   // over an arena range holding one fails instead of summing the refused residues
   struct ArenaRefusal {
     const uint64_t* arena;
-    size_t words;  // C * K * 2 * L * N of that arena
+    size_t words;  // shelfi_arena_words(C, K) of that arena
     size_t learner;
   };
   std::vector<ArenaRefusal> arena_refused;
@@ -197,7 +197,7 @@ struct shelfi_ctx {
   std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)
   std::string pal_keytag;        // PALISADE keys: key tag
   int wire = 0;                  // encrypt output: 0 blob, 1 PALISADE archive
-  // device weight-limb buffers of wavg_arena_many (ring; reused while weights repeat)
+  // device weight-limb buffers of wavg_packed (ring; reused while weights repeat)
   static constexpr int kWeightRing = 8;
   uint32_t* wl_dev[kWeightRing] = {};
   size_t wl_cap[kWeightRing] = {};
@@ -221,26 +221,39 @@ namespace shelfi {
 
 // device-side launchers (kernels.hip)
 constexpr int kWavgMaxLearners = 16;  // per launch (limb sums stay < 2^64)
-constexpr int kArenaChunk = 512;      // residues per (chunk, learner) slice of an arena
+constexpr int kArenaChunk = 512;      // residues per (row, learner) slice of an arena
 struct WavgArgs {
-  const uint64_t* ptrs[kWavgMaxLearners];          // SEPARATE layout: learner batches
+  const uint64_t* ptrs[kWavgMaxLearners];          // learner batches [K][2][L][N]
   uint32_t wl[kWavgMaxLearners][kMaxTowers][2];    // 30-bit limbs of W_{c,t}
-  const uint64_t* arena;                           // INTERLEAVED layout (or null)
   uint64_t* out;
   uint64_t rows;  // K * 2 * L
   uint32_t C, L, logN, accumulate;
-  uint32_t arena_learners, first_learner;          // arena width, first learner of this pass
-  uint32_t* bad;  // SEPARATE layout: device flag set when an input residue is >= q (or null)
+  uint32_t* bad;  // device flag set when an input residue is >= q (or null)
 };
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
-void launch_wavg_arena_many(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows,
-                            uint32_t L, uint32_t logN, const TowerConst* tc, uint64_t* out,
-                            hipStream_t s);
+// Packed arena (round 3): the aggregator's resident layout.  Tower t's residues are
+// stored at B_t = 4 ceil(bitlength(q_t) / 4) bits (32 <= B_t <= 60) instead of 64: rows of 512
+// residues of one (ct, poly, tower) in natural order, each row holding the C learners' slices
+// side by side, a slice 16 B_t dwords (lane l of a wave owns residues 2l, 2l + 1 (+128 g, g < 4),
+// packed into B_t / 4 dwords stored as 16-byte / 8-byte / 4-byte planes, see kernels.hip).
+struct ArenaPack {
+  uint32_t w[kMaxTowers];    // B_t
+  uint32_t pre[kMaxTowers];  // sum of B_t' for t' < t
+  uint32_t sum;              // sum of B_t
+};
+ArenaPack arena_pack(const Params& p);                 // api.cpp
+uint64_t arena_ct_words(const Params& p, uint64_t C);  // uint64 words per ciphertext of C learners
+// sum_c W_c x_c over C learners (any C: groups of 16 folded into a running sum), weight limbs
+// wl_dev [C][L][2]; rows = K * 2 * L ciphertext polynomials
+void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows, uint32_t L,
+                        uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* out, hipStream_t s);
+// Packs rows [row0, row0 + rows) of learner `learner`'s [K][2][L][N] batch (src holds exactly those
+// rows' residues, 512 per row) into its arena slices; *bad |= 1 when a residue is >= q_t.
+void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner,
+                       uint32_t L, uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* arena,
+                       uint32_t* bad, hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
-// flags *bad when a residue of learner `learner`'s slices of an arena of C learners is >= q_t
-void launch_arena_check(const uint64_t* arena, uint32_t C, uint32_t learner, uint64_t rows, uint32_t L,
-                        uint32_t logN, const TowerConst* tc, uint32_t* bad, hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                 const DeviceTables& dt, hipStream_t s);
 void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,

@@ -198,11 +198,16 @@ int shelfi_palisade_embed_context(const uint8_t* ctxfile, size_t len, uint8_t** 
  * EvalAdd, ckks.cpp:286-297).  in_dev: host array of C device pointers. */
 int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float* w, size_t C,
                     size_t K, uint64_t* out_dev, void* stream);
-/* Learner-interleaved arena: the aggregator's resident layout for C learners' K
- * ciphertexts, uint64 [K*2*L*N/512][C][512] (512-residue slices of every learner side
- * by side), so one aggregation block reads one contiguous C x 4 KiB region.
- * shelfi_arena_words() = C*K*2*L*N.  shelfi_dev_arena_put copies learner `learner`'s
- * [K][2][L][N] batch (device memory, or host memory if src_on_host) into its slices. */
+/* Packed learner-interleaved arena: the aggregator's resident layout for C learners' K
+ * ciphertexts.  Rows of 512 residues in [K][2][L][N] order; a row holds the C learners'
+ * slices side by side, and every residue of tower t is packed to B_t = 4 ceil(bitlength(q_t)/4)
+ * bits (>= 32; 60/52/52/52 at the reference's 2^15/L4: 216 of 256 bits per coefficient), so one
+ * aggregation wave reads one contiguous C-slice region and the launch moves 16% fewer bytes
+ * (DESIGN.md §3).  The layout is opaque: size it with shelfi_arena_words() (uint64 words;
+ * ciphertexts [k0, k1) of an arena start at word k0 * shelfi_arena_words(ctx, C, 1) and are
+ * themselves an arena of k1 - k0 ciphertexts).  shelfi_dev_arena_put packs learner
+ * `learner`'s [K][2][L][N] uint64 batch (device memory, or host memory if src_on_host) into
+ * its slices. */
 size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K);
 /* Every put validates what landed: one device pass over the learner's slices checks that
  * each residue is < q_t (the aggregation's carry-free limb sums assume canonical

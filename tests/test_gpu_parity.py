@@ -167,6 +167,49 @@ def test_wavg_arena_bitexact(cfg2, C, K):
     assert ar.wavg(w, out=buf) is buf
 
 
+@pytest.mark.parametrize("scale,first,depth,C,K", [
+    (52, 60, 1, 16, 2),   # 2^13-class chain, B = 60, 52
+    (40, 60, 2, 9, 3),    # B = 60, 40, 40
+    (41, 57, 2, 3, 2),    # 57 / 41-bit towers: B = 60, 44, 44 (widths rounded up to 4)
+    (35, 47, 3, 18, 1),   # B = 48, 36, 36, 36; > 16 learners (two groups)
+    (30, 45, 1, 5, 2),    # 30-bit towers: B = 32 (the minimum width)
+])
+def test_wavg_arena_packed_widths(tmp_path, scale, first, depth, C, K):
+    """The packed arena at every width class its kernels carry: residues at 0, q-1
+    and random, device and host placement, whole-range and sub-range aggregation == oracle."""
+    ck = m.CKKS("ckks", 1024, scale, str(tmp_path) + os.sep, multDepth=depth, firstModBits=first,
+                seed=3, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    inf, q, psi, N, S, delta = _ctx_arrays(ck)
+    L = len(q)
+    words = ck._lib.shelfi_arena_words(ck._ctx, C, K)
+    B = [max(32, (int(x).bit_length() + 3) // 4 * 4) for x in q]
+    assert words == C * K * 2 * N * sum(B) // 64
+    rng = np.random.default_rng(scale * 100 + C)
+    cts = []
+    for c in range(C):
+        a = np.empty((K, 2, L, N), np.uint64)
+        for t in range(L):
+            a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+            a[:, 0, t, :7] = int(q[t]) - 1
+            a[:, 1, t, -5:] = 0
+        cts.append(a)
+    ar = D.Arena(ck, C, K)
+    for c in range(C):
+        if c % 3 == 1:
+            ar.put(c, m.blob_pack(ck, cts[c]))
+        else:
+            ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
+    w = list(rng.uniform(-1, 1, C))
+    got = ar.wavg(w)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+    if K > 1:
+        got = ar.wavg(w, k0=1, k1=K)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg([c[1:] for c in cts], w, q, delta))
+
+
 def test_wavg_arena_many_learners_ranges_and_weights(cfg2):
     """> 16 learners in one pass (wavg_arena_many): sub-ranges of the arena, alternating
     weight vectors (the device weight ring), residues at q-1 with weight 1.0."""
