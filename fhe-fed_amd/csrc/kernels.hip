@@ -220,15 +220,14 @@ __device__ __forceinline__ PackedRow packed_row(uint64_t r, uint32_t C, uint32_t
   return {base, t, B};
 }
 
-// One wave = one row: sum_c W_c x_c mod q_t over the row's C learner slices (carry-free limb
-// sums per group of 16 learners, as wavg_kernel), the row's 512 uint64 results stored.
-template <int B>
+// One wave = one row: sum_c W_c x_c mod q_t over the row's C learner slices (carry-free limb sums
+// per group of 16 learners, as wavg_kernel), into r[8] (lane l's residues 2l + (j & 1) + 128 (j >> 1)).
+template <int B, int U>
 __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl, uint32_t C,
-                                                const uint32_t* __restrict__ wlt, uint32_t wl_stride,
-                                                const TowerConst& c, uint64_t* __restrict__ out,
-                                                uint32_t lane) {
+                                                const uint32_t* __restrict__ wlt,
+                                                uint32_t wl_stride, const TowerConst& c, uint32_t lane,
+                                                uint64_t (&r)[8]) {
   using S = PackShape<B>;
-  uint64_t r[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = 0;
   for (uint32_t k0 = 0; k0 < C; k0 += kWavgMaxLearners) {
@@ -238,7 +237,7 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[j][i] = 0;
-#pragma unroll 2
+#pragma unroll U
     for (uint32_t k = k0; k < k1; ++k) {
       uint32_t w[S::D];
       pk_load<B>(sl + (uint64_t)k * S::SLICE, lane, w);
@@ -253,44 +252,46 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t f = wavg_fold(s[j][0], s[j][1], s[j][2], s[j][3], c);
-      r[j] = k0 ? addmod(r[j], f, c.q) : f;
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    u32x4 o;
-    o.x = (uint32_t)r[2 * g];
-    o.y = (uint32_t)(r[2 * g] >> 32);
-    o.z = (uint32_t)r[2 * g + 1];
-    o.w = (uint32_t)(r[2 * g + 1] >> 32);
-    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + 128 * g + 2 * lane));
+    for (int j = 0; j < 8; ++j) r[j] = addmod(r[j], wavg_fold(s[j][0], s[j][1], s[j][2], s[j][3], c), c.q);
   }
 }
 
-constexpr int kPackedRowsPerBlock = 4;  // 4 waves, one row each
+constexpr int kPackedWaves = 4;  // waves per block, one row each
 
-__global__ __launch_bounds__(64 * kPackedRowsPerBlock) void wavg_packed(const uint32_t* __restrict__ arena,
-                                                                       const uint32_t* __restrict__ wl,
-                                                                       uint32_t C, uint64_t rows, uint32_t L,
-                                                                       uint32_t logN, ArenaPack ap,
-                                                                       const TowerConst* __restrict__ tcs,
-                                                                       uint64_t* __restrict__ out) {
-  const uint64_t r = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedRowsPerBlock + (threadIdx.x >> 6));
+template <int U>
+__global__ __launch_bounds__(64 * kPackedWaves) void wavg_packed(const uint32_t* __restrict__ arena,
+                                                                const uint32_t* __restrict__ wl,
+                                                                uint32_t C, uint64_t rows, uint32_t L,
+                                                                uint32_t logN, ArenaPack ap,
+                                                                const TowerConst* __restrict__ tcs,
+                                                                uint64_t* __restrict__ out) {
+  const uint64_t r = (uint64_t)blockIdx.x * kPackedWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (r >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   const PackedRow pr = packed_row(r, C, L, logN, ap);
   const TowerConst c = tcs[pr.t];
   const uint32_t* __restrict__ sl = arena + pr.base;
   const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
-  uint64_t* __restrict__ o = out + r * kArenaChunk;
+  uint64_t res[8];
   switch (pr.B) {
 #define WPR(BB) \
-  case BB: wavg_packed_row<BB>(sl, C, wlt, 2 * L, c, o, lane); break;
+  case BB: wavg_packed_row<BB, U>(sl, C, wlt, 2 * L, c, lane, res); break;
     WPR(32) WPR(36) WPR(40) WPR(44) WPR(48) WPR(52) WPR(56) WPR(60)
 #undef WPR
-    default: break;
+    default:
+#pragma unroll
+      for (int j = 0; j < 8; ++j) res[j] = 0;
+      break;
+  }
+  uint64_t* __restrict__ o = out + r * kArenaChunk;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u32x4 v;
+    v.x = (uint32_t)res[2 * g];
+    v.y = (uint32_t)(res[2 * g] >> 32);
+    v.z = (uint32_t)res[2 * g + 1];
+    v.w = (uint32_t)(res[2 * g + 1] >> 32);
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + 128 * g + 2 * lane));
   }
 }
 
@@ -324,11 +325,11 @@ __device__ __forceinline__ bool pack_row(const uint64_t* __restrict__ src, uint3
   return bad;
 }
 
-__global__ __launch_bounds__(64 * kPackedRowsPerBlock) void arena_pack_kernel(
+__global__ __launch_bounds__(64 * kPackedWaves) void arena_pack_kernel(
     const uint64_t* __restrict__ src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner, uint32_t L,
     uint32_t logN, ArenaPack ap, const TowerConst* __restrict__ tcs, uint32_t* __restrict__ arena,
     uint32_t* __restrict__ bad) {
-  const uint64_t i = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedRowsPerBlock + (threadIdx.x >> 6));
+  const uint64_t i = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedWaves + (threadIdx.x >> 6));
   if (i >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   const PackedRow pr = packed_row(row0 + i, C, L, logN, ap);
@@ -359,10 +360,23 @@ void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t 
                         uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* out, hipStream_t s) {
   const uint64_t nrows = (rows << logN) / kArenaChunk;
   if (!nrows) return;
-  const uint64_t blocks = (nrows + kPackedRowsPerBlock - 1) / kPackedRowsPerBlock;
+  const uint64_t blocks = (nrows + kPackedWaves - 1) / kPackedWaves;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  hipLaunchKernelGGL(wavg_packed, dim3((uint32_t)blocks), dim3(64 * kPackedRowsPerBlock), 0, s,
-                     reinterpret_cast<const uint32_t*>(arena), wl_dev, C, nrows, L, logN, ap, tc, out);
+  if (nrows > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  // learners unrolled per iteration: SHELFI_PACK_UNROLL=1|2|4 (A/B probe switch, read per launch;
+  // 2 and 4 measured equal, profiles/probes/r03_wavg_packed_ab.txt)
+  const char* env = getenv("SHELFI_PACK_UNROLL");
+  const int u = env ? atoi(env) : 2;
+#define WPK(UU)                                                                                              \
+  hipLaunchKernelGGL((wavg_packed<UU>), dim3((uint32_t)blocks), dim3(64 * kPackedWaves), 0, s,               \
+                     reinterpret_cast<const uint32_t*>(arena), wl_dev, C, nrows, L, logN, ap, tc, out)
+  if (u == 1)
+    WPK(1);
+  else if (u == 4)
+    WPK(4);
+  else
+    WPK(2);
+#undef WPK
   SHELFI_HIP(hipGetLastError());
 }
 
@@ -370,9 +384,9 @@ void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32
                        uint32_t L, uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* arena,
                        uint32_t* bad, hipStream_t s) {
   if (!rows) return;
-  const uint64_t blocks = (rows + kPackedRowsPerBlock - 1) / kPackedRowsPerBlock;
+  const uint64_t blocks = (rows + kPackedWaves - 1) / kPackedWaves;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "arena too large"};
-  hipLaunchKernelGGL(arena_pack_kernel, dim3((uint32_t)blocks), dim3(64 * kPackedRowsPerBlock), 0, s, src, row0,
+  hipLaunchKernelGGL(arena_pack_kernel, dim3((uint32_t)blocks), dim3(64 * kPackedWaves), 0, s, src, row0,
                      rows, C, learner, L, logN, ap, tc, reinterpret_cast<uint32_t*>(arena), bad);
   SHELFI_HIP(hipGetLastError());
 }

@@ -168,15 +168,16 @@ def test_wavg_arena_bitexact(cfg2, C, K):
 
 
 @pytest.mark.parametrize("scale,first,depth,C,K", [
-    (52, 60, 1, 16, 2),   # 2^13-class chain, B = 60, 52
+    (52, 60, 1, 16, 2),   # 2^13-class chain, B = 60, 52 or 56 (a 53-bit prime)
     (40, 60, 2, 9, 3),    # B = 60, 40, 40
     (41, 57, 2, 3, 2),    # 57 / 41-bit towers: B = 60, 44, 44 (widths rounded up to 4)
     (35, 47, 3, 18, 1),   # B = 48, 36, 36, 36; > 16 learners (two groups)
     (30, 45, 1, 5, 2),    # 30-bit towers: B = 32 (the minimum width)
 ])
-def test_wavg_arena_packed_widths(tmp_path, scale, first, depth, C, K):
+def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C, K):
     """The packed arena at every width class its kernels carry: residues at 0, q-1
-    and random, device and host placement, whole-range and sub-range aggregation == oracle."""
+    and random, device and host placement, whole-range and sub-range aggregation == oracle, at
+    every learner unroll depth of wavg_packed."""
     ck = m.CKKS("ckks", 1024, scale, str(tmp_path) + os.sep, multDepth=depth, firstModBits=first,
                 seed=3, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
@@ -201,9 +202,13 @@ def test_wavg_arena_packed_widths(tmp_path, scale, first, depth, C, K):
         else:
             ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
     w = list(rng.uniform(-1, 1, C))
-    got = ar.wavg(w)
-    torch.cuda.synchronize()
-    assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg(cts, w, q, delta))
+    ref = O.wavg(cts, w, q, delta)
+    for unroll in ("1", "2", "4"):
+        monkeypatch.setenv("SHELFI_PACK_UNROLL", unroll)
+        got = ar.wavg(w)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), unroll
+    monkeypatch.delenv("SHELFI_PACK_UNROLL")
     if K > 1:
         got = ar.wavg(w, k0=1, k1=K)
         torch.cuda.synchronize()

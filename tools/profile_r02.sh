@@ -16,8 +16,9 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
   -- /usr/bin/python3 bench.py $B > /dev/null 2> "$out/wfetch.err"
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out" -o wwrite \
   -- /usr/bin/python3 bench.py $B > /dev/null 2> "$out/wwrite.err"
+algo=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['roofline']['bytes_per_launch'])" "$out/${tag}_bench.json")
 python3 tools/pmc_traffic.py "$out/wfetch_counter_collection.csv" "$out/wwrite_counter_collection.csv" \
-  --kernel "wavg_kernel<true," --workload cfg3 --learners 16 --algorithmic-bytes 25455230976 \
+  --kernel "wavg_packed" --workload cfg3 --learners 16 --algorithmic-bytes "$algo" \
   -o "$out/wavg_traffic.json" > /dev/null
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out" -o efetch \
   -- /usr/bin/python3 tools/encdec_prof.py 714 1 > /dev/null 2> "$out/efetch.err"
