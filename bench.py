@@ -671,7 +671,7 @@ def main():
             ck.set_wire_format("shelfi")
 
     # roofline of the dominant kernel: algorithmic bytes = the C learners' packed residues
-    # (K * 2 * N * sum_t B_t / 8 each, B_t = 4 ceil(bitlength(q_t) / 4)) read once
+    # (K * 2 * N * sum_t U_t / 8 each, U_t ~ bitlength(q_t)) read once
     # + the uint64 aggregate K * 2 * L * N * 8 written once
     bytes_per_launch = main_mode["in_bytes"] + K_loc * 2 * L * N * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
@@ -681,7 +681,8 @@ def main():
             tj = json.load(f)
         kname = "wavg_packed" if args.layout == "arena" else "wavg_kernel"
         if (tj.get("workload") == args.workload and tj.get("learners") == C_loc and K_loc == K
-                and str(tj.get("kernel", "")).startswith(kname)):
+                and str(tj.get("kernel", "")).startswith(kname)
+                and int(tj.get("algorithmic_bytes_per_launch", -1)) == bytes_per_launch):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

@@ -84,8 +84,9 @@ def wavg(ckks, cts: Sequence, weights: Sequence[float], out=None):
 class Arena:
     """The aggregator's resident layout for C learners' K ciphertexts: one HBM buffer of
     rows of 512 residues (the [K][2][L][N] order), each row holding the C learners' slices
-    side by side, every residue of tower t packed to B_t = 4 ceil(bitlength(q_t) / 4) bits
-    (60 / 52 / 52 / 52 at 2^15 / L4: 216 of 256 bits per coefficient).  put()
+    side by side, every residue of tower t packed to U_t bits (bitlength(q_t) when that is 1
+    mod 4, else rounded up to a multiple of 4; 60 / 53 / 52 / 53 at 2^15 / L4: 218 of 256 bits
+    per coefficient).  put()
     packs and validates each learner's batch once per round; wavg() then reads one
     contiguous C-slice region per row and writes the [K][2][L][N] uint64 aggregate."""
 

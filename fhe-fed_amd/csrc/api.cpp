@@ -1456,21 +1456,22 @@ static size_t arena_stage_cts(const Params& p) {
   return std::max<size_t>(1, (64ull << 20) / (2ull * p.L * p.N * 8));
 }
 
-// Packed widths of the resident arena: B_t = 4 ceil(bitlength(q_t) / 4), at least 32.
+// Packed widths of the resident arena: U_t = bitlength(q_t) when that is 1 mod 4 (a
+// 4-multiple field + a flag plane for the top bit), else 4 ceil(bitlength(q_t) / 4); at least 32.
 ArenaPack arena_pack(const Params& p) {
   ArenaPack ap;
   std::memset(&ap, 0, sizeof(ap));
   for (uint32_t t = 0; t < p.L; ++t) {
     const uint32_t bits = 64 - (uint32_t)__builtin_clzll(p.q[t]);
-    const uint32_t B = std::max(32u, (bits + 3) & ~3u);
-    if (B > 60) throw Error{SHELFI_ERR_ARG, "arena: modulus above 2^60"};
-    ap.w[t] = B;
+    const uint32_t U = bits <= 32 ? 32u : (bits % 4 == 1 ? bits : (bits + 3) & ~3u);
+    if (U > 60) throw Error{SHELFI_ERR_ARG, "arena: modulus above 2^60"};
+    ap.w[t] = U;
     ap.pre[t] = ap.sum;
-    ap.sum += B;
+    ap.sum += U;
   }
   return ap;
 }
-// uint64 words per ciphertext of a C-learner arena: 2 N sum_t B_t / 64 per learner
+// uint64 words per ciphertext of a C-learner arena: 2 N sum_t U_t / 64 per learner
 uint64_t arena_ct_words(const Params& p, uint64_t C) {
   return C * 2ull * (p.N / kArenaChunk) * 8ull * arena_pack(p).sum;
 }

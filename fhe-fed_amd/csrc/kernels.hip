@@ -125,37 +125,42 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
 
 // ------------------------------------------------------------ packed arena ----
 // The aggregator's resident layout (round 3; ArenaPack in shelfi_internal.h).  A residue of
-// tower t carries bitlength(q_t) bits of information; storing it in 64 wastes 4 of them for a
-// 60-bit q_0 and 12 for the 52-bit towers of the reference parameters (ckks.cpp:26-33:
+// tower t carries bitlength(q_t) bits of information; storing it in 64 wastes 4 of them for the
+// 60-bit q_0 and 11-12 for the 52/53-bit towers of the reference parameters (ckks.cpp:26-33:
 // scaleFactorBits 52, first modulus 60).  wavg is HBM-bound and reads every learner's residues
-// once, so the arena keeps each tower at B_t = 4 ceil(bitlength(q_t) / 4) bits: at 2^15 / L4
-// (B = 60, 52, 52, 52) a client ciphertext is 216 / 256 of its uint64 size, and the launch moves
-// 16 x 216 + 1 x 256 instead of 17 x 256 bits per coefficient (the aggregate is written as
-// uint64 [K][2][L][N] for decrypt and the collectives).
+// once, so the arena keeps tower t at U_t = bitlength(q_t) bits when that is 1 mod 4 (a field of
+// B_t = U_t - 1 bits plus one top bit in a flag plane) and at U_t = B_t = 4 ceil(bitlength / 4)
+// otherwise (at least 32).  At 2^15 / L4 (60, 53, 52, 53 bits) a client ciphertext is 218 / 256
+// of its uint64 size, and the launch moves 16 x 218 + 256 instead of 17 x 256 bits per
+// coefficient (the aggregate is written as uint64 [K][2][L][N] for decrypt and the collectives).
 //
 // Geometry: rows of 512 residues (one (ct, poly, tower) polynomial has N / 512 rows) in the
-// natural [K][2][L][N] order; a row holds C learner slices side by side; a slice is
-// 512 B_t bits = 16 B_t dwords.  One wave handles one row: lane l owns the 8 residues
-// 2l + (j & 1) + 128 (j >> 1), j < 8 — so the uint64 output of a row is 4 coalesced 16-byte
-// stores per lane — and its 8 B_t-bit fields, concatenated low bit first, are B_t / 4 dwords
-// d = 0 .. D-1 stored as planes: d < 4 N4 in N4 16-byte planes (plane p: lane l's dwords
-// 4p .. 4p+3 at dword p 256 + 4 l of the slice), then an 8-byte plane (if D mod 4 >= 2) and a
-// 4-byte plane (if D is odd).  Every load and store of a plane is a contiguous wave access.
-template <int B>
+// natural [K][2][L][N] order; a row holds C learner slices side by side; a slice is 512 U_t bits
+// = 16 U_t dwords.  One wave handles one row: lane l owns the 8 residues 2l + (j & 1) + 128 (j >> 1),
+// j < 8 — so the uint64 output of a row is 4 coalesced 16-byte stores per lane — and their low
+// B_t bits, concatenated low bit first, are B_t / 4 dwords d = 0 .. D-1 stored as planes: d < 4 N4
+// in N4 16-byte planes (plane p: lane l's dwords 4p .. 4p+3 at dword p 256 + 4 l of the slice),
+// then an 8-byte plane (if D mod 4 >= 2) and a 4-byte plane (if D is odd); with a flag plane, byte
+// 64 B_t + l of the slice holds bit B_t of lane l's 8 residues.  Every plane access is one
+// contiguous wave access.
+template <int UB>
 struct PackShape {
-  static_assert(B % 4 == 0 && B >= 32 && B <= 60, "packed width");
-  static constexpr int D = B / 4;                 // dwords per lane (8 residues)
+  static constexpr int B = UB & ~3, F = UB & 3;   // field bits, flag plane (0 / 1)
+  static_assert(F <= 1 && B >= 32 && UB <= 60, "packed width");
+  static constexpr int D = B / 4;                 // field dwords per lane (8 residues)
   static constexpr int N4 = D / 4;                // 16-byte planes
   static constexpr int H2 = (D % 4) >= 2 ? 1 : 0; // an 8-byte plane
   static constexpr int H1 = D & 1;                // a 4-byte plane
   static constexpr int O2 = N4 * 256, O1 = O2 + H2 * 128;
-  static constexpr int SLICE = 16 * B;            // dwords per learner slice
+  static constexpr int OF = 64 * B;               // flag plane (bytes)
+  static constexpr int SLICE = 16 * UB;           // dwords per learner slice
 };
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-template <int B>
-__device__ __forceinline__ void pk_load(const uint32_t* __restrict__ sl, uint32_t lane, uint32_t (&w)[B / 4]) {
-  using S = PackShape<B>;
+template <int UB>
+__device__ __forceinline__ void pk_load(const uint32_t* __restrict__ sl, uint32_t lane,
+                                        uint32_t (&w)[PackShape<UB>::D], uint32_t& fl) {
+  using S = PackShape<UB>;
 #pragma unroll
   for (int p = 0; p < S::N4; ++p) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sl + p * 256 + 4 * lane));
@@ -170,10 +175,12 @@ __device__ __forceinline__ void pk_load(const uint32_t* __restrict__ sl, uint32_
     w[4 * S::N4 + 1] = v.y;
   }
   if (S::H1) w[S::D - 1] = __builtin_nontemporal_load(sl + S::O1 + lane);
+  fl = S::F ? (uint32_t)__builtin_nontemporal_load(reinterpret_cast<const uint8_t*>(sl) + S::OF + lane) : 0u;
 }
-template <int B>
-__device__ __forceinline__ void pk_store(uint32_t* __restrict__ sl, uint32_t lane, const uint32_t (&w)[B / 4]) {
-  using S = PackShape<B>;
+template <int UB>
+__device__ __forceinline__ void pk_store(uint32_t* __restrict__ sl, uint32_t lane,
+                                         const uint32_t (&w)[PackShape<UB>::D], uint32_t fl) {
+  using S = PackShape<UB>;
 #pragma unroll
   for (int p = 0; p < S::N4; ++p) {
     u32x4 v;
@@ -190,6 +197,7 @@ __device__ __forceinline__ void pk_store(uint32_t* __restrict__ sl, uint32_t lan
     *reinterpret_cast<u32x2*>(sl + S::O2 + 2 * lane) = v;
   }
   if (S::H1) sl[S::O1 + lane] = w[S::D - 1];
+  if (S::F) reinterpret_cast<uint8_t*>(sl)[S::OF + lane] = (uint8_t)fl;
 }
 // Bits [o, o + nb) of a lane's field stream (o, nb compile-time after unrolling, nb <= 30):
 // one v_bfe_u32 inside a dword, v_alignbit_b32 + mask across two.
@@ -202,10 +210,10 @@ __device__ __forceinline__ uint32_t pk_bits(const uint32_t (&w)[D], int o, int n
 }
 
 // Row geometry of a packed arena, wave-uniform: the row's learner-0 slice (dwords from the
-// arena base), its tower and width.
+// arena base), its tower and width U_t.
 struct PackedRow {
   uint64_t base;
-  uint32_t t, B;
+  uint32_t t, U;
 };
 __device__ __forceinline__ PackedRow packed_row(uint64_t r, uint32_t C, uint32_t L, uint32_t logN,
                                                 const ArenaPack& ap) {
@@ -214,20 +222,23 @@ __device__ __forceinline__ PackedRow packed_row(uint64_t r, uint32_t C, uint32_t
   const uint32_t t = (uint32_t)(tp % L);
   const uint64_t g = tp / L;     // (ct, poly) index
   const uint32_t chunk = (uint32_t)(r & ((1u << lr) - 1));
-  const uint32_t B = ap.w[t];
-  const uint64_t base =
-      16ull * C * (((g * ap.sum + ap.pre[t]) << lr) + (uint64_t)chunk * B);
-  return {base, t, B};
+  const uint32_t U = ap.w[t];
+  const uint64_t base = 16ull * C * (((g * ap.sum + ap.pre[t]) << lr) + (uint64_t)chunk * U);
+  return {base, t, U};
 }
+// One instantiation per width class (a wave-uniform switch on U_t)
+#define SHELFI_PACK_WIDTHS(X) \
+  X(32) X(33) X(36) X(37) X(40) X(41) X(44) X(45) X(48) X(49) X(52) X(53) X(56) X(57) X(60)
 
 // One wave = one row: sum_c W_c x_c mod q_t over the row's C learner slices (carry-free limb sums
 // per group of 16 learners, as wavg_kernel), into r[8] (lane l's residues 2l + (j & 1) + 128 (j >> 1)).
-template <int B, int U>
+template <int UB, int UR>
 __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl, uint32_t C,
                                                 const uint32_t* __restrict__ wlt,
                                                 uint32_t wl_stride, const TowerConst& c, uint32_t lane,
                                                 uint64_t (&r)[8]) {
-  using S = PackShape<B>;
+  using S = PackShape<UB>;
+  constexpr int B = S::B;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = 0;
   for (uint32_t k0 = 0; k0 < C; k0 += kWavgMaxLearners) {
@@ -237,14 +248,16 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[j][i] = 0;
-#pragma unroll U
+#pragma unroll UR
     for (uint32_t k = k0; k < k1; ++k) {
-      uint32_t w[S::D];
-      pk_load<B>(sl + (uint64_t)k * S::SLICE, lane, w);
+      uint32_t w[S::D], fl;
+      pk_load<UB>(sl + (uint64_t)k * S::SLICE, lane, w, fl);
       const uint32_t w0 = wlt[k * wl_stride], w1 = wlt[k * wl_stride + 1];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint32_t x0 = pk_bits(w, j * B, 30), x1 = pk_bits(w, j * B + 30, B - 30);
+        const uint32_t x0 = pk_bits(w, j * B, 30);
+        uint32_t x1 = pk_bits(w, j * B + 30, B - 30);
+        if (S::F) x1 |= ((fl >> j) & 1u) << (B - 30);  // bit B of the residue (< 2^(B+1) <= 2^57)
         s[j][0] += (uint64_t)x0 * w0;
         s[j][1] += (uint64_t)x0 * w1;
         s[j][2] += (uint64_t)x1 * w0;
@@ -258,7 +271,7 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
 
 constexpr int kPackedWaves = 4;  // waves per block, one row each
 
-template <int U>
+template <int UR>
 __global__ __launch_bounds__(64 * kPackedWaves) void wavg_packed(const uint32_t* __restrict__ arena,
                                                                 const uint32_t* __restrict__ wl,
                                                                 uint32_t C, uint64_t rows, uint32_t L,
@@ -273,10 +286,10 @@ __global__ __launch_bounds__(64 * kPackedWaves) void wavg_packed(const uint32_t*
   const uint32_t* __restrict__ sl = arena + pr.base;
   const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
   uint64_t res[8];
-  switch (pr.B) {
-#define WPR(BB) \
-  case BB: wavg_packed_row<BB, U>(sl, C, wlt, 2 * L, c, lane, res); break;
-    WPR(32) WPR(36) WPR(40) WPR(44) WPR(48) WPR(52) WPR(56) WPR(60)
+  switch (pr.U) {
+#define WPR(UU) \
+  case UU: wavg_packed_row<UU, UR>(sl, C, wlt, 2 * L, c, lane, res); break;
+    SHELFI_PACK_WIDTHS(WPR)
 #undef WPR
     default:
 #pragma unroll
@@ -297,10 +310,11 @@ __global__ __launch_bounds__(64 * kPackedWaves) void wavg_packed(const uint32_t*
 
 // Upload of one learner's rows into its packed slices, with the canonical-residue check of
 // every residue (the limb sums above assume x < q_t; a refused slot is never aggregated).
-template <int B>
+template <int UB>
 __device__ __forceinline__ bool pack_row(const uint64_t* __restrict__ src, uint32_t* __restrict__ sl, uint64_t q,
                                          uint32_t lane) {
-  using S = PackShape<B>;
+  using S = PackShape<UB>;
+  constexpr int B = S::B;
   uint64_t x[8];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -309,19 +323,20 @@ __device__ __forceinline__ bool pack_row(const uint64_t* __restrict__ src, uint3
     x[2 * g + 1] = ((uint64_t)v.w << 32) | v.z;
   }
   bool bad = false;
-  uint32_t w[S::D];
+  uint32_t w[S::D], fl = 0;
 #pragma unroll
   for (int d = 0; d < S::D; ++d) w[d] = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     bad |= x[j] >= q;
     const uint64_t v = x[j] & ((1ull << B) - 1);
+    fl |= (uint32_t)((x[j] >> B) & 1) << j;  // kept only with a flag plane (else x >= 2^B > q: refused)
     const int o = j * B, i = o >> 5, s = o & 31;
     w[i] |= (uint32_t)(v << s);
     if (s + B > 32) w[i + 1] |= (uint32_t)(v >> (32 - s));
     if (s + B > 64) w[i + 2] |= (uint32_t)(v >> (64 - s));
   }
-  pk_store<B>(sl, lane, w);
+  pk_store<UB>(sl, lane, w, fl);
   return bad;
 }
 
@@ -329,18 +344,18 @@ __global__ __launch_bounds__(64 * kPackedWaves) void arena_pack_kernel(
     const uint64_t* __restrict__ src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner, uint32_t L,
     uint32_t logN, ArenaPack ap, const TowerConst* __restrict__ tcs, uint32_t* __restrict__ arena,
     uint32_t* __restrict__ bad) {
-  const uint64_t i = __builtin_amdgcn_readfirstlane((uint32_t)blockIdx.x * kPackedWaves + (threadIdx.x >> 6));
+  const uint64_t i = (uint64_t)blockIdx.x * kPackedWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (i >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   const PackedRow pr = packed_row(row0 + i, C, L, logN, ap);
   const uint64_t q = tcs[pr.t].q;
   const uint64_t* __restrict__ s = src + i * kArenaChunk;
-  uint32_t* __restrict__ sl = arena + pr.base + (uint64_t)learner * 16 * pr.B;
+  uint32_t* __restrict__ sl = arena + pr.base + (uint64_t)learner * 16 * pr.U;
   bool b = false;
-  switch (pr.B) {
-#define PKR(BB) \
-  case BB: b = pack_row<BB>(s, sl, q, lane); break;
-    PKR(32) PKR(36) PKR(40) PKR(44) PKR(48) PKR(52) PKR(56) PKR(60)
+  switch (pr.U) {
+#define PKR(UU) \
+  case UU: b = pack_row<UU>(s, sl, q, lane); break;
+    SHELFI_PACK_WIDTHS(PKR)
 #undef PKR
     default: b = true; break;
   }

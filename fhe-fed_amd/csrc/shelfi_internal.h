@@ -232,14 +232,15 @@ struct WavgArgs {
 };
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s);
 // Packed arena (round 3): the aggregator's resident layout.  Tower t's residues are
-// stored at B_t = 4 ceil(bitlength(q_t) / 4) bits (32 <= B_t <= 60) instead of 64: rows of 512
-// residues of one (ct, poly, tower) in natural order, each row holding the C learners' slices
-// side by side, a slice 16 B_t dwords (lane l of a wave owns residues 2l, 2l + 1 (+128 g, g < 4),
-// packed into B_t / 4 dwords stored as 16-byte / 8-byte / 4-byte planes, see kernels.hip).
+// stored at U_t bits instead of 64: U_t = bitlength(q_t) when that is 1 mod 4 (a field of U_t - 1
+// bits + the top bit in a flag plane), else 4 ceil(bitlength(q_t) / 4); at least 32, at most 60.
+// Rows of 512 residues of one (ct, poly, tower) in natural order, each row holding the C learners'
+// slices side by side, a slice 16 U_t dwords (lane l of a wave owns residues 2l, 2l + 1 (+128 g,
+// g < 4), packed into 16-byte / 8-byte / 4-byte field planes and a byte flag plane, see kernels.hip).
 struct ArenaPack {
-  uint32_t w[kMaxTowers];    // B_t
-  uint32_t pre[kMaxTowers];  // sum of B_t' for t' < t
-  uint32_t sum;              // sum of B_t
+  uint32_t w[kMaxTowers];    // U_t
+  uint32_t pre[kMaxTowers];  // sum of U_t' for t' < t
+  uint32_t sum;              // sum of U_t
 };
 ArenaPack arena_pack(const Params& p);                 // api.cpp
 uint64_t arena_ct_words(const Params& p, uint64_t C);  // uint64 words per ciphertext of C learners

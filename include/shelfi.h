@@ -200,9 +200,10 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
                     size_t K, uint64_t* out_dev, void* stream);
 /* Packed learner-interleaved arena: the aggregator's resident layout for C learners' K
  * ciphertexts.  Rows of 512 residues in [K][2][L][N] order; a row holds the C learners'
- * slices side by side, and every residue of tower t is packed to B_t = 4 ceil(bitlength(q_t)/4)
- * bits (>= 32; 60/52/52/52 at the reference's 2^15/L4: 216 of 256 bits per coefficient), so one
- * aggregation wave reads one contiguous C-slice region and the launch moves 16% fewer bytes
+ * slices side by side, and every residue of tower t is packed to U_t bits (bitlength(q_t) when
+ * that is 1 mod 4, else rounded up to a multiple of 4; >= 32): 60/53/52/53 at the reference's
+ * 2^15/L4, 218 of 256 bits per coefficient, so one aggregation wave reads one contiguous C-slice
+ * region and the launch moves 14% fewer bytes
  * (DESIGN.md §3).  The layout is opaque: size it with shelfi_arena_words() (uint64 words;
  * ciphertexts [k0, k1) of an arena start at word k0 * shelfi_arena_words(ctx, C, 1) and are
  * themselves an arena of k1 - k0 ciphertexts).  shelfi_dev_arena_put packs learner

@@ -168,15 +168,15 @@ def test_wavg_arena_bitexact(cfg2, C, K):
 
 
 @pytest.mark.parametrize("scale,first,depth,C,K", [
-    (52, 60, 1, 16, 2),   # 2^13-class chain, B = 60, 52 or 56 (a 53-bit prime)
-    (40, 60, 2, 9, 3),    # B = 60, 40, 40
-    (41, 57, 2, 3, 2),    # 57 / 41-bit towers: B = 60, 44, 44 (widths rounded up to 4)
-    (35, 47, 3, 18, 1),   # B = 48, 36, 36, 36; > 16 learners (two groups)
-    (30, 45, 1, 5, 2),    # 30-bit towers: B = 32 (the minimum width)
+    (52, 60, 1, 16, 2),   # 2^13-class chain: 60 and 53 bits (a 52-bit field + the flag plane)
+    (40, 60, 2, 9, 3),    # 60, 40/41 bits
+    (41, 57, 2, 3, 2),    # 57 / 41-bit towers: flag planes over 56- and 40-bit fields
+    (35, 47, 3, 18, 1),   # 48, 36 bits (rounded up to 4); > 16 learners (two groups)
+    (30, 45, 1, 5, 2),    # 45 bits (flag plane) and 30-bit towers at the 32-bit minimum
 ])
 def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C, K):
     """The packed arena at every width class its kernels carry: residues at 0, q-1
-    and random, device and host placement, whole-range and sub-range aggregation == oracle, at
+    (the top bit, for towers whose bitlength is 1 mod 4, lives in the flag plane) and random, device and host placement, whole-range and sub-range aggregation == oracle, at
     every learner unroll depth of wavg_packed."""
     ck = m.CKKS("ckks", 1024, scale, str(tmp_path) + os.sep, multDepth=depth, firstModBits=first,
                 seed=3, decodeNoise=False)
@@ -184,8 +184,9 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
     inf, q, psi, N, S, delta = _ctx_arrays(ck)
     L = len(q)
     words = ck._lib.shelfi_arena_words(ck._ctx, C, K)
-    B = [max(32, (int(x).bit_length() + 3) // 4 * 4) for x in q]
-    assert words == C * K * 2 * N * sum(B) // 64
+    bits = [int(x).bit_length() for x in q]
+    U = [32 if b <= 32 else (b if b % 4 == 1 else (b + 3) // 4 * 4) for b in bits]
+    assert words == C * K * 2 * N * sum(U) // 64
     rng = np.random.default_rng(scale * 100 + C)
     cts = []
     for c in range(C):
