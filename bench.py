@@ -692,6 +692,13 @@ def main():
                 "kernel": "wavg_packed" if args.layout == "arena" else "wavg_kernel",
                 "bytes_per_launch": bytes_per_launch,
                 "launch_ms_avg": round(kern_avg_ms, 4), "launch_ms_min": round(kern_ms[0], 4)}
+    if args.layout == "arena":
+        # the packed arena's widths and what the same launch amounts to in uint64
+        # residues (the rounds-1/2 arena's bytes): an effective rate, not a fraction of any peak
+        bits = [int(x).bit_length() for x in ck.info()["moduli"]]
+        roofline["packed_bits_per_coeff"] = sum(32 if b <= 32 else (b if b % 4 == 1 else (b + 3) // 4 * 4)
+                                                for b in bits)
+        roofline["uint64_equivalent_GBps"] = round((C_loc + 1) * K_loc * 2 * L * N * 8 / (kern_avg_ms * 1e-3) / 1e9, 1)
     if untuned is not None:
         roofline["untuned_output"] = {"launch_ms_avg": round(untuned, 4),
                                       "frac": round(bytes_per_launch / (untuned * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
