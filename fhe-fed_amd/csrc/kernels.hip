@@ -1609,8 +1609,11 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 // indices i = i0 + (16/R) r of group h = c mod N/16 (i0 = c div N/16; LOGR = 4: the whole group).
 // Same samples and rounding as enc_prep_kernel, then for every tower the columns stages of v,
 // m + e0 and e1 and the lazy stores into pbuf that the blocks pass reads.
-template <int LOGR, bool TAB>
-__global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
+// WV: waves per SIMD the register budget is cut for.  TWL: the tower's column-stage twiddles are
+// staged in LDS per tower instead of scalar-loaded (the scalar loads of 15 {w, w'} pairs per polynomial
+// were spilling SGPRs).
+template <int LOGR, bool TAB, int WV = 4, bool TWL = false>
+__global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
                                                       double delta, const uint64_t* __restrict__ cdt,
                                                       int T, Key8 key, uint64_t g0,
@@ -1624,6 +1627,8 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
   static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
   __shared__ uint32_t thi[64], tlo[64];
   __shared__ uint64_t tabs[kEncTab];  // this tower's DeviceTables::enc_tab slice
+  __shared__ ulonglong2 twl[1 << LOGR];  // TWL: this tower's {w, w'} for column stages (index m + i)
+  static_assert(!TWL || TAB, "LDS twiddles ride on the table path's per-tower barrier");
   load_cdt32(cdt, T, thi, tlo);
   __syncthreads();
   const uint32_t N = 1u << logN, BLK = N >> LOGR, N16 = N >> 4, V0 = N >> 6;
@@ -1652,7 +1657,15 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
       const int m = 1 << s, tr = R >> (s + 1);
 #pragma unroll
       for (int i = 0; i < m; ++i) {
-        const uint64_t W = w[m + i], Wp = wp[m + i];
+        uint64_t W, Wp;
+        if constexpr (TWL) {
+          const ulonglong2 T2 = twl[m + i];
+          W = T2.x;
+          Wp = T2.y;
+        } else {
+          W = w[m + i];
+          Wp = wp[m + i];
+        }
 #pragma unroll
         for (int jj = 0; jj < tr; ++jj) {
           const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
@@ -1725,6 +1738,10 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
         }
         __syncthreads();  // the previous tower's lookups are done (every thread runs every tower)
         for (uint32_t i = threadIdx.x; i < (uint32_t)kEncTab; i += 256) tabs[i] = enc_tab[(size_t)t * kEncTab + i];
+        if constexpr (TWL) {
+          if (threadIdx.x < (uint32_t)R)
+            twl[threadIdx.x] = make_ulonglong2(tw[((uint64_t)t << logN) + threadIdx.x], twp[((uint64_t)t << logN) + threadIdx.x]);
+        }
         __syncthreads();
         {
           uint64_t x[R];
@@ -1784,6 +1801,12 @@ __global__ __launch_bounds__(256, 4) void enc_cols_fused(const double2* __restri
   const auto message_poly = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
     for (uint32_t t = ta; t < tb; ++t) {
+      if constexpr (TWL) {
+        __syncthreads();  // every thread runs every tower
+        if (threadIdx.x < (uint32_t)R)
+          twl[threadIdx.x] = make_ulonglong2(tw[((uint64_t)t << logN) + threadIdx.x], twp[((uint64_t)t << logN) + threadIdx.x]);
+        __syncthreads();
+      }
       const TowerConst cst = tcs[t];
       uint64_t x[R];
       if (cst.red_ok) {
@@ -1867,14 +1890,20 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t nb = (K << (p.logN - nlogR)) / 256;
     const char* tabenv = getenv("SHELFI_ENC_TAB");  // A/B probe switch (read per launch)
     const bool tab = !(tabenv && *tabenv == '0');
-#define ENC_COLS(LR, TB)                                                                                        \
-  hipLaunchKernelGGL((enc_cols_fused<LR, TB>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L, \
+    // LDS column twiddles at 3 waves/SIMD (no SGPR / VGPR spills): enc_cols_fused 578 -> 534 us per
+    // 714 cts (probes/r03_enc_cols_twl.txt); SHELFI_ENC_TWL=0 keeps the scalar-loaded twiddles
+    const char* twlenv = getenv("SHELFI_ENC_TWL");  // A/B probe switch (read per launch)
+    const bool twl = !(twlenv && *twlenv == '0');
+#define ENC_COLS(LR, TB, ...)                                                                                   \
+  hipLaunchKernelGGL((enc_cols_fused<LR, TB, ##__VA_ARGS__>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L, \
                      p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split,  \
                      dt.enc_tab)
     if (nlogR == 3 && tab)
       ENC_COLS(3, true);
     else if (nlogR == 3)
       ENC_COLS(3, false);
+    else if (tab && twl)  // 164 VGPRs without spills at 3 waves (4 would spill 36)
+      ENC_COLS(4, true, 3, true);
     else if (tab)
       ENC_COLS(4, true);
     else
