@@ -98,9 +98,17 @@ class Arena:
         if device is None:
             device = "cuda:%d" % inf["device"]
         lib = _lib.load()
+        # the packed layout is sized by the context's moduli: an arena belongs to this parameter
+        # generation (loadCryptoParams / genCryptoContextAndKeyGen start a new one)
+        self._gen = getattr(ckks, "_params_gen", 0)
         self.ct_words = lib.shelfi_arena_words(ckks._ctx, self.C, 1)  # packed words per ciphertext
         words = lib.shelfi_arena_words(ckks._ctx, self.C, self.K)
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
+
+    def _check_gen(self):
+        if getattr(self.ckks, "_params_gen", 0) != self._gen:
+            raise ValueError("the context's parameters or keys were reloaded since this arena was "
+                             "made: its packed layout no longer matches; make a new Arena")
 
     def put(self, learner: int, ct):
         """Place learner `learner`'s batch: a [K][2][L][N] CUDA tensor, or its upload as it
@@ -108,6 +116,7 @@ class Arena:
         header is checked against the context (parameters, key, length, K) before any copy;
         every put then checks that each placed residue is < q_t, and a refused slot keeps
         wavg() failing until a valid put replaces it (shelfi_dev_arena_put[_blob])."""
+        self._check_gen()
         if isinstance(ct, (bytes, bytearray, memoryview)):
             import numpy as np
 
@@ -127,6 +136,7 @@ class Arena:
     def wavg(self, weights: Sequence[float], out=None, k0: int = 0, k1: int | None = None):
         """Aggregate ciphertexts [k0, k1) of every learner into out[:k1-k0]."""
         torch = _torch()
+        self._check_gen()
         if len(weights) != self.C:
             raise ValueError("need one weight per learner")
         k1 = self.K if k1 is None else int(k1)
@@ -153,6 +163,7 @@ class Arena:
         fastest released; buffers in `include` (already allocated [K][2][L][N] tensors) are
         candidates too, ahead of the new ones.  Returns (buffer, per-candidate ms)."""
         torch = _torch()
+        self._check_gen()
         cands = list(include)
         for c in cands:
             _check_ct(c, self.ckks, self.K)

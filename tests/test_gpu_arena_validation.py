@@ -217,3 +217,25 @@ def test_device_checks_after_reloading_other_parameters(tmp_path):
         D.wavg(ck, [old], [1.0])
     new = D.encrypt(ck, torch.zeros(100, dtype=torch.float64, device="cuda"))
     assert tuple(new.shape) == (1, 2, 2, 8192)
+
+
+def test_arena_refuses_use_after_params_reload(tmp_path):
+    """The packed arena is sized by the context's moduli (shelfi_arena_words): after the context
+    reloads its parameters (loadCryptoParams / genCryptoContextAndKeyGen, here 2^15/L4 -> the
+    reference's 2^13/L2 files) the old arena's put and wavg raise instead of packing against the
+    new moduli."""
+    d = str(tmp_path) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    ar = D.Arena(ck, 2, 1)
+    x = torch.zeros((1, 2, 4, 32768), dtype=torch.int64, device="cuda")
+    ar.put(0, x)
+    ar.put(1, x)
+    ar.wavg([0.5, 0.5])
+    ck.cryptodir = PALISADE_DIR
+    ck.loadCryptoParams()
+    assert ck.info()["ring_dim"] == 8192
+    with pytest.raises(ValueError):
+        ar.put(0, x)
+    with pytest.raises(ValueError):
+        ar.wavg([0.5, 0.5])
