@@ -699,6 +699,8 @@ def main():
         roofline["packed_bits_per_coeff"] = sum(32 if b <= 32 else (b if b % 4 == 1 else (b + 3) // 4 * 4)
                                                 for b in bits)
         roofline["uint64_equivalent_GBps"] = round((C_loc + 1) * K_loc * 2 * L * N * 8 / (kern_avg_ms * 1e-3) / 1e9, 1)
+        roofline["bytes_basis"] = ("achieved/frac count the packed arena's bytes (U_t bits per residue) + the uint64 "
+                                   "aggregate; uint64_equivalent_GBps is the same launch in uint64 residues (no peak)")
     if untuned is not None:
         roofline["untuned_output"] = {"launch_ms_avg": round(untuned, 4),
                                       "frac": round(bytes_per_launch / (untuned * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
