@@ -1542,9 +1542,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
 // thread = column c of ciphertext k, coefficients j = c + BLK r.  For every tower the
 // three polynomials v, m + e0, e1 are reduced, run through the first LOGR stages and
 // stored lazily ([0, 8q)) into pbuf [K][3][L][N] for ntt_fwd_blocks_enc.
-// TWL (LOGR >= 5, where 31-63 {w, w'} pairs held in SGPRs spilled 80-208 of them): the tower's
-// column-stage twiddles are staged in LDS per tower (every thread of the grid is live: no early exit).
-template <int LOGR, int POLY, bool TWL = false>
+template <int LOGR, int POLY>
 __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restrict__ me0,
                                                         const int16_t* __restrict__ ve, uint64_t K,
                                                         uint32_t logN, uint32_t L,
@@ -1569,12 +1567,6 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
     const uint64_t q = cst.q;
     const uint64_t* __restrict__ w = tw + ((uint64_t)t << logN);
     const uint64_t* __restrict__ wp = twp + ((uint64_t)t << logN);
-    __shared__ ulonglong2 twl[TWL ? R : 1];
-    if constexpr (TWL) {
-      __syncthreads();  // the previous tower's reads are done
-      for (uint32_t i = threadIdx.x; i < (uint32_t)R; i += 256) twl[i] = make_ulonglong2(w[i], wp[i]);
-      __syncthreads();
-    }
     uint64_t x[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1592,15 +1584,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
       const int m = 1 << s, tr = R >> (s + 1);
 #pragma unroll
       for (int i = 0; i < m; ++i) {
-        uint64_t W, Wp;
-        if constexpr (TWL) {
-          const ulonglong2 T2 = twl[m + i];
-          W = T2.x;
-          Wp = T2.y;
-        } else {
-          W = w[m + i];
-          Wp = wp[m + i];
-        }
+        const uint64_t W = w[m + i], Wp = wp[m + i];
 #pragma unroll
         for (int jj = 0; jj < tr; ++jj) {
           const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
@@ -1937,26 +1921,20 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   // blocks pass fused with the public-key combine writes the ciphertexts
   if (nlogR > 0 && !fused) {
     const uint64_t nb = K * ((p.N >> nlogR) / 256);
-    const char* twlenv = getenv("SHELFI_ENC_TWL");  // A/B probe switch (read per launch)
-    const bool twl = !(twlenv && *twlenv == '0');
-#define COLS_ENC(LR, TW)                                                                            \
-  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 0, TW>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
-                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                             \
-  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 1, TW>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
-                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                             \
-  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 2, TW>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+#define COLS_ENC(LR)                                                                          \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 0>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                       \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 1>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
+                     p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);                       \
+  hipLaunchKernelGGL((ntt_fwd_cols_enc<LR, 2>), dim3((uint32_t)nb), dim3(256), 0, s, me0, ve, K,  \
                      p.logN, p.L, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf);
     switch (nlogR) {
-      case 1: COLS_ENC(1, false) break;
-      case 2: COLS_ENC(2, false) break;
-      case 3: COLS_ENC(3, false) break;
-      case 4: COLS_ENC(4, false) break;
-      case 5:
-        if (twl) { COLS_ENC(5, true) } else { COLS_ENC(5, false) }
-        break;
-      case 6:
-        if (twl) { COLS_ENC(6, true) } else { COLS_ENC(6, false) }
-        break;
+      case 1: COLS_ENC(1) break;
+      case 2: COLS_ENC(2) break;
+      case 3: COLS_ENC(3) break;
+      case 4: COLS_ENC(4) break;
+      case 5: COLS_ENC(5) break;
+      case 6: COLS_ENC(6) break;
       default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};
     }
 #undef COLS_ENC
