@@ -1,11 +1,11 @@
 """BASELINE configs at their full sizes on the HIP path, bit-exact vs the oracle
 (oracle/ckks_oracle.c or_wavg_fast, Shoup form, 16 threads), through the kernels the
 bench times:
-  * cfg3's per-GPU shard (16 learners x 714 ciphertexts, 2^15 / L4, 22.3 GiB) through the
-    arena kernel bench.py times (wavg_kernel<true>, with output placement tuning) and
-    the pointer-list kernel (wavg_kernel<false>);
-  * cfg3's ciphertext-sharded shape at N = 8 (128 learners x 89 ciphertexts) through
-    the single-pass many-learner kernel (wavg_arena_many);
+  * cfg3's per-GPU shard (16 learners x 714 ciphertexts, 2^15 / L4, 22.3 GiB of uint64
+    residues, 19.0 GiB packed) through the packed-arena kernel bench.py times (wavg_packed,
+    with output placement tuning) and the pointer-list kernel (wavg_kernel);
+  * cfg3's ciphertext-sharded shape at N = 8 (128 learners x 89 ciphertexts) through one
+    pass of wavg_packed (8 groups of 16 learners folded into a running sum);
   * cfg4 (16 learners x 32 ciphertexts, 2^16 / L6);
   * cfg5 (64 learners of 10 % of ResNet-50 -> 156 ciphertexts; 8 of them here): the
     masked selection of attack/masking/masking.py:15-21 packed per learner, encrypted,
@@ -79,7 +79,7 @@ def test_cfg3_shard_full_size_arena_and_pointer_kernels(cfg2):
 
 def test_cfg3_ciphertext_sharded_shape_many_learners(cfg2):
     """One rank of the N = 8 ciphertext-sharded step: 128 learners x 89 ciphertexts in
-    one pass of wavg_arena_many, weights 1/128 and Dirichlet."""
+    one pass of wavg_packed, weights 1/128 and Dirichlet."""
     ck, q, N, delta = cfg2
     L, C, K = len(q), 128, 89
     cts = _random_cts(C, K, L, N, q, 77)

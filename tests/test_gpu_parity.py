@@ -138,7 +138,7 @@ def test_wavg_device_bitexact(cfg, C, K, request):
 
 @pytest.mark.parametrize("C,K", [(16, 3), (20, 2), (1, 1), (5, 4), (40, 1), (128, 1)])
 def test_wavg_arena_bitexact(cfg2, C, K):
-    """Learner-interleaved arena (device and host-blob placement) == oracle."""
+    """Packed learner-interleaved arena (device and host-blob placement) == oracle."""
     inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
     L = len(q)
     rng = np.random.default_rng(C * 7 + K)
@@ -283,7 +283,7 @@ def test_arena_packed_layout_bytes(cfg1):
 
 
 def test_wavg_arena_many_learners_ranges_and_weights(cfg2):
-    """> 16 learners in one pass (wavg_arena_many): sub-ranges of the arena, alternating
+    """> 16 learners in one pass of wavg_packed: sub-ranges of the arena, alternating
     weight vectors (the device weight ring), residues at q-1 with weight 1.0."""
     inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
     L, C, K = len(q), 48, 3
