@@ -1,4 +1,6 @@
-"""A/B of the arena wavg kernel's rows per block (SHELFI_WAVG_ROWS=1|2, read per launch) on
+"""(Round-3 probe of the uint64 arena kernel, before the packed arena: since then the arena runs
+wavg_packed, which ignores SHELFI_WAVG_ROWS; tools/wavg_packed_ab.py is its A/B tool.)
+A/B of the arena wavg kernel's rows per block (SHELFI_WAVG_ROWS=1|2, read per launch) on
 the BASELINE shapes, in one process on one box: launches alternate between the variants in
 rounds, HIP events around each round.  Prints achieved TB/s (algorithmic bytes
 (C+1) K 2 L N 8 per launch) per shape and variant, median over rounds.
