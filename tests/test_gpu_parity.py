@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import arena_layout as AL
 import palisade_fixture as P
 from conftest import PALISADE_DIR
 
@@ -216,47 +217,6 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
         assert np.array_equal(got.cpu().numpy().view(np.uint64), O.wavg([c[1:] for c in cts], w, q, delta))
 
 
-def _pack_arena_np(cts, q, N):
-    """numpy/int restatement of the packed arena's documented layout (kernels.hip
-    'packed arena'): rows of 512 residues in [K][2][L][N] order, the C learners' slices side by
-    side, a slice 16 U_t dwords; lane l's residues 2l + (j & 1) + 128 (j >> 1) as B_t-bit fields in
-    16-, 8- and 4-byte planes, bit B_t in a byte flag plane when U_t is 1 mod 4."""
-    C, (K, _, L, _) = len(cts), cts[0].shape
-    U = [32 if int(x).bit_length() <= 32 else (int(x).bit_length() if int(x).bit_length() % 4 == 1
-                                               else (int(x).bit_length() + 3) // 4 * 4) for x in q]
-    out = []
-    for k in range(K):
-        for p in range(2):
-            for t in range(L):
-                Bt, F = U[t] & ~3, U[t] & 1
-                D = Bt // 4
-                N4, H2, H1 = D // 4, 1 if D % 4 >= 2 else 0, D & 1
-                O2, O1 = N4 * 256, N4 * 256 + H2 * 128
-                for ch in range(N // 512):
-                    for c in range(C):
-                        row = cts[c][k, p, t, ch * 512:(ch + 1) * 512]
-                        sl = np.zeros(16 * U[t], np.uint32)
-                        flags = np.zeros(64, np.uint8)
-                        for lane in range(64):
-                            acc, fl = 0, 0
-                            for j in range(8):
-                                x = int(row[2 * lane + (j & 1) + 128 * (j >> 1)])
-                                acc |= (x & ((1 << Bt) - 1)) << (j * Bt)
-                                fl |= ((x >> Bt) & 1) << j
-                            d = [(acc >> (32 * i)) & 0xFFFFFFFF for i in range(D)]
-                            for pl in range(N4):
-                                sl[pl * 256 + 4 * lane:pl * 256 + 4 * lane + 4] = d[4 * pl:4 * pl + 4]
-                            if H2:
-                                sl[O2 + 2 * lane:O2 + 2 * lane + 2] = d[4 * N4:4 * N4 + 2]
-                            if H1:
-                                sl[O1 + lane] = d[D - 1]
-                            flags[lane] = fl
-                        if F:
-                            sl.view(np.uint8)[64 * Bt:64 * Bt + 64] = flags
-                        out.append(sl)
-    return np.concatenate(out)
-
-
 def test_arena_packed_layout_bytes(cfg1):
     """The arena's words equal the documented packed layout restated in numpy (2^13/L2: a 60-bit
     field tower and a 53-bit tower stored as a 52-bit field + flag plane), residues at q-1, 2^B and
@@ -279,7 +239,7 @@ def test_arena_packed_layout_bytes(cfg1):
     ar.put(1, m.blob_pack(cfg1, cts[1]))
     torch.cuda.synchronize()
     got = ar.buf.cpu().numpy().view(np.uint32)
-    assert np.array_equal(got, _pack_arena_np(cts, q, N))
+    assert np.array_equal(got, AL.pack_arena(cts, q, N))
 
 
 def test_wavg_arena_many_learners_ranges_and_weights(cfg2):

@@ -293,3 +293,41 @@ def test_distributed_combine_gloo_world2(mode):
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_packed_arena_layout_restatement_round_trips():
+    """The numpy restatement of the packed arena (tests/arena_layout.py, the layout the GPU test
+    pins the device words against) is lossless at every width class: residues at 0, q-1, 2^B
+    (the flag-plane bit) and random, for 60/53/52-bit towers (the reference's 2^13 and 2^15
+    chains), 57/41 (flag planes over 56- and 40-bit fields), 48/36 and 30-bit towers (32)."""
+    import numpy as np
+
+    import arena_layout as AL
+
+    chains = [
+        [0xFFFFFFFFFFFC001, 0x10000000060001],            # 2^13 / L2: 60, 53 bits
+        [(1 << 56) + 0x1D0001, (1 << 40) + 0x4001],       # 57, 41 bits (values need not be prime here)
+        [(1 << 47) + 0x1001, (1 << 35) + 0x2001],         # 48, 36
+        [(1 << 44) + 0x8001, (1 << 29) + 0x2001],         # 45, 30 -> 32
+    ]
+    rng = np.random.default_rng(4)
+    N, K, C = 1024, 1, 2
+    for q in chains:
+        L = len(q)
+        U = AL.widths(q)
+        cts = []
+        for c in range(C):
+            a = np.empty((K, 2, L, N), np.uint64)
+            for t in range(L):
+                a[:, :, t, :] = rng.integers(0, q[t], (K, 2, N), dtype=np.uint64)
+                a[:, :, t, 3:30:3] = q[t] - 1
+                a[:, 1, t, 50:60] = 0
+                Bt = U[t] & ~3
+                if U[t] & 1:
+                    a[:, 0, t, 70:90] = 1 << Bt
+            cts.append(a)
+        words = AL.pack_arena(cts, q, N)
+        assert words.size == C * K * 2 * N * sum(U) // 32
+        back = AL.unpack_arena(words, C, K, L, N, q)
+        for a, b in zip(cts, back):
+            assert np.array_equal(a, b)
