@@ -1451,6 +1451,16 @@ static void arena_place(shelfi_ctx* ctx, size_t K, size_t learner, size_t C, uin
                     "marked refused until a valid upload replaces it)"};
   }
 }
+// How host uploads reach the device: a contiguous run (a library blob's payload, a host batch) as one
+// hipMemcpyAsync from the caller's pageable memory (54 GB/s for a 1.5 GB upload), the 2 L tower runs
+// of 256 KiB per ciphertext of a PALISADE archive through the bytes API's pinned staging ring (49 vs
+// 18.5 GB/s as separate copies; probes/r03_arena_put.txt).  SHELFI_ARENA_STAGER=0|1 forces one (A/B
+// probe switch, read per call).
+static bool arena_use_stager(size_t pieces, size_t bytes) {
+  const char* e = getenv("SHELFI_ARENA_STAGER");
+  if (e && (*e == '0' || *e == '1')) return *e == '1';
+  return pieces > 1 && bytes / pieces < (4u << 20);
+}
 // Host uploads are staged through the scratch in pieces of about 64 MiB.
 static size_t arena_stage_cts(const Params& p) {
   return std::max<size_t>(1, (64ull << 20) / (2ull * p.L * p.N * 8));
@@ -1516,11 +1526,19 @@ int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size
       });
       return;
     }
+    // host batches go through the pinned staging ring (the bytes API's copy pool)
+    StageRun sr(stager(ctx));
     arena_place(ctx, K, learner, C, arena_dev, s, arena_stage_cts(p), true, [&](size_t k0, size_t kn, uint64_t* dst) {
-      SHELFI_HIP(hipMemcpyAsync(dst, (const uint64_t*)src + k0 * ct_words, kn * ct_words * 8,
-                                hipMemcpyHostToDevice, s));
+      if (!arena_use_stager(1, kn * ct_words * 8)) {
+        SHELFI_HIP(hipMemcpyAsync(dst, (const uint64_t*)src + k0 * ct_words, kn * ct_words * 8,
+                                  hipMemcpyHostToDevice, s));
+      } else {
+        const HostPiece pc{(uint8_t*)((const uint64_t*)src + k0 * ct_words), kn * ct_words * 8};
+        sr.s.h2dv(dst, &pc, 1, s);
+      }
       return (const uint64_t*)dst;
     });
+    sr.finish();
   });
 }
 
@@ -1539,16 +1557,22 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
     const Params& p = ctx->p;
     hipStream_t s = (hipStream_t)stream;
     std::vector<HostPiece> pcs;
+    StageRun sr(stager(ctx));
     arena_place(ctx, K, learner, C, arena_dev, s, arena_stage_cts(p), true, [&](size_t k0, size_t kn, uint64_t* dst) {
       // a blob: one payload run; an archive: 2 L tower runs per ciphertext
       v.pieces(k0, kn, p, pcs);
-      uint8_t* d = (uint8_t*)dst;
-      for (const HostPiece& pc : pcs) {
-        SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, s));
-        d += pc.n;
+      if (arena_use_stager(pcs.size(), kn * 2ull * p.L * p.N * 8)) {
+        sr.s.h2dv(dst, pcs.data(), pcs.size(), s);  // pinned staging ring, gathered in order
+      } else {
+        uint8_t* d = (uint8_t*)dst;
+        for (const HostPiece& pc : pcs) {
+          SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, s));
+          d += pc.n;
+        }
       }
       return (const uint64_t*)dst;
     });
+    sr.finish();
   });
 }
 
