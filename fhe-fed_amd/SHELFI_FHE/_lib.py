@@ -115,6 +115,7 @@ SIGNATURES = {
     "shelfi_blob_pack": (C.c_int, [C.c_void_p, u64p, C.c_uint64, C.c_uint32, C.c_double,
                                    C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "shelfi_blob_header_bytes": (C.c_size_t, []),
+    "shelfi_blob_unpack": (C.c_int, [C.c_void_p, u8p, C.c_size_t, u64p]),
     "shelfi_dev_wavg": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), f32p, C.c_size_t, C.c_size_t,
                                   C.c_void_p, C.c_void_p]),
     "shelfi_arena_words": (C.c_size_t, [C.c_void_p, C.c_size_t, C.c_size_t]),

@@ -62,20 +62,34 @@ static BlobHeader parse_blob(const uint8_t* blob, size_t len, const shelfi_ctx* 
   if (!blob || len < sizeof(BlobHeader)) throw Error{SHELFI_ERR_FORMAT, "ciphertext blob too short"};
   BlobHeader h;
   std::memcpy(&h, blob, sizeof(h));
-  if (std::memcmp(h.magic, "SHCT", 4) != 0 || h.version != 1 || h.header_bytes != 64)
+  // version 1: uint64 residues [K][2][L][N]; version 2: the packed wire payload (the arena's slice
+  // format with C = 1, U_t bits per residue: DESIGN.md §3, §5.3)
+  if (std::memcmp(h.magic, "SHCT", 4) != 0 || (h.version != 1 && h.version != 2) || h.header_bytes != 64)
     throw Error{SHELFI_ERR_FORMAT, "not a SHELFI ciphertext blob (bad magic/version)"};
   if (h.L == 0 || h.L > kMaxTowers || h.logN < 10 || h.logN > 17)
     throw Error{SHELFI_ERR_FORMAT, "corrupt ciphertext blob header"};
-  // K comes from an untrusted header: bound it by the payload before multiplying, so a
-  // forged K whose K * ct_bytes wraps mod 2^64 cannot pass the length check.
-  const uint64_t ct_bytes = 2ull * h.L * (8ull << h.logN);
-  if (h.K > (len - sizeof(BlobHeader)) / ct_bytes ||
-      len != sizeof(BlobHeader) + h.K * ct_bytes)
-    throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
   if (ctx) {
     if (h.logN != ctx->p.logN || h.L != ctx->p.L || h.params_id != ctx->params_id)
       throw Error{SHELFI_ERR_FORMAT, "ciphertext was produced under different crypto parameters"};
   }
+  const uint64_t payload = len - sizeof(BlobHeader);
+  if (h.version == 2 && !ctx) {
+    // without a context the packed widths are unknown: a ciphertext is 2 (N / 512) rows of 64 U
+    // bytes for some 32 L <= U <= 60 L
+    const uint64_t unit = 2ull * (1ull << (h.logN - 9)) * 64;
+    bool ok = h.K ? payload % h.K == 0 : payload == 0;
+    if (ok && h.K) {
+      const uint64_t per = payload / h.K;
+      ok = per % unit == 0 && per / unit >= 32ull * h.L && per / unit <= 60ull * h.L;
+    }
+    if (!ok) throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
+    return h;
+  }
+  // K comes from an untrusted header: bound it by the payload before multiplying, so a
+  // forged K whose K * ct_bytes wraps mod 2^64 cannot pass the length check.
+  const uint64_t ct_bytes = h.version == 1 ? 2ull * h.L * (8ull << h.logN) : arena_ct_words(ctx->p, 1) * 8;
+  if (h.K > payload / ct_bytes || len != sizeof(BlobHeader) + h.K * ct_bytes)
+    throw Error{SHELFI_ERR_FORMAT, "ciphertext blob length does not match header"};
   return h;
 }
 
@@ -793,9 +807,25 @@ static BlobHeader make_header(const shelfi_ctx* ctx, uint64_t K, uint32_t depth,
 // Where the residues of a bytes-API ciphertext batch live in host memory: a library
 // blob (one contiguous payload) or a PALISADE archive (2*L tower runs per ciphertext,
 // palisade_codec.h).  Both map onto the device layout [K][2][L][N].
+// Packed wire payload sizes (version-2 blobs): bytes of one (ct, poly) group of the first Lu towers.
+static uint64_t packed_poly_bytes(const Params& p, uint32_t Lu) {
+  const ArenaPack ap = arena_pack(p);
+  uint64_t u = 0;
+  for (uint32_t t = 0; t < Lu; ++t) u += ap.w[t];
+  return (uint64_t)(p.N / kArenaChunk) * 64 * u;
+}
+// The widths of the first Lu towers (the buffers a prefix upload unpacks)
+static ArenaPack arena_pack_prefix(const Params& p, uint32_t Lu) {
+  Params q = p;
+  q.L = Lu;
+  return arena_pack(q);
+}
+
 struct CtLayout {
   uint8_t* base = nullptr;
   bool pal = false;
+  bool packed = false;  // a version-2 (packed) library blob
+  int fmt() const { return pal ? 1 : packed ? 2 : 0; }  // shelfi_set_wire_format's numbering
   uint64_t K = 0;
   uint32_t depth = 0;
   uint64_t level = 0;
@@ -807,6 +837,17 @@ struct CtLayout {
     out.clear();
     if (!Lu) Lu = p.L;
     const size_t poly_bytes = (size_t)p.L * p.N * 8, ct_bytes = 2 * poly_bytes;
+    if (packed) {  // (ct, poly) groups of packed rows; a tower prefix is a prefix of each group
+      const uint64_t pg = packed_poly_bytes(p, p.L);
+      if (Lu == p.L) {
+        out.push_back(HostPiece{base + sizeof(BlobHeader) + k0 * 2 * pg, kn * 2 * pg});
+        return;
+      }
+      const uint64_t pl = packed_poly_bytes(p, Lu);
+      for (uint64_t i = 2 * k0; i < 2 * (k0 + kn); ++i)
+        out.push_back(HostPiece{base + sizeof(BlobHeader) + i * pg, (size_t)pl});
+      return;
+    }
     if (!pal) {
       if (Lu == p.L) {
         out.push_back(HostPiece{base + sizeof(BlobHeader) + k0 * ct_bytes, kn * ct_bytes});
@@ -846,6 +887,7 @@ static CtLayout open_cts(const shelfi_ctx* ctx, const uint8_t* b, size_t len) {
     return v;
   }
   BlobHeader h = parse_blob(b, len, ctx);
+  v.packed = h.version == 2;
   v.K = h.K;
   v.depth = h.depth;
   v.level = h.level;
@@ -857,11 +899,13 @@ static CtLayout open_cts(const shelfi_ctx* ctx, const uint8_t* b, size_t len) {
 
 // Size of (and, with buf, the header / framing of) an output batch in the ctx's
 // format; returns its layout.
-static CtLayout make_output(const shelfi_ctx* ctx, bool pal, uint64_t K, uint32_t depth,
+static CtLayout make_output(const shelfi_ctx* ctx, int fmt, uint64_t K, uint32_t depth,
                             uint64_t level, double scale, uint8_t* buf, size_t* total) {
+  const bool pal = fmt == 1;
   CtLayout v;
   v.base = buf;
   v.pal = pal;
+  v.packed = fmt == 2;
   v.K = K;
   v.depth = depth;
   v.level = level;
@@ -875,9 +919,10 @@ static CtLayout make_output(const shelfi_ctx* ctx, bool pal, uint64_t K, uint32_
                             4, true, true, buf, total);
     return v;
   }
-  *total = sizeof(BlobHeader) + K * 2ull * p.L * p.N * 8;
+  *total = sizeof(BlobHeader) + K * (v.packed ? 2 * packed_poly_bytes(p, p.L) : 2ull * p.L * p.N * 8);
   if (buf) {
-    const BlobHeader h = make_header(ctx, K, depth, scale);
+    BlobHeader h = make_header(ctx, K, depth, scale);
+    if (v.packed) h.version = 2;
     std::memcpy(buf, &h, sizeof(h));
   }
   return v;
@@ -968,9 +1013,13 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
   uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
   kc = std::min<uint64_t>(kc, K);
   const size_t xin = kc * p.batch * 8, cto = kc * ct_bytes;
-  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (xin + cto));
+  // packed wire output: the chunk is packed on the device (U_t bits per residue) before its D2H
+  const size_t pko = dst.packed ? kc * 2 * packed_poly_bytes(p, p.L) : 0;
+  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (xin + cto + pko));
   uint8_t* xb[2] = {io, io + xin};
   uint8_t* cb[2] = {io + 2 * xin, io + 2 * xin + cto};
+  uint8_t* pb[2] = {io + 2 * (xin + cto), io + 2 * (xin + cto) + pko};
+  const ArenaPack ap = arena_pack(p);
   void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc));
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
@@ -988,10 +1037,13 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
     if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));  // ct buffer drained
     launch_encrypt(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
                    g0 + k0, ctx->dev_flag, pp.b);
+    if (dst.packed)  // canonical residues: the residue check cannot fire
+      launch_blob_pack((const uint64_t*)cb[b], kn, p.L, p.logN, ap, ctx->dt.tc, (uint32_t*)pb[b],
+                       ctx->dev_flag + 5, pp.b);
     SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
     SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
     dst.pieces(k0, kn, p, pcs);
-    sr.s.d2hv(pcs.data(), pcs.size(), cb[b], pp.c);
+    sr.s.d2hv(pcs.data(), pcs.size(), dst.packed ? pb[b] : cb[b], pp.c);
     SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
     sr.s.poll();
   }
@@ -1015,16 +1067,16 @@ int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out
     const Params& p = ctx->p;
     const uint64_t K = (n + p.batch - 1) / p.batch;  // ckks.cpp:65
     size_t total = 0;
-    make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, nullptr, &total);
+    make_output(ctx, ctx->wire, K, 1, 0, p.delta, nullptr, &total);
     *out_len = total;
     if (!out) return;
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     advise_huge(out, total);
     // residues first (the parallel drains first-touch the fresh pages), framing after
-    CtLayout dst = make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, nullptr, &total);
+    CtLayout dst = make_output(ctx, ctx->wire, K, 1, 0, p.delta, nullptr, &total);
     dst.base = out;
     if (K) encrypt_bytes_pipeline(ctx, x, n, K, dst);
-    make_output(ctx, ctx->wire == 1, K, 1, 0, p.delta, out, &total);
+    make_output(ctx, ctx->wire, K, 1, 0, p.delta, out, &total);
   });
 }
 
@@ -1063,6 +1115,8 @@ static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* c
     const CtLayout& h0 = in.front();
     if (h.pal != h0.pal)
       throw Error{SHELFI_ERR_FORMAT, "learners mix PALISADE archives and library blobs"};
+    if (h.packed != h0.packed)
+      throw Error{SHELFI_ERR_FORMAT, "learners mix packed and uint64 library blobs"};
     if (h.K != h0.K)
       throw Error{SHELFI_ERR_FORMAT, "learners hold different numbers of ciphertexts"};
     if (h.depth != h0.depth || h.scale != h0.scale || h.level != h0.level)
@@ -1096,9 +1150,18 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
-  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (in_chunk + out_chunk));
+  // packed wire (version-2 blobs): uploads land packed and are unpacked on the device; a packed
+  // output is packed before its D2H
+  const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
+  const bool pin = in.front().packed, pout = dst.packed;
+  const size_t pin_chunk = pin ? group * kc * pct : 0, pout_chunk = pout ? kc * pct : 0;
+  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (in_chunk + out_chunk + pin_chunk + pout_chunk));
   uint8_t* inb[2] = {io, io + in_chunk};
   uint8_t* outb[2] = {io + 2 * in_chunk, io + 2 * in_chunk + out_chunk};
+  uint8_t* const pbase = io + 2 * (in_chunk + out_chunk);
+  uint8_t* pinb[2] = {pbase, pbase + pin_chunk};
+  uint8_t* poutb[2] = {pbase + 2 * pin_chunk, pbase + 2 * pin_chunk + pout_chunk};
+  const ArenaPack ap = arena_pack(p);
   // A: staged H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
@@ -1128,15 +1191,20 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
+        // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked)
+        uint8_t* land = pin ? pinb[b] + c * kn * pct : inb[b] + c * kn * ct_bytes;
         if (zc) {  // DMA straight from the registered upload
-          uint8_t* d = inb[b] + c * kn * ct_bytes;
+          uint8_t* d = land;
           for (const HostPiece& pc : pcs) {
             SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, pp.a));
             d += pc.n;
           }
         } else {
-          sr.s.h2dv(inb[b] + c * kn * ct_bytes, pcs.data(), pcs.size(), pp.a);
+          sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
         }
+        if (pin)
+          launch_blob_unpack((const uint32_t*)land, kn, p.L, p.logN, ap, (uint64_t*)(inb[b] + c * kn * ct_bytes),
+                             pp.a);
       }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
@@ -1155,9 +1223,14 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       launch_wavg(a, ctx->dt.tc, pp.b);
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       if (c0 + gc >= C) {
+        if (pout) {  // the sum is canonical: the residue check cannot fire
+          launch_blob_pack((const uint64_t*)outb[b], kn, p.L, p.logN, ap, ctx->dt.tc, (uint32_t*)poutb[b],
+                           ctx->dev_flag + 5, pp.b);
+          SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+        }
         SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
         dst.pieces(k0, kn, p, pcs);
-        sr.s.d2hv(pcs.data(), pcs.size(), outb[b], pp.c);
+        sr.s.d2hv(pcs.data(), pcs.size(), pout ? poutb[b] : outb[b], pp.c);
         SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
       }
       sr.s.poll();
@@ -1180,14 +1253,14 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
       // ckks.cpp:270-309: with no learners the loop never runs and the empty
       // vector<Ciphertext> is serialized; here an empty batch in the ctx's wire format
       // (depth 2 / scale Delta^2: what a weighted average of fresh ciphertexts carries)
-      const bool pal = ctx->wire == 1;
+      const int fmt = ctx->wire;
       const double scale = ctx->p.delta * ctx->p.delta;
       size_t total = 0;
-      make_output(ctx, pal, 0, 2, 0, scale, nullptr, &total);
+      make_output(ctx, fmt, 0, 2, 0, scale, nullptr, &total);
       *out_len = total;
       if (!out) return;
       if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
-      make_output(ctx, pal, 0, 2, 0, scale, out, &total);
+      make_output(ctx, fmt, 0, 2, 0, scale, out, &total);
       return;
     }
     check_weights(weights, C, ctx->p.delta);
@@ -1198,16 +1271,16 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     const uint32_t depth = h0.depth + 1;
     const double scale = h0.scale * ctx->p.delta;
     size_t total = 0;
-    make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, nullptr, &total);
+    make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, nullptr, &total);
     *out_len = total;
     if (!out) return;  // size query
     if (out_cap < total) throw Error{SHELFI_ERR_ARG, "output buffer too small"};
     advise_huge(out, total);
     // residues first (the parallel drains first-touch the fresh pages), framing after
-    CtLayout dst = make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, nullptr, &total);
+    CtLayout dst = make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, nullptr, &total);
     dst.base = out;
     if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst, lens);
-    make_output(ctx, h0.pal, h0.K, depth, h0.level, scale, out, &total);
+    make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, out, &total);
   });
 }
 
@@ -1314,9 +1387,14 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
     kc = std::min<uint64_t>(kc, K);
     const size_t cin = kc * ct_bytes, dout = kc * p.batch * 8;
-    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout));
+    // a packed blob's tower prefix lands packed and is unpacked on the device
+    const uint64_t ppre = 2 * packed_poly_bytes(p, pd.L);  // packed bytes of one ciphertext's prefix
+    const size_t pin = h.packed ? kc * ppre : 0;
+    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout + pin));
     uint8_t* cb[2] = {io, io + cin};
     uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
+    uint8_t* pb[2] = {io + 2 * (cin + dout), io + 2 * (cin + dout) + pin};
+    const ArenaPack apd = arena_pack_prefix(p, pd.L);
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(pd, kc));
     Pipe pp(ctx);
     StageRun sr(stager(ctx));
@@ -1330,7 +1408,8 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
       h.pieces(k0, kn, p, pcs, pd.L);
-      sr.s.h2dv(cb[b], pcs.data(), pcs.size(), pp.a);
+      sr.s.h2dv(h.packed ? pb[b] : cb[b], pcs.data(), pcs.size(), pp.a);
+      if (h.packed) launch_blob_unpack((const uint32_t*)pb[b], kn, pd.L, p.logN, apd, (uint64_t*)cb[b], pp.a);
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
@@ -1361,6 +1440,55 @@ int shelfi_blob_info(const uint8_t* blob, size_t len, uint64_t* num_cts, uint32_
 }
 
 size_t shelfi_blob_header_bytes(void) { return sizeof(BlobHeader); }
+
+// Host restatement of blob_unpack_kernel (the packed wire payload): row r of the
+// [K][2][L][N] batch, lane l, field j -> residue 128 (j >> 1) + 2 l + (j & 1).
+int shelfi_blob_unpack(const shelfi_ctx* ctx, const uint8_t* blob, size_t len, uint64_t* out) {
+  if (!ctx || !blob || !out) return SHELFI_ERR_ARG;
+  return guarded([&] {
+    const BlobHeader h = parse_blob(blob, len, ctx);
+    const Params& p = ctx->p;
+    const uint8_t* pay = blob + sizeof(BlobHeader);
+    if (h.version == 1) {
+      std::memcpy(out, pay, h.K * 2ull * p.L * p.N * 8);
+      return;
+    }
+    const ArenaPack ap = arena_pack(p);
+    const uint32_t rpt = p.N / kArenaChunk;
+    size_t off = 0;  // dwords
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(pay);
+    uint64_t* o = out;
+    for (uint64_t g = 0; g < h.K * 2; ++g)
+      for (uint32_t t = 0; t < p.L; ++t) {
+        const uint32_t U = ap.w[t], B = U & ~3u, F = U & 1u, D = B / 4;
+        const uint32_t N4 = D / 4, H2 = (D % 4) >= 2 ? 1 : 0, H1 = D & 1;
+        const uint32_t O2 = N4 * 256, O1 = O2 + H2 * 128;
+        for (uint32_t c = 0; c < rpt; ++c, off += 16 * U, o += kArenaChunk) {
+          const uint32_t* sl = w + off;
+          for (uint32_t lane = 0; lane < 64; ++lane) {
+            uint32_t d[15] = {0};
+            for (uint32_t q = 0; q < N4; ++q)
+              for (uint32_t i = 0; i < 4; ++i) d[4 * q + i] = sl[q * 256 + 4 * lane + i];
+            if (H2) {
+              d[4 * N4] = sl[O2 + 2 * lane];
+              d[4 * N4 + 1] = sl[O2 + 2 * lane + 1];
+            }
+            if (H1) d[D - 1] = sl[O1 + lane];
+            const uint32_t fl = F ? reinterpret_cast<const uint8_t*>(sl)[64 * B + lane] : 0;
+            for (uint32_t j = 0; j < 8; ++j) {
+              const uint32_t bo = j * B, i = bo >> 5, sh = bo & 31;
+              uint64_t v = (uint64_t)d[i] >> sh;
+              if (sh + B > 32) v |= (uint64_t)d[i + 1] << (32 - sh);
+              if (sh + B > 64) v |= (uint64_t)d[i + 2] << (64 - sh);
+              v &= (1ull << B) - 1;
+              if (F) v |= (uint64_t)((fl >> j) & 1u) << B;
+              o[128 * (j >> 1) + 2 * lane + (j & 1)] = v;
+            }
+          }
+        }
+      }
+  });
+}
 
 int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t K, uint32_t depth,
                      double scale, uint8_t** out, size_t* out_len) {
@@ -1558,18 +1686,26 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
     hipStream_t s = (hipStream_t)stream;
     std::vector<HostPiece> pcs;
     StageRun sr(stager(ctx));
+    // a packed blob lands packed (in the bytes-API buffer, idle under the ctx lock) and is unpacked
+    const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
+    uint8_t* pk = v.packed ? (uint8_t*)ensure(ctx->io, ctx->io_bytes, std::min(K, arena_stage_cts(p)) * pct) : nullptr;
+    const ArenaPack ap = arena_pack(p);
     arena_place(ctx, K, learner, C, arena_dev, s, arena_stage_cts(p), true, [&](size_t k0, size_t kn, uint64_t* dst) {
       // a blob: one payload run; an archive: 2 L tower runs per ciphertext
       v.pieces(k0, kn, p, pcs);
-      if (arena_use_stager(pcs.size(), kn * 2ull * p.L * p.N * 8)) {
-        sr.s.h2dv(dst, pcs.data(), pcs.size(), s);  // pinned staging ring, gathered in order
+      uint8_t* land = v.packed ? pk : (uint8_t*)dst;
+      size_t bytes = 0;
+      for (const HostPiece& pc : pcs) bytes += pc.n;
+      if (arena_use_stager(pcs.size(), bytes)) {
+        sr.s.h2dv(land, pcs.data(), pcs.size(), s);  // pinned staging ring, gathered in order
       } else {
-        uint8_t* d = (uint8_t*)dst;
+        uint8_t* d = land;
         for (const HostPiece& pc : pcs) {
           SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, s));
           d += pc.n;
         }
       }
+      if (v.packed) launch_blob_unpack((const uint32_t*)pk, kn, p.L, p.logN, ap, dst, s);
       return (const uint64_t*)dst;
     });
     sr.finish();
@@ -1760,7 +1896,7 @@ int shelfi_gauss_cdt(double sigma, uint64_t* cdt, int max_entries) {
 
 // ------------------------------------------------- PALISADE wire format ----
 int shelfi_set_wire_format(shelfi_ctx* ctx, int format) {
-  if (!ctx || (format != 0 && format != 1)) return SHELFI_ERR_ARG;
+  if (!ctx || format < 0 || format > 2) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
     if (format == 1 && ctx->pal_ctx_obj.empty())

@@ -406,6 +406,74 @@ void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32
   SHELFI_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------- packed wire blobs ----
+// A packed library blob (wire format "packed", shelfi_set_wire_format 2) carries its payload in the
+// arena's slice format with C = 1: ciphertexts [k0, k0 + kn) of a blob are kn consecutive
+// (ct, poly) groups, so a chunk packs / unpacks with row indices relative to its first ciphertext.
+template <int UB>
+__device__ __forceinline__ void unpack_row(const uint32_t* __restrict__ sl, uint64_t* __restrict__ dst,
+                                           uint32_t lane) {
+  using S = PackShape<UB>;
+  constexpr int B = S::B;
+  uint32_t w[S::D], fl;
+  pk_load<UB>(sl, lane, w, fl);
+  uint64_t x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int o = j * B, i = o >> 5, s = o & 31;
+    uint64_t v = (uint64_t)w[i] >> s;
+    if (s + B > 32) v |= (uint64_t)w[i + 1] << (32 - s);
+    if (s + B > 64) v |= (uint64_t)w[i + 2] << (64 - s);
+    v &= (1ull << B) - 1;
+    if (S::F) v |= (uint64_t)((fl >> j) & 1u) << B;
+    x[j] = v;
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u32x4 v;
+    v.x = (uint32_t)x[2 * g];
+    v.y = (uint32_t)(x[2 * g] >> 32);
+    v.z = (uint32_t)x[2 * g + 1];
+    v.w = (uint32_t)(x[2 * g + 1] >> 32);
+    *reinterpret_cast<u32x4*>(dst + 128 * g + 2 * lane) = v;
+  }
+}
+
+__global__ __launch_bounds__(64 * kPackedWaves) void blob_unpack_kernel(const uint32_t* __restrict__ src,
+                                                                       uint64_t rows, uint32_t L, uint32_t logN,
+                                                                       ArenaPack ap, uint64_t* __restrict__ dst) {
+  const uint64_t r = (uint64_t)blockIdx.x * kPackedWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (r >= rows) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const PackedRow pr = packed_row(r, 1, L, logN, ap);
+  const uint32_t* __restrict__ sl = src + pr.base;
+  uint64_t* __restrict__ o = dst + r * kArenaChunk;
+  switch (pr.U) {
+#define UPR(UU) \
+  case UU: unpack_row<UU>(sl, o, lane); break;
+    SHELFI_PACK_WIDTHS(UPR)
+#undef UPR
+    default: break;
+  }
+}
+
+void launch_blob_pack(const uint64_t* src, uint64_t K, uint32_t L, uint32_t logN, const ArenaPack& ap,
+                      const TowerConst* tc, uint32_t* dst, uint32_t* bad, hipStream_t s) {
+  launch_arena_pack(src, 0, K * 2 * L << (logN - 9), 1, 0, L, logN, ap, tc, reinterpret_cast<uint64_t*>(dst), bad,
+                    s);
+}
+
+void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t logN, const ArenaPack& ap,
+                        uint64_t* dst, hipStream_t s) {
+  const uint64_t rows = K * 2 * L << (logN - 9);
+  if (!rows) return;
+  const uint64_t blocks = (rows + kPackedWaves - 1) / kPackedWaves;
+  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "blob too large"};
+  hipLaunchKernelGGL(blob_unpack_kernel, dim3((uint32_t)blocks), dim3(64 * kPackedWaves), 0, s, src, rows, L, logN,
+                     ap, dst);
+  SHELFI_HIP(hipGetLastError());
+}
+
 // Rows per wavg block: with C <= 8 learners a one-row thread has only C 16-byte loads in
 // flight; the kernel then takes 2 rows.  Measured in one process per shape (tools/wavg_rows_ab.py,
 // profiles/probes/r03_wavg_rows_ab.txt).  SHELFI_WAVG_ROWS=1|2 forces one (A/B probe switch, read

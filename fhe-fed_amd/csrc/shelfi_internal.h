@@ -253,6 +253,12 @@ void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t 
 void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner,
                        uint32_t L, uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* arena,
                        uint32_t* bad, hipStream_t s);
+// Packed wire blobs: K ciphertexts [K][2][L][N] <-> the arena's slice format with C = 1 (ap from the
+// towers the buffer holds); pack flags *bad when a residue is >= q_t.
+void launch_blob_pack(const uint64_t* src, uint64_t K, uint32_t L, uint32_t logN, const ArenaPack& ap,
+                      const TowerConst* tc, uint32_t* dst, uint32_t* bad, hipStream_t s);
+void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t logN, const ArenaPack& ap,
+                        uint64_t* dst, hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,

@@ -135,6 +135,9 @@ int shelfi_blob_pack(const shelfi_ctx* ctx, const uint64_t* residues, uint64_t n
                      uint32_t depth, double scale, uint8_t** out, size_t* out_len);
 /* Offset of the residue payload inside a blob (64-byte header). */
 size_t shelfi_blob_header_bytes(void);
+/* Host-only: a blob's residues as [K][2][L][N] uint64 (out: K*2*L*N words) — a version-1 payload
+ * copied, a version-2 (packed wire, shelfi_set_wire_format 2) payload unpacked. */
+int shelfi_blob_unpack(const shelfi_ctx* ctx, const uint8_t* blob, size_t len, uint64_t* out);
 
 /* ---- PALISADE 1.11 wire format -------------- */
 /* The reference's bytes are cereal PortableBinary archives of
@@ -153,7 +156,11 @@ typedef struct {
   uint64_t ctx_offset, ctx_length; /* the embedded context object inside the archive */
   char keytag[257];
 } shelfi_palisade_info;
-int shelfi_set_wire_format(shelfi_ctx* ctx, int format); /* 0 blob (default), 1 PALISADE */
+/* 0 blob (default), 1 PALISADE archive, 2 packed blob (version 2: the residues at their moduli's
+ * widths, the arena's slice format with C = 1 — 218 of 256 bits per coefficient at 2^15/L4, so a
+ * PCIe-bound upload carries 15% fewer bytes).  Every entry that takes ciphertext
+ * bytes accepts all three. */
+int shelfi_set_wire_format(shelfi_ctx* ctx, int format);
 /* Host-only: parse an archive; residues [K][2][L][N] copied out when non-NULL. */
 int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
                           uint64_t* residues);
