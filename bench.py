@@ -670,6 +670,28 @@ def main():
             del pblobs, res_p
         finally:
             ck.set_wire_format("shelfi")
+        # and in the packed wire format (version-2 blobs at the moduli's widths)
+        try:
+            ck.set_wire_format("packed")
+            xa = np.random.default_rng(7).uniform(-1, 1, Ka * batch)
+            kblobs = [ck.encrypt(xa) for _ in range(Cl)]
+            ck.computeWeightedAverage(kblobs, weights)  # warm
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                res_k = ck.computeWeightedAverage(kblobs, weights)
+            dt_k = (time.perf_counter() - t0) / reps
+            ck.decrypt(res_k, Ka * batch)  # warm
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ck.decrypt(res_k, Ka * batch)
+            dt_kd = (time.perf_counter() - t0) / reps
+            api["packed_wire"] = {"value": round(Cl * Ka / dt_k, 1), "ms_per_call": round(dt_k * 1e3, 2),
+                                  "blob_bytes_per_learner": len(kblobs[0]), "aggregate_bytes": len(res_k),
+                                  "input_GB_per_s": round(Cl * len(kblobs[0]) / dt_k / 1e9, 2),
+                                  "decrypt_ms_per_call": round(dt_kd * 1e3, 2)}
+            del kblobs, res_k
+        finally:
+            ck.set_wire_format("shelfi")
 
     # roofline of the dominant kernel: algorithmic bytes = the C learners' packed residues
     # (K * 2 * N * sum_t U_t / 8 each, U_t ~ bitlength(q_t)) read once
