@@ -38,13 +38,14 @@ namespace {
 std::unique_ptr<CKKS> make_ckks(const std::string& scheme, unsigned batchSize, unsigned scaleFactorBits,
                                 const std::string& cryptodir, unsigned multDepth, uint64_t seed, bool decodeNoise,
                                 const std::string& wireFormat, int device) {
-  if (wireFormat != "palisade" && wireFormat != "shelfi")
-    throw py::value_error("wireFormat must be 'palisade' or 'shelfi'");
+  if (wireFormat != "palisade" && wireFormat != "shelfi" && wireFormat != "packed")
+    throw py::value_error("wireFormat must be 'palisade', 'shelfi' or 'packed'");
   CKKS::Options o;
   o.multDepth = multDepth;
   o.seed = seed;
   o.decodeNoise = decodeNoise;
   o.wire_palisade = wireFormat == "palisade";
+  o.wire_packed = wireFormat == "packed";
   o.device = device;
   return std::make_unique<CKKS>(scheme, batchSize, scaleFactorBits, cryptodir, o);
 }

@@ -22,8 +22,8 @@
 // bad arguments / out-of-range values (pybind11: ValueError), std::runtime_error otherwise
 // (pybind11: RuntimeError); soft errors print as the reference does.  Byte format: the
 // reference's own PALISADE cereal archives (ckks.cpp:98-100, :163-165) once keys are
-// generated or loaded, or this library's blob (Options::wire_palisade = false); both are
-// accepted as inputs.
+// generated or loaded, or this library's blob (Options::wire_palisade = false; packed at the
+// moduli's widths with Options::wire_packed); all are accepted as inputs.
 #ifndef SHELFI_SCHEME_HPP_
 #define SHELFI_SCHEME_HPP_
 
@@ -84,6 +84,7 @@ class CKKS : public Scheme {
     uint64_t seed = 0;          // deterministic encryption randomness (parity tests); 0: OS entropy
     bool decodeNoise = true;    // PALISADE 1.11's decode noise flooding (its Decrypt floods)
     bool wire_palisade = true;  // encrypt / aggregate answer in PALISADE's cereal archives
+    bool wire_packed = false;   // with wire_palisade false: packed library blobs (version 2)
   };
 
   CKKS(std::string scheme, unsigned batchSize, unsigned scaleFactorBits, std::string cryptodir)
@@ -231,7 +232,9 @@ class CKKS : public Scheme {
  private:
   // keys generated here or loaded from PALISADE files carry the context object and key tag
   // PALISADE's archive format needs
-  void apply_wire_format() { throw_on_error(shelfi_set_wire_format(ctx_, opt_.wire_palisade ? 1 : 0), "wire format"); }
+  void apply_wire_format() {
+    throw_on_error(shelfi_set_wire_format(ctx_, opt_.wire_palisade ? 1 : opt_.wire_packed ? 2 : 0), "wire format");
+  }
 
   unsigned batchSize;
   unsigned scaleFactorBits;
