@@ -1202,12 +1202,13 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         } else {
           sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
         }
-        if (pin)
-          launch_blob_unpack((const uint32_t*)land, kn, p.L, p.logN, ap, (uint64_t*)(inb[b] + c * kn * ct_bytes),
-                             pp.a);
       }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+      if (pin)  // unpacked on the compute stream, so the upload stream moves on to the next chunk
+        for (size_t c = 0; c < gc; ++c)
+          launch_blob_unpack((const uint32_t*)(pinb[b] + c * kn * pct), kn, p.L, p.logN, ap,
+                             (uint64_t*)(inb[b] + c * kn * ct_bytes), pp.b);
       if (ci >= 2 && c0 == 0) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       WavgArgs a;
       std::memset(&a, 0, sizeof(a));
@@ -1409,9 +1410,9 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
       h.pieces(k0, kn, p, pcs, pd.L);
       sr.s.h2dv(h.packed ? pb[b] : cb[b], pcs.data(), pcs.size(), pp.a);
-      if (h.packed) launch_blob_unpack((const uint32_t*)pb[b], kn, pd.L, p.logN, apd, (uint64_t*)cb[b], pp.a);
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+      if (h.packed) launch_blob_unpack((const uint32_t*)pb[b], kn, pd.L, p.logN, apd, (uint64_t*)cb[b], pp.b);
       if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       dn.g0 += (ci ? kc : 0);
       launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
