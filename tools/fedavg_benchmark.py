@@ -35,8 +35,9 @@ def main():
                     help="rate: encrypted prefix fraction; mask: top-k fraction of each key")
     ap.add_argument("--layers", default="")
     ap.add_argument("--pack", action="store_true")
-    ap.add_argument("--wire", choices=["shelfi", "palisade"], default="shelfi",
-                    help="bytes format of the ciphertexts (palisade = the reference's own archives)")
+    ap.add_argument("--wire", choices=["shelfi", "palisade", "packed"], default="shelfi",
+                    help="bytes format of the ciphertexts (palisade = the reference's own archives, "
+                         "packed = this library's blob at the moduli's bit widths)")
     a = ap.parse_args()
     shapes = {"lenet5": F.lenet5_shapes(), "resnet18": F.resnet_shapes(18),
               "resnet50": F.resnet_shapes(50)}[a.model]
@@ -48,8 +49,8 @@ def main():
         ck.loadCryptoParams()  # benchmark.py:481 (the reference's own keys)
     else:
         ck.genCryptoContextAndKeyGen()
-    if a.wire == "palisade":
-        ck.set_wire_format("palisade")
+    if a.wire != "shelfi":
+        ck.set_wire_format(a.wire)
     t_init = time.time() - t0
     masks = None
     if a.select == "mask":  # masking.py:15-21 top-k of a sensitivity map (synthetic: |grad| ~ U(0,1))
