@@ -101,3 +101,68 @@ def test_packed_blob_into_arena(c2):
     assert torch.equal(a.buf, b.buf)
     w = [0.2, 0.5, 0.3]
     assert torch.equal(a.wavg(w), b.wavg(w))
+
+
+def _packed(ck):
+    class _W:
+        def __enter__(self):
+            ck.set_wire_format("packed")
+
+        def __exit__(self, *a):
+            ck.set_wire_format("shelfi")
+    return _W()
+
+
+def test_packed_empty_inputs(c2):
+    """Edge cases of the reference's API (ckks.cpp:65, 273-309) in the packed format: an empty
+    vector encrypts to zero ciphertexts, no learners aggregate to the empty batch."""
+    ck = c2
+    with _packed(ck):
+        e0 = ck.encrypt(np.zeros(0))
+        assert int.from_bytes(e0[4:6], "little") == 2 and m.blob_info(e0)["num_cts"] == 0
+        assert ck.decrypt(e0, 0).shape == (0,)
+        assert m.blob_info(ck.computeWeightedAverage([e0, e0], [0.5, 0.5]))["num_cts"] == 0
+        assert m.blob_info(ck.computeWeightedAverage([], []))["num_cts"] == 0
+
+
+def test_packed_blob_validation(c1, c2):
+    """A packed upload is held to the uint64 blob's rules: residues read at the field width must
+    be < q_t (a field of all ones is 2^U_t - 1 >= q_t), the length must match the header, and a
+    blob of other parameters is refused — by computeWeightedAverage, decrypt and Arena.put."""
+    ck = c2
+    inf = ck.info()
+    S = inf["batch"]
+    x = np.linspace(-1, 1, 2 * S)
+    good = _enc(ck, x, "packed", 300)
+    hdr = m._lib.load().shelfi_blob_header_bytes()
+    U0 = AL.widths(inf["moduli"])[0]
+    bad = bytearray(good)
+    bad[hdr:hdr + 64 * U0] = b"\xff" * (64 * U0)  # ct 0, c0, tower 0: its first row's slice
+    bad = bytes(bad)
+    small = _enc(c1, np.linspace(-1, 1, 100), "packed", 301)
+    with _packed(ck):
+        with pytest.raises(RuntimeError, match="residue >= its tower modulus"):
+            ck.computeWeightedAverage([good, bad], [0.5, 0.5])
+        with pytest.raises((ValueError, RuntimeError)):
+            ck.computeWeightedAverage([good, good[:-4]], [0.5, 0.5])
+        with pytest.raises((ValueError, RuntimeError)):
+            ck.computeWeightedAverage([good, small], [0.5, 0.5])
+        with pytest.raises((ValueError, RuntimeError)):
+            ck.decrypt(good[:-4], 2 * S)
+        with pytest.raises((ValueError, RuntimeError)):
+            ck.decrypt(small, 100)
+        ar = D.Arena(ck, 2, 2)
+        with pytest.raises(m.ShelfiError, match="residue"):
+            ar.put(0, bad)
+        with pytest.raises(m.ShelfiError, match="parameters"):
+            ar.put(1, small)
+        with pytest.raises(m.ShelfiError, match="length"):
+            ar.put(1, good[:-4])
+        # the context and the arena stay usable
+        out = ck.decrypt(ck.computeWeightedAverage([good, good], [0.5, 0.5]), 2 * S)
+        assert np.abs(out - x).max() < 1e-7
+        ar.put(0, good)
+        ar.put(1, good)
+        ref = m.blob_residues(ck.computeWeightedAverage([good, good], [0.25, 0.75]), inf["ring_dim"],
+                              inf["num_towers"], ckks=ck)
+        assert np.array_equal(ar.wavg([0.25, 0.75]).cpu().numpy().view(np.uint64), ref)
