@@ -271,14 +271,16 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
 
 constexpr int kPackedWaves = 4;  // waves per block, one row each
 
-template <int UR>
-__global__ __launch_bounds__(64 * kPackedWaves) void wavg_packed(const uint32_t* __restrict__ arena,
-                                                                const uint32_t* __restrict__ wl,
-                                                                uint32_t C, uint64_t rows, uint32_t L,
-                                                                uint32_t logN, ArenaPack ap,
-                                                                const TowerConst* __restrict__ tcs,
-                                                                uint64_t* __restrict__ out) {
-  const uint64_t r = (uint64_t)blockIdx.x * kPackedWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+template <int UR, int WV = kPackedWaves>
+__global__ __launch_bounds__(64 * WV) void wavg_packed(const uint32_t* __restrict__ arena,
+                                                      const uint32_t* __restrict__ wl, uint32_t C,
+                                                      uint64_t rows, uint32_t L, uint32_t logN, ArenaPack ap,
+                                                      const TowerConst* __restrict__ tcs,
+                                                      uint64_t* __restrict__ out, uint32_t xcd) {
+  // xcd: consecutive blocks land on the 8 XCDs in turn; remap so each XCD walks one contiguous
+  // eighth of the rows (probe switch SHELFI_PACK_XCD; needs gridDim.x % 8 == 0)
+  const uint32_t b = xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const uint64_t r = (uint64_t)b * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (r >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   const PackedRow pr = packed_row(r, C, L, logN, ap);
@@ -375,22 +377,32 @@ void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t 
                         uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* out, hipStream_t s) {
   const uint64_t nrows = (rows << logN) / kArenaChunk;
   if (!nrows) return;
-  const uint64_t blocks = (nrows + kPackedWaves - 1) / kPackedWaves;
-  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   if (nrows > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  // learners unrolled per iteration: SHELFI_PACK_UNROLL=1|2|4 (A/B probe switch, read per launch;
-  // 2 and 4 measured equal, profiles/probes/r03_wavg_packed_ab.txt)
+  // A/B probe switches, read per launch (profiles/probes/r03_wavg_packed_ab.txt): learners unrolled
+  // per iteration SHELFI_PACK_UNROLL=1|2|4 (2 and 4 measured equal), waves (rows) per block
+  // SHELFI_PACK_WAVES=2|4|8, XCD-contiguous block order SHELFI_PACK_XCD=1
   const char* env = getenv("SHELFI_PACK_UNROLL");
   const int u = env ? atoi(env) : 2;
-#define WPK(UU)                                                                                              \
-  hipLaunchKernelGGL((wavg_packed<UU>), dim3((uint32_t)blocks), dim3(64 * kPackedWaves), 0, s,               \
-                     reinterpret_cast<const uint32_t*>(arena), wl_dev, C, nrows, L, logN, ap, tc, out)
-  if (u == 1)
-    WPK(1);
+  const char* wenv = getenv("SHELFI_PACK_WAVES");
+  const int wv = wenv ? atoi(wenv) : kPackedWaves;
+  const char* xenv = getenv("SHELFI_PACK_XCD");
+  const int wvs = (wv == 2 || wv == 8) && u == 2 ? wv : kPackedWaves;
+  const uint64_t blocks = (nrows + wvs - 1) / wvs;
+  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  const uint32_t xcd = xenv && *xenv == '1' && blocks % 8 == 0 ? 1u : 0u;
+#define WPK(UU, WW)                                                                                          \
+  hipLaunchKernelGGL((wavg_packed<UU, WW>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s,                     \
+                     reinterpret_cast<const uint32_t*>(arena), wl_dev, C, nrows, L, logN, ap, tc, out, xcd)
+  if (wvs == 2)
+    WPK(2, 2);
+  else if (wvs == 8)
+    WPK(2, 8);
+  else if (u == 1)
+    WPK(1, 4);
   else if (u == 4)
-    WPK(4);
+    WPK(4, 4);
   else
-    WPK(2);
+    WPK(2, 4);
 #undef WPK
   SHELFI_HIP(hipGetLastError());
 }
