@@ -178,7 +178,7 @@ def test_wavg_arena_bitexact(cfg2, C, K):
 def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C, K):
     """The packed arena at every width class its kernels carry: residues at 0, q-1
     (the top bit, for towers whose bitlength is 1 mod 4, lives in the flag plane) and random, device and host placement, whole-range and sub-range aggregation == oracle, at
-    every learner unroll depth of wavg_packed."""
+    every learner unroll depth of wavg_packed and under its probe switches."""
     ck = m.CKKS("ckks", 1024, scale, str(tmp_path) + os.sep, multDepth=depth, firstModBits=first,
                 seed=3, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
@@ -211,6 +211,13 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), unroll
     monkeypatch.delenv("SHELFI_PACK_UNROLL")
+    # the probe switches: rows per block, XCD-contiguous block order
+    for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_XCD", "1")):
+        monkeypatch.setenv(env, val)
+        got = ar.wavg(w)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), (env, val)
+        monkeypatch.delenv(env)
     if K > 1:
         got = ar.wavg(w, k0=1, k1=K)
         torch.cuda.synchronize()
