@@ -81,7 +81,7 @@ def parse():
                          "the sums to the consumer, shelfi_dev_decrypt_sum folds them on load)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
-    ap.add_argument("--place-output", type=int, default=8,
+    ap.add_argument("--place-output", type=int, default=16,
                     help="arena layout, no collective: time this many candidate output buffers before "
                          "the timed region and keep the fastest placement (Arena.place_output; the "
                          "plain torch.empty buffer's launch is reported as roofline.untuned_output); "
@@ -344,7 +344,9 @@ def main():
         placement = None
         if args.layout == "arena" and shard != "learners" and args.place_output > 0:
             # where the aggregate lands in HBM relative to the arena moves the launch time by
-            # up to 12%: keep the fastest of a few candidate buffers
+            # up to 12%: keep the fastest of a few candidate buffers; the penalty
+            # follows ~3 GiB address ranges (probes/r03_placement_alloc.txt), so 16 candidates
+            # (24 GiB of address space, freed after the pick) find a fast range more often than 8
             # candidate 0 is a plain torch.empty buffer allocated first (on some boxes every
             # buffer allocated next to the others ran slower than it)
             plain0 = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
