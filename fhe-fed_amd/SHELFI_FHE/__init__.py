@@ -367,8 +367,14 @@ def blob_residues(blob: bytes, ring_dim: int, num_towers: int, ckks: "CKKS | Non
     if version == 2:
         if ckks is None:
             raise ValueError("a packed blob needs its context to unpack (blob_residues(..., ckks=ck))")
+        # the library writes K * 2 * L * N words for the context's (L, N): the shape is the
+        # context's, and a caller's shape that differs is refused rather than overrun
+        inf = ckks.info()
+        if (int(ring_dim), int(num_towers)) != (inf["ring_dim"], inf["num_towers"]):
+            raise ValueError("blob_residues: shape (N=%d, L=%d) is not the context's (N=%d, L=%d)"
+                             % (ring_dim, num_towers, inf["ring_dim"], inf["num_towers"]))
         K = blob_info(blob)["num_cts"]
-        out = np.empty((K, 2, num_towers, ring_dim), np.uint64)
+        out = np.empty((K, 2, inf["num_towers"], inf["ring_dim"]), np.uint64)
         b = bytes(blob)
         check(lib.shelfi_blob_unpack(ckks._ctx, C.cast(C.c_char_p(b), _lib.u8p), len(b),
                                      out.ctypes.data_as(_lib.u64p)), "blob_unpack")

@@ -123,6 +123,7 @@ SIGNATURES = {
                                        C.c_void_p, C.c_void_p]),
     "shelfi_dev_arena_put_blob": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
+    "shelfi_dev_arena_release": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
     "shelfi_dev_wavg_arena_pick_output": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t,

@@ -105,7 +105,25 @@ class Arena:
         words = lib.shelfi_arena_words(ckks._ctx, self.C, self.K)
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
 
+    def release(self):
+        """Drop this arena's refusal marks in the context and free its memory."""
+        buf = getattr(self, "buf", None)
+        if buf is None:
+            return
+        ctx = getattr(self.ckks, "_ctx", None)
+        if ctx is not None and getattr(ctx, "value", None):
+            _lib.load().shelfi_dev_arena_release(ctx, C.c_void_p(buf.data_ptr()), buf.numel())
+        self.buf = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
     def _check_gen(self):
+        if getattr(self, "buf", None) is None:
+            raise ValueError("the arena was released")
         if getattr(self.ckks, "_params_gen", 0) != self._gen:
             raise ValueError("the context's parameters or keys were reloaded since this arena was "
                              "made: its packed layout no longer matches; make a new Arena")

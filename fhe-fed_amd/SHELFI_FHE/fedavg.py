@@ -106,9 +106,13 @@ class Selection:
 
 
 def top_k_mask(sensitivity: np.ndarray, fraction: float) -> np.ndarray:
-    """masking.py:15-21 get_top_k_mask: True on the `fraction` largest entries."""
+    """masking.py:15-21 get_top_k_mask: True on the k = int(len(vector) * p) largest entries
+    (`torch.topk(vector, int(len(vector) * p), largest=True)`: the product truncates, so the
+    count is the floor of n * p).  The reference's Mask is the complement (False marks the
+    protected entries, masking.py:19-20); here True marks the entries that get encrypted.
+    Among equal values torch.topk's choice is unspecified, so is this one's."""
     s = np.asarray(sensitivity).reshape(-1)
-    k = int(round(s.size * fraction))
+    k = int(s.size * fraction)
     mask = np.zeros(s.size, dtype=bool)
     if k > 0:
         mask[np.argpartition(-s, k - 1)[:k]] = True

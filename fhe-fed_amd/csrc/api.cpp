@@ -157,6 +157,7 @@ void free_ntt_tables(DeviceTables& dt) {
 
 static void free_tables(shelfi_ctx* ctx) {
   eval_release(ctx, false);  // level / extended-basis tables belong to these parameters
+  ctx->arena_refused.clear();  // arenas are laid out for these parameters
   free_ntt_tables(ctx->dt);
   dfree_t(ctx->dt.fft_inv);
   dfree_t(ctx->dt.fft_fwd);
@@ -166,6 +167,7 @@ static void free_tables(shelfi_ctx* ctx) {
 
 static void free_keys(shelfi_ctx* ctx) {
   eval_release(ctx, true);  // the relinearization key belongs to the secret key
+  ctx->arena_refused.clear();  // a reload starts a new parameter/key generation of arenas
   dfree_t(ctx->dk.pk);
   dfree_t(ctx->dk.pk_sh);
   dfree_t(ctx->dk.sk);
@@ -1542,6 +1544,23 @@ size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K) {
 }  // extern "C"
 
 namespace shelfi {
+// The refusal bookkeeping of one put into slot `learner` of the arena [arena, arena + words) of C
+// learners (ctx lock held): the slot's earlier entry is superseded, and so is every entry that
+// overlaps this arena but names another base, span or learner count (that arena was freed and
+// this memory reused); a refused put records the slot.
+static void arena_mark(shelfi_ctx* ctx, const uint64_t* arena, size_t words, size_t C, size_t learner,
+                       bool refused) {
+  auto& R = ctx->arena_refused;
+  for (size_t i = 0; i < R.size();) {
+    const auto& r = R[i];
+    const bool same_arena = r.arena == arena && r.words == words && r.C == C;
+    const bool overlaps = arena < r.arena + r.words && r.arena < arena + words;
+    if ((same_arena && r.learner == learner) || (overlaps && !same_arena)) R.erase(R.begin() + (long)i);
+    else ++i;
+  }
+  if (refused) R.push_back({arena, words, C, learner});
+}
+
 // Placement of a learner's batch into its packed slices (arena_pack_kernel: the canonical-residue
 // check of every residue rides along, ~0.3 ms of HBM per 1.4 GiB against ~30 ms of PCIe for the
 // upload), then the slot's refusal mark is set or cleared.  `rows_of(k0, kn, dst)` makes
@@ -1568,17 +1587,12 @@ static void arena_place(shelfi_ctx* ctx, size_t K, size_t learner, size_t C, uin
   uint32_t flag = 0;
   SHELFI_HIP(hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, s));
   SHELFI_HIP(hipStreamSynchronize(s));
-  auto& R = ctx->arena_refused;
-  for (size_t i = 0; i < R.size();)  // this slot's earlier refusal, if any, is superseded
-    if (R[i].arena == arena_dev && R[i].learner == learner) R.erase(R.begin() + (long)i);
-    else ++i;
-  if (flag) {
-    R.push_back({arena_dev, (size_t)arena_ct_words(p, C) * K, learner});
+  arena_mark(ctx, arena_dev, (size_t)arena_ct_words(p, C) * K, C, learner, flag != 0);
+  if (flag)
     throw Error{SHELFI_ERR_FORMAT,
                 "learner " + std::to_string(learner) +
                     ": ciphertext residue >= its tower modulus (malformed upload; the arena slot is "
                     "marked refused until a valid upload replaces it)"};
-  }
 }
 // How host uploads reach the device: a contiguous run (a library blob's payload, a host batch) as one
 // hipMemcpyAsync from the caller's pageable memory (54 GB/s for a 1.5 GB upload), the 2 L tower runs
@@ -1676,11 +1690,19 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
   if (!ctx || !arena_dev || !blob || learner >= C) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
   return guarded([&] {
-    // header first, against the context (parameters, key tag / key id), before any copy
-    const CtLayout v = open_cts(ctx, blob, len);
-    if (v.K != K)
-      throw Error{SHELFI_ERR_FORMAT, "upload holds " + std::to_string(v.K) + " ciphertexts, the arena " +
-                                         std::to_string(K)};
+    // header first, against the context (parameters, key tag / key id), before any copy; a
+    // refused header marks the slot refused too, so the slot's previous round cannot be
+    // aggregated as if this upload had landed (the residue check below does the same)
+    CtLayout v;
+    try {
+      v = open_cts(ctx, blob, len);
+      if (v.K != K)
+        throw Error{SHELFI_ERR_FORMAT, "upload holds " + std::to_string(v.K) + " ciphertexts, the arena " +
+                                           std::to_string(K)};
+    } catch (...) {
+      arena_mark(ctx, arena_dev, (size_t)arena_ct_words(ctx->p, C) * K, C, learner, true);
+      throw;
+    }
     if (!K) return;
     DeviceGuard g(ctx->device);
     const Params& p = ctx->p;
@@ -1710,6 +1732,17 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
       return (const uint64_t*)dst;
     });
     sr.finish();
+  });
+}
+
+int shelfi_dev_arena_release(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t words) {
+  if (!ctx || (words && !arena_dev)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    auto& R = ctx->arena_refused;
+    for (size_t i = 0; i < R.size();)
+      if (arena_dev < R[i].arena + R[i].words && R[i].arena < arena_dev + words) R.erase(R.begin() + (long)i);
+      else ++i;
   });
 }
 

@@ -2064,11 +2064,20 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
 // 30-bit limb, below 2^64 without carries: one v_mad_u64_u32 per product), then one carry
 // pass; X is exact either way, so the two paths give the same bits.
 //
-// k (round 3): sum_t y_t / q_t = k + X / Q exactly, and X / Q is within 2^-17 of 0 for every X
-// this decode can represent (|X| < 2^127 << Q / 2, the 128-bit read below), so k needs no
-// double precision: binary32 terms (y_t >> s_t) * (2^s_t / q_t) with y_t >> s_t < 2^32
-// (TowerConst::crt_sh), each within 2^-31 + 2^-23 of y_t / q_t, round half up.  The oracle's CRT is exact (multi-word centring); the two agree wherever the
-// decode is defined.  For L <= 7, k <= L fits a 32-bit limb multiplier.
+// k (round 3): sum_t y_t / q_t = k + X / Q exactly (Q here is the decoded prefix's modulus Q',
+// decode_towers: the shortest tower prefix above 2^130, or every tower when the chain is
+// shorter).  Every X this decode represents has |X| < 2^127 (the signed 128-bit read below), so
+// over a prefix above 2^130 X / Q' is within 2^-3 of 0: k = round(sum) has 3/8 of headroom on
+// either side of its rounding boundary.  The binary32 estimate spends at most ~L * 2^-21 of it:
+// terms (y_t >> s_t) * (2^s_t / q_t) with y_t >> s_t < 2^32 (TowerConst::crt_sh) are each within
+// 2^-31 + 2^-23 of y_t / q_t, and L <= 7 float additions of values below 8 round by <= 2^-21
+// each; round half up.  Correctness therefore needs |X| < 2^127, which every decryptable
+// ciphertext meets by construction (|X| ~ |m| * scale: the encoder refuses |x scale| > 2^61 and
+// a depth-2 aggregate multiplies by weights W < 2^63), not a runtime check;
+// tests/test_gpu_decode_towers.py::test_prefix_decode_near_the_2_127_limit decodes |X| ~ 2^125
+// over a 2^132 prefix.  Over a chain below 2^130 the decode is the plain centred CRT mod Q, and a
+// valid decryption has |X| << Q / 2.  The oracle's CRT is exact (multi-word centring); the two
+// agree wherever the decode is defined.  For L <= 7, k <= L fits a 32-bit limb multiplier.
 template <class YF>
 __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst* __restrict__ tcs,
                                             uint64_t Qlo, uint64_t Qhi, double inv_scale) {

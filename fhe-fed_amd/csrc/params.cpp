@@ -91,15 +91,35 @@ uint64_t min_root(uint64_t m, uint64_t q) {
   return best;
 }
 
-// HE-standard 128-bit classic table used by PALISADE's ParamsGen, plus the
-// batching constraint N >= 2 * batch.
+// PALISADE 1.11 ParamsGenCKKS's ring dimension, as reached from ckks.cpp:28
+// (genCryptoContextCKKS(multDepth, scaleFactorBits, batchSize), ringDim 0, HYBRID key
+// switching with dnum = ComputeNumLargeDigits(0, multDepth)) [PALISADE-1.11]:
+//   qBound  = firstModSize + (numPrimes - 1) * scaleFactorBits          (an estimate in bits)
+//   qBound += ceil(ceil(qBound / dnum) / 60) * 60                         (HYBRID: log2 P)
+//   N       = FindRingDim(HEStd_ternary, HEStd_128_classic, qBound), and N >= 2 * batch.
+// Bounding log2(Q * P), not log2 Q, is what code/params_results.csv:2-16 records: the
+// archive size of one client's CNN_OriginalFedAvg ciphertexts is the same at scale bits 14,
+// 20, 33, 40 and 52 for each batch, i.e. N = 8192 at every row (log Q alone would give 4096
+// at batch 1024/2048 below 52 bits).
+uint32_t hybrid_dnum(uint32_t L) {
+  const uint32_t depth = L - 1;
+  uint32_t dn = depth > 3 ? 3 : (depth > 0 ? 2 : 1);
+  return dn > L ? L : dn;
+}
+
+double ring_dim_qbound(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits) {
+  double qb = (L > 1 ? first_mod_bits : scale_bits) + (double)(L - 1) * scale_bits;
+  qb += std::ceil(std::ceil(qb / hybrid_dnum(L)) / 60.0) * 60.0;
+  return qb;
+}
+
 uint32_t default_ring_dim(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
                           uint32_t batch) {
   static const uint32_t dims[] = {1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072};
   static const uint32_t maxlog[] = {27, 54, 109, 218, 438, 881, 1761, 3524};
-  double logq = (L > 1 ? first_mod_bits : scale_bits) + (double)(L - 1) * scale_bits;
+  const double qb = ring_dim_qbound(L, scale_bits, first_mod_bits);
   for (int i = 0; i < 8; ++i)
-    if (logq <= maxlog[i] && dims[i] >= 2ull * batch) return dims[i];
+    if (qb <= maxlog[i] && dims[i] >= 2ull * batch) return dims[i];
   return 0;
 }
 
@@ -130,9 +150,7 @@ void generate_chain(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_
 // its key polynomials carry exactly the two special primes this returns).
 void special_primes(uint32_t N, uint32_t L, const uint64_t* q, uint32_t* dnum, uint32_t* alpha,
                     uint32_t* kP, uint64_t* p, uint64_t* ppsi) {
-  const uint32_t depth = L - 1;
-  uint32_t dn = depth > 3 ? 3 : (depth > 0 ? 2 : 1);
-  if (dn > L) dn = L;
+  const uint32_t dn = hybrid_dnum(L);
   const uint32_t al = (L + dn - 1) / dn;
   uint32_t max_bits = 0;
   for (uint32_t j = 0; j < dn; ++j) {

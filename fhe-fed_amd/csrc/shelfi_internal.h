@@ -69,6 +69,8 @@ uint64_t shoup(uint64_t w, uint64_t q);  // floor(w * 2^64 / q)
 uint64_t mod_signed(int64_t v, uint64_t q);
 bool is_prime(uint64_t n);
 uint32_t default_ring_dim(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits, uint32_t batch);
+uint32_t hybrid_dnum(uint32_t L);
+double ring_dim_qbound(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits);
 void generate_chain(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits,
                     uint64_t* q, uint64_t* psi);
 uint64_t min_root(uint64_t m, uint64_t q);
@@ -185,9 +187,13 @@ struct shelfi_ctx {
                                  // upload residue >= q, [4] arena upload residue >= q
   // arena slots whose last upload was refused (shelfi_dev_arena_put*): an aggregation
   // over an arena range holding one fails instead of summing the refused residues
+  // (an entry names the arena by its base, its shelfi_arena_words(C, K) span and C, so a later
+  // put into a differently shaped arena over the same memory -- the old one was freed -- drops it;
+  // shelfi_dev_arena_release and a parameter/key reload drop entries explicitly)
   struct ArenaRefusal {
     const uint64_t* arena;
     size_t words;  // shelfi_arena_words(C, K) of that arena
+    size_t C;
     size_t learner;
   };
   std::vector<ArenaRefusal> arena_refused;

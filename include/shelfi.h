@@ -230,9 +230,15 @@ int shelfi_dev_arena_put(shelfi_ctx* ctx, const void* src, int src_on_host, size
  * moduli (params_id), the key (key_id / PALISADE keyTag, as EvalAdd refuses other keys,
  * SURVEY App. B.7), the CKKS-packed encoding and the length; the batch must hold exactly
  * K ciphertexts.  Refusals are SHELFI_ERR_FORMAT; the residues are then validated as
- * for shelfi_dev_arena_put. */
+ * for shelfi_dev_arena_put.  A refused header marks the slot refused as well (its previous
+ * contents are not aggregated as if the upload had landed). */
 int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t K, size_t learner,
                               size_t C, uint64_t* arena_dev, void* stream);
+/* Forget the refusal marks of an arena's memory [arena_dev, arena_dev + words) before it is
+ * freed or reused (no reference counterpart: the reference has no resident arena).  A put
+ * into a differently shaped arena over the same memory, and a parameter or key reload, drop
+ * stale marks by themselves. */
+int shelfi_dev_arena_release(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t words);
 /* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream);

@@ -1007,6 +1007,26 @@ static uint32_t prod_bits(const uint64_t* q, uint32_t i0, uint32_t i1) {
   return bits;
 }
 
+/* PALISADE 1.11 ParamsGenCKKS ring dimension for genCryptoContextCKKS(multDepth,
+ * scaleFactorBits, batch) with ringDim 0 (ckks.cpp:28) [PALISADE-1.11]:
+ *   qBound = firstModSize + (L - 1) scaleBits;  HYBRID: qBound += ceil(ceil(qBound/dnum)/60) 60
+ *   N = smallest HE-standard (ternary, 128-bit classic) dimension with log2 bound >= qBound,
+ *       and N >= 2 batch.
+ * Pinned by code/params_results.csv:2-16: every (batch, scale bits) row has the N = 8192
+ * archive size (tests/test_palisade_codec.py). Returns 0 when no dimension fits. */
+uint32_t or_ring_dim(uint32_t L, uint32_t scale_bits, uint32_t first_mod_bits, uint32_t batch) {
+  static const uint32_t dims[] = {1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072};
+  static const uint32_t maxlog[] = {27, 54, 109, 218, 438, 881, 1761, 3524};
+  uint32_t dn = (L - 1 > 3) ? 3 : (L - 1 > 0 ? 2 : 1);
+  if (dn > L) dn = L;
+  uint32_t qb = (L > 1 ? first_mod_bits : scale_bits) + (L - 1) * scale_bits;
+  uint32_t digit = (qb + dn - 1) / dn;
+  qb += ((digit + 59) / 60) * 60;
+  for (int i = 0; i < 8; ++i)
+    if (qb <= maxlog[i] && dims[i] >= 2ull * batch) return dims[i];
+  return 0;
+}
+
 /* ComputeNumLargeDigits(0, multDepth = L - 1): 3 above depth 3, 2 from depth 1, else 1;
  * alpha = ceil(L / dnum); kP = ceil(maxBits / 60) primes below FirstPrime(60, 2N) by
  * PreviousPrime, skipping Q's moduli; roots are the minimal primitive 2N-th roots. */

@@ -45,6 +45,7 @@ def _load():
         "or_prev_prime": (C.c_uint64, [C.c_uint64, C.c_uint64]),
         "or_next_prime": (C.c_uint64, [C.c_uint64, C.c_uint64]),
         "or_min_root": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+        "or_ring_dim": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
         "or_params_generate": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p]),
         "or_ntt_fwd": (None, [u64p, C.c_uint32, C.c_uint64, C.c_uint64]),
         "or_decrypt_coeffs": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
@@ -121,15 +122,35 @@ def params_generate(N: int, L: int, scale_bits: int = 52, first_mod_bits: int = 
 
 
 def min_ring_dim(log_q: float, batch: int) -> int:
-    """PALISADE ParamsGen ring dimension: smallest power of two meeting the
-    HE-standard 128-bit classic bound for log2(Q) and N >= 2*batch
-    [PALISADE-1.11 StdLatticeParm table]."""
+    """HE-standard table lookup: smallest power of two whose 128-bit classic (ternary secret)
+    bound covers log_q bits, with N >= 2*batch [PALISADE-1.11 StdLatticeParm table]."""
     table = [(1024, 27), (2048, 54), (4096, 109), (8192, 218), (16384, 438), (32768, 881),
              (65536, 1761), (131072, 3524)]
     for n, maxlog in table:
         if log_q <= maxlog and n >= 2 * batch:
             return n
     raise ValueError("no ring dimension for log_q=%s batch=%s" % (log_q, batch))
+
+
+def q_bound(L: int, scale_bits: int = 52, first_mod_bits: int = 60) -> int:
+    """PALISADE 1.11 ParamsGenCKKS's modulus estimate under HYBRID key switching, in bits:
+    firstModSize + (L-1)*scaleBits for Q, plus ceil(ceil(qBound/dnum)/60)*60 for the special
+    primes P, dnum = ComputeNumLargeDigits(0, L-1) [PALISADE-1.11]."""
+    dn = 3 if L - 1 > 3 else (2 if L - 1 > 0 else 1)
+    dn = min(dn, L)
+    qb = (first_mod_bits if L > 1 else scale_bits) + (L - 1) * scale_bits
+    digit = -(-qb // dn)  # ceil(qBound / dnum)
+    return qb + -(-digit // 60) * 60
+
+
+def ring_dim(L: int, scale_bits: int, batch: int, first_mod_bits: int = 60) -> int:
+    """ckks.cpp:28 genCryptoContextCKKS(multDepth = L-1, scaleBits, batch), ringDim 0: the
+    ring dimension ParamsGen picks for log2(Q*P) (q_bound).  code/params_results.csv:2-16
+    pins it: N = 8192 for every (batch, scale bits) row of benchmark_crypto.py's sweep.
+    The C twin is or_ring_dim."""
+    n = min_ring_dim(q_bound(L, scale_bits, first_mod_bits), batch)
+    assert n == lib.or_ring_dim(L, scale_bits, first_mod_bits, batch)
+    return n
 
 
 # ------------------------------------------------------------------- NTT ----

@@ -72,7 +72,7 @@ def oracle_round(O, name, palisade_keys=None):
         psi = np.array(ctx["psi"], np.uint64)
         N = ctx["N"]
     else:
-        N = O.min_ring_dim(60 + (L - 1) * 52, slots)
+        N = O.ring_dim(L, 52, slots)
         q, psi = O.params_generate(N, L, 52, 60)
         s, e, a = O.sample_keygen(kseed, N, q)
         sk, pk = O.keygen(s, e, a, q, psi)

@@ -36,6 +36,29 @@ def test_top_k_mask():
     assert F.top_k_mask(sens, 0.4).tolist() == [False, True, False, True, False]
 
 
+def _topk_indices(v, k):
+    """torch.topk(v, k, largest=True).indices as a set, restated for tie-free v: the indices of
+    the k largest values (a full descending sort, the first k)."""
+    order = sorted(range(len(v)), key=lambda i: -float(v[i]))
+    return set(order[:k])
+
+
+@pytest.mark.parametrize("n,p", [(5, 0.5), (7, 0.3), (10, 0.25), (9, 0.95), (1000, 0.4), (3, 0.1),
+                                 (161, 0.1), (11, 1.0), (4, 0.0)])
+def test_top_k_mask_count_and_index_set(n, p):
+    """masking.py:17: k = int(len(vector) * p), the floor -- 5 * 0.5 = 2.5 -> 2, 7 * 0.3 -> 2,
+    9 * 0.95 = 8.55 -> 8 (round() would take one more) -- and the encrypted set is exactly
+    topk's index set on tie-free input."""
+    v = np.random.default_rng(n).permutation(n).astype(np.float64) * 0.37 + 0.01
+    mask = F.top_k_mask(v, p)
+    k = int(len(v) * p)
+    assert int(mask.sum()) == k
+    assert set(np.flatnonzero(mask).tolist()) == _topk_indices(v, k)
+    torch = pytest.importorskip("torch")
+    t = torch.from_numpy(v)
+    assert set(np.flatnonzero(mask).tolist()) == set(torch.topk(t, k, largest=True).indices.tolist())
+
+
 def test_flatten_roundtrip():
     torch = pytest.importorskip("torch")
     st = {"w": torch.randn(3, 4), "b": torch.randn(4)}

@@ -239,3 +239,94 @@ def test_arena_refuses_use_after_params_reload(tmp_path):
         ar.put(0, x)
     with pytest.raises(ValueError):
         ar.wavg([0.5, 0.5])
+
+
+def _raw_put(ck, ptr, C, Kk, learner, t):
+    return _lib.load().shelfi_dev_arena_put(ck._ctx, ctypes.c_void_p(t.data_ptr()), 0, Kk, learner, C,
+                                            ctypes.c_void_p(ptr), ctypes.c_void_p(D._stream_ptr(t)))
+
+
+def _raw_wavg(ck, ptr, w, Kk, out):
+    wf = (ctypes.c_float * len(w))(*w)
+    return _lib.load().shelfi_dev_wavg_arena(ck._ctx, ctypes.c_void_p(ptr), wf, len(w), Kk,
+                                             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(D._stream_ptr(out)))
+
+
+def test_stale_refusal_does_not_outlive_its_arena(c2):
+    """a refusal recorded for learner 5 of a C = 8 arena must not block a
+    C = 4 arena later laid over the same memory (the caching allocator hands freed ranges out
+    again): its first valid put supersedes the stale mark.  shelfi_dev_arena_release drops the
+    marks of a range explicitly (Arena.release / __del__)."""
+    inf = c2.info()
+    B = inf["batch"]
+    cts = [D.encrypt(c2, torch.tensor(x, device="cuda")) for x in _xs(4, K * B)]
+    lib = _lib.load()
+    w8 = lib.shelfi_arena_words(c2._ctx, 8, K)
+    mem = torch.empty(w8, dtype=torch.int64, device="cuda")
+    base = mem.data_ptr()
+    bad = cts[0].clone()
+    bad[0, 0, 0, 0] = -1
+    assert _raw_put(c2, base, 8, K, 5, bad) == _lib.SHELFI_ERR_FORMAT
+    out = torch.empty((K, 2, inf["num_towers"], inf["ring_dim"]), dtype=torch.int64, device="cuda")
+    assert _raw_wavg(c2, base, [0.125] * 8, K, out) == _lib.SHELFI_ERR_STATE
+    # the same memory as a C = 4 arena (learner 5 does not even exist there)
+    for i in range(4):
+        assert _raw_put(c2, base, 4, K, i, cts[i]) == 0, _err()
+    w = [0.1, 0.2, 0.3, 0.4]
+    assert _raw_wavg(c2, base, w, K, out) == 0, _err()
+    ref = O.wavg([c.cpu().numpy().view(np.uint64) for c in cts], w, np.array(inf["moduli"], np.uint64),
+                 inf["delta"])
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), ref)
+    # explicit release: a refused slot of a same-shaped arena is forgotten with its memory
+    assert _raw_put(c2, base, 4, K, 2, bad) == _lib.SHELFI_ERR_FORMAT
+    assert _raw_wavg(c2, base, w, K, out) == _lib.SHELFI_ERR_STATE
+    assert lib.shelfi_dev_arena_release(c2._ctx, ctypes.c_void_p(base), w8) == 0
+    assert _raw_put(c2, base, 4, K, 2, cts[2]) == 0
+    assert _raw_wavg(c2, base, w, K, out) == 0
+    ar = D.Arena(c2, 2, K)
+    with pytest.raises(m.ShelfiError):
+        ar.put(0, bad)
+    ar.release()
+    with pytest.raises(ValueError, match="released"):
+        ar.wavg([0.5, 0.5])
+
+
+def test_refused_header_marks_the_slot(c2, c2_other_key):
+    """a put_blob refused at its header (another key, wrong K, truncated) marks the
+    slot like a residue-level refusal, so the slot's previous round is not aggregated as if the
+    new upload had landed."""
+    B = c2.info()["batch"]
+    xs = _xs(2, K * B)
+    blobs = [c2.encrypt(x) for x in xs]
+    ar = D.Arena(c2, 2, K)
+    for i, b in enumerate(blobs):
+        ar.put(i, b)
+    w = [0.5, 0.5]
+    good = ar.wavg(w).cpu().numpy().view(np.uint64).copy()
+    with pytest.raises(m.ShelfiError, match="different key"):
+        ar.put(1, c2_other_key.encrypt(xs[1]))
+    with pytest.raises(m.ShelfiError, match="refused upload for learner 1"):
+        ar.wavg(w)
+    ar.put(1, blobs[1])
+    with pytest.raises(m.ShelfiError, match="length"):
+        ar.put(0, blobs[0][:-8])
+    with pytest.raises(m.ShelfiError, match="refused upload for learner 0"):
+        ar.wavg(w)
+    ar.put(0, blobs[0])
+    assert np.array_equal(ar.wavg(w).cpu().numpy().view(np.uint64), good)
+
+
+def test_blob_residues_refuses_a_shape_other_than_the_contexts(c2):
+    c2.set_wire_format("packed")
+    try:
+        blob = c2.encrypt(np.zeros(100))
+    finally:
+        c2.set_wire_format("shelfi")
+    inf = c2.info()
+    r = m.blob_residues(blob, inf["ring_dim"], inf["num_towers"], ckks=c2)
+    assert r.shape == (1, 2, inf["num_towers"], inf["ring_dim"])
+    with pytest.raises(ValueError, match="context"):
+        m.blob_residues(blob, inf["ring_dim"], inf["num_towers"] - 1, ckks=c2)
+    with pytest.raises(ValueError, match="context"):
+        m.blob_residues(blob, inf["ring_dim"] // 2, inf["num_towers"], ckks=c2)

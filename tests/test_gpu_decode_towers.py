@@ -88,3 +88,28 @@ def test_lower_level_decrypt(ck):
     _same(a, b)
     full = D.decrypt(ck, ct, B, inf["delta"]).cpu().numpy()
     _same(a, full)
+
+
+def test_prefix_decode_near_the_2_127_limit(tmp_path):
+    """the prefix decode's k estimate has the least headroom when the prefix modulus
+    is just above 2^130 and |X| is near 2^127.  A 60 + 36 + 36 (+ 37)-bit chain decodes over a
+    2^132 prefix (3 of 4 towers); 16 learners at x ~ 2^24 with weights 2^25 give a depth-2
+    aggregate with |X| ~ 2^125 (X / Q' ~ 2^-7).  Trimmed and all-tower decodes must agree bit
+    for bit and match the plaintext sum."""
+    d = str(tmp_path) + os.sep
+    c = m.CKKS("ckks", 1024, 36, d, multDepth=3, firstModBits=60, seed=17, decodeNoise=False)
+    assert c.genCryptoContextAndKeyGen() == 1
+    inf = c.info()
+    bits = [int(q).bit_length() for q in inf["moduli"]]
+    assert sum(bits[:2]) < 130 < sum(bits[:3])  # the decode keeps 3 towers
+    rng = np.random.default_rng(127)
+    n = inf["batch"]
+    xs = [rng.uniform(0.9, 1.0, n) * 2.0 ** 24 * rng.choice([-1.0, 1.0], n) for _ in range(16)]
+    xs = [np.sign(xs[0]) * np.abs(x) for x in xs]  # same sign per slot: the sum stays near the limit
+    w = [2.0 ** 25] * 16
+    agg = c.computeWeightedAverage([c.encrypt(x) for x in xs], w)
+    a, b = _both(lambda: np.asarray(c.decrypt(agg, n)))
+    _same(a, b)
+    ref = sum(wi * x for wi, x in zip(w, xs))
+    assert np.abs(ref).max() * inf["delta"] ** 2 > 2.0 ** 124
+    assert np.abs(a - ref).max() < 1e-6 * np.abs(ref).max()

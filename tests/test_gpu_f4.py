@@ -22,8 +22,10 @@ from SHELFI_FHE import device as D  # noqa: E402
 #   cfg2/3's ring (2^15, L = 4, two full digits), cfg4's (2^16, L = 6: three digits, 48 KiB of
 #   LDS in the inner-product pass), 2^11 (one NTT block: no columns passes), 2^17 (2^12-element
 #   blocks) and 30-bit scaling primes (q < 2^40: the towers the lazy one-step reduction skips)
-CASES = [(4096, 1, 52, 60), (4096, 2, 52, 60), (16384, 3, 52, 60), (32768, 5, 52, 60), (1024, 1, 52, 60),
-         (65536, 1, 52, 60), (4096, 1, 30, 40)]
+#   The L = 3 chain pins N = 2^13 explicitly: ParamsGen's own choice for it is 2^14 (log2(Q*P)
+#   = 164 + 120 bits), which the (16384, 3) case's ring already covers.
+CASES = [(4096, 1, 52, 60), (4096, 2, 52, 60, 8192), (16384, 3, 52, 60), (32768, 5, 52, 60),
+         (1024, 1, 52, 60), (65536, 1, 52, 60), (4096, 1, 30, 40)]
 
 
 def _u64(t):
@@ -32,8 +34,10 @@ def _u64(t):
 
 @pytest.fixture(scope="module", params=CASES, ids=lambda c: "b%d_d%d_s%d" % c[:3])
 def ctx(request):
-    batch, depth, sb, fb = request.param
-    c = m.CKKS("ckks", batch, sb, "", multDepth=depth, firstModBits=fb, seed=404 + depth, decodeNoise=False)
+    batch, depth, sb, fb = request.param[:4]
+    rd = request.param[4] if len(request.param) > 4 else 0
+    c = m.CKKS("ckks", batch, sb, "", multDepth=depth, firstModBits=fb, ringDim=rd, seed=404 + depth,
+               decodeNoise=False)
     assert c.genCryptoContextAndKeyGen() == 1
     c.evalMultKeyGen()
     inf = c.info()
@@ -106,7 +110,7 @@ def test_eval_key_import_gives_identical_products(ctx):
     c = ctx["c"]
     inf = ctx["inf"]
     other = m.CKKS("ckks", inf["batch"], inf["scale_bits"], "", multDepth=len(ctx["q"]) - 1,
-                   firstModBits=inf["first_mod_bits"], decodeNoise=False)
+                   firstModBits=inf["first_mod_bits"], ringDim=inf["ring_dim"], decodeNoise=False)
     pk, sk = c.get_keys()
     other.set_keys(pk, sk)
     with pytest.raises(RuntimeError, match="evaluation key"):

@@ -45,8 +45,7 @@ def test_library_is_gfx950_code_object():
 def test_params_generate_matches_oracle(batch, sb, depth, fb):
     N, q, psi = m.params_generate(batch, sb, depth, fb)
     L = depth + 1
-    logq = (fb if L > 1 else sb) + (L - 1) * sb
-    assert N == O.min_ring_dim(logq, batch)
+    assert N == O.ring_dim(L, sb, batch, fb)
     qo, psio = O.params_generate(N, L, sb, fb)
     assert q == [int(x) for x in qo]
     assert psi == [int(x) for x in psio]

@@ -25,7 +25,7 @@ def test_params_match_committed_context(d):
     q, psi = O.params_generate(8192, 2, 52, 60)
     assert [int(x) for x in q] == ctx["q"] == [0x0FFFFFFFFFFFC001, 0x0010000000060001]
     assert [int(x) for x in psi] == ctx["psi"] == [0x179C0F8FADCC, 0x10D0EF11890]
-    assert O.min_ring_dim(60 + 52, 4096) == 8192
+    assert O.ring_dim(2, 52, 4096) == 8192
 
 
 def test_context_scalars():
@@ -102,8 +102,8 @@ def test_extrapolated_chains():
     q6, _ = O.params_generate(1 << 16, 6, 52, 60)
     assert [int(x) for x in q6] == [0x0FFFFFFFFFFC0001, 0x0010000000200001, 0x000FFFFFFFE40001,
                                     0x0010000000180001, 0x000FFFFFFFF00001, 0x0010000000060001]
-    assert O.min_ring_dim(60 + 3 * 52, 16384) == 1 << 15
-    assert O.min_ring_dim(60 + 5 * 52, 32768) == 1 << 16
+    assert O.ring_dim(4, 52, 16384) == 1 << 15
+    assert O.ring_dim(6, 52, 32768) == 1 << 16
 
 
 def _direct_ntt(a, q, psi):

@@ -24,6 +24,7 @@ import pickle
 import numpy as np
 import pytest
 
+import oracle as O
 import palisade_fixture as P
 from conftest import PALISADE_DIR, PALISADE_PYBIND_DIR
 
@@ -143,18 +144,16 @@ def test_key_writer_reproduces_the_reference_files(d):
 CNN_KEYS = [("conv2d_1.weight", 800), ("conv2d_1.bias", 32), ("conv2d_2.weight", 51200),
             ("conv2d_2.bias", 64), ("linear_1.weight", 1605632), ("linear_1.bias", 512),
             ("linear_2.weight", 5120), ("linear_2.bias", 10)]
-# code/params_results.csv:2-16, "Communication" column per batch size (same for every
-# scale-bit setting: the ring stays 2^13 with 2 towers)
+# code/params_results.csv:2-16, "Communication" column: one value per batch size at every
+# scale-bit setting (14, 20, 33, 40, 52), so PALISADE kept N = 8192 with 2 towers on every row
+# of benchmark_crypto.py's sweep (:123-130)
 PICKLED_BYTES = {1024: 427260022, 2048: 214437402, 4096: 108157302}
+SWEEP = [(b, sb) for b in (1024, 2048, 4096) for sb in (14, 20, 33, 40, 52)]
 
 
-@pytest.mark.parametrize("batch", sorted(PICKLED_BYTES))
-def test_pickled_encrypt_archives_match_params_results(batch):
-    """benchmark_crypto.py:183-191: enc_learner_layer[0] (an OrderedDict key ->
-    encrypt() bytes) pickled with HIGHEST_PROTOCOL.  Residue values do not change sizes."""
-    N, q, psi, _, _ = _read_keys(PALISADE_DIR)
-    pub = open(os.path.join(PALISADE_DIR, "key-public.txt"), "rb").read()
-    ctx_obj, tag = m.palisade_key_context(pub)
+def _pickled_cnn_archives(N, q, ctx_obj, tag, batch):
+    """benchmark_crypto.py:183-191: enc_learner_layer[0] (an OrderedDict key -> encrypt()
+    bytes) pickled with HIGHEST_PROTOCOL.  Residue values do not change sizes."""
     L, delta = len(q), float(q[-1])
     od = collections.OrderedDict()
     for k, n in CNN_KEYS:
@@ -162,7 +161,45 @@ def test_pickled_encrypt_archives_match_params_results(batch):
         r = np.zeros((K, 2, L, N), np.uint64)
         od[k] = m.palisade_write(ctx_obj, tag, q, r, depth=1, level=0, scale=delta, key_params=True)
     assert sum(math.ceil(n / batch) for _, n in CNN_KEYS) == {4096: 412, 2048: 817, 1024: 1628}[batch]
-    assert len(pickle.dumps(od, protocol=pickle.HIGHEST_PROTOCOL)) == PICKLED_BYTES[batch]
+    return len(pickle.dumps(od, protocol=pickle.HIGHEST_PROTOCOL))
+
+
+@pytest.mark.parametrize("batch", sorted(PICKLED_BYTES))
+def test_pickled_encrypt_archives_match_params_results(batch):
+    """The committed keys' context (batch 4096, 52 bits) at each batch's ciphertext count."""
+    N, q, psi, _, _ = _read_keys(PALISADE_DIR)
+    pub = open(os.path.join(PALISADE_DIR, "key-public.txt"), "rb").read()
+    ctx_obj, tag = m.palisade_key_context(pub)
+    assert _pickled_cnn_archives(N, q, ctx_obj, tag, batch) == PICKLED_BYTES[batch]
+
+
+@pytest.mark.parametrize("batch,sb", SWEEP)
+def test_sweep_contexts_match_params_results(batch, sb):
+    """Every row of code/params_results.csv:2-16 through this library's ParamsGen:
+    genCryptoContextCKKS(1, sb, batch) (ckks.cpp:26-28) must land on N = 8192 (the ring
+    bounds log2(Q*P) with the HYBRID special primes, not log2 Q), and one client's pickled
+    CNN_OriginalFedAvg archives under the context genCryptoContextAndKeyGen writes for it
+    must have exactly the recorded byte count.  The oracle's rule (or_ring_dim) agrees."""
+    N, q, psi = m.params_generate(batch, sb, 1)
+    assert N == 8192 and len(q) == 2
+    assert O.ring_dim(2, sb, batch) == 8192
+    qo, psio = O.params_generate(N, 2, sb, 60)
+    assert q == [int(x) for x in qo] and psi == [int(x) for x in psio]
+    # the last tower is FirstPrime(sb, 2N): 17 and 21 bits at 14 and 20 (65537, 0x10c001)
+    assert q[1] == {14: 0x10001, 20: 0x10C001}.get(sb, q[1]) and q[1].bit_length() >= sb
+    ctx_file = m.palisade_context_file(N, q, psi, sb, batch)
+    ctx_obj = m.palisade_embed_context(ctx_file)
+    assert _pickled_cnn_archives(N, q, ctx_obj, "0123456789abcdef" * 2, batch) == PICKLED_BYTES[batch]
+    if (batch, sb) == (4096, 52):  # the committed context, byte for byte
+        assert ctx_file == open(os.path.join(PALISADE_DIR, "cryptocontext.txt"), "rb").read()
+
+
+def test_log_q_alone_would_contradict_params_results():
+    """The rule fixed in round 4: bounding log2 Q alone picks N = 4096 on 8 of the 15 rows,
+    whose archives would be about half the recorded size."""
+    wrong = [(b, sb) for b, sb in SWEEP if O.min_ring_dim(60 + sb, b) != 8192]
+    assert len(wrong) == 8 and all(b in (1024, 2048) and sb < 52 for b, sb in wrong)
+    assert all(O.ring_dim(2, sb, b) == 8192 for b, sb in SWEEP)
 
 
 @pytest.mark.parametrize("K", [1, 3])
