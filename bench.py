@@ -780,7 +780,9 @@ def main():
         with open(args.encdec_traffic_json) as f:
             et = json.load(f)
         if args.workload in ("cfg3", "cfg2", "cfg5"):  # 2^15 / L4: the parameters it was measured at
-            for name in ("encrypt", "decrypt"):
+            for name in ("encrypt", "decrypt", "decrypt_flooded"):
+                if name not in et:
+                    continue
                 res[name + "_traffic"] = {
                     "hbm_bytes_per_ct": round(et[name]["hbm_bytes_per_ct"]),
                     "algorithmic_bytes_per_ct": et["algorithmic_bytes_per_ct"],

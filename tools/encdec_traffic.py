@@ -14,8 +14,23 @@ import statistics
 
 ENCRYPT = ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
            "ntt_fwd_blocks_enc")
-DECRYPT = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
-           "fft_fwd_blocks<false>", "fft_fwd_cols")
+_DEC_COMMON = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
+               "fft_fwd_cols")
+# the decode FFT's first pass is a template over FLOOD: fft_fwd_blocks<bool> (LDS loops) or
+# fft_fwd_blocks_ct<BL, K1..K4, bool> (register chunks, the default since round 3).  The exact
+# decrypt counts the `false` instantiations, the flooded one the `true` ones plus the sigma pass.
+DECRYPT = _DEC_COMMON + ("fft_fwd_blocks<false>", "fft_fwd_blocks_ct<@false>")
+DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks<true>", "fft_fwd_blocks_ct<@true>", "decode_stats_kernel",
+                                 "decode_flood_kernel")
+
+
+def _matches(full, n):
+    """`prefix@flag`: a template whose name starts with prefix and whose last argument is flag."""
+    if "@" in n:
+        pre, flag = n.rstrip(">").split("@")
+        head = full.split("(")[0]
+        return head.startswith(pre) and head.rstrip().endswith(", " + flag + ">")
+    return full.startswith(n) or n in full
 
 
 def per_kernel(path, counter):
@@ -32,7 +47,7 @@ def chain(fetch, write, names):
     for k in sorted(set(fetch) | set(write)):
         short = k.split("(")[0].replace("void ", "").replace("shelfi::", "")
         full = k.replace("void ", "").replace("shelfi::", "")
-        if not any(full.startswith(n) or n in full for n in names):
+        if not any(_matches(full, n) for n in names):
             continue
         b = 2.0 * fetch.get(k, 0.0) * 1024 + write.get(k, 0.0) * 1024
         out[short] = b
@@ -52,12 +67,12 @@ def main():
     f, w = per_kernel(a.fetch_csv, "FETCH_SIZE"), per_kernel(a.write_csv, "WRITE_SIZE")
     res = {"cts_per_call": a.cts, "algorithmic_bytes_per_ct": a.bytes_per_ct,
            "correction": "2*FETCH_SIZE + WRITE_SIZE per kernel (KiB -> B), median over dispatches"}
-    for name, names in (("encrypt", ENCRYPT), ("decrypt", DECRYPT)):
+    for name, names in (("encrypt", ENCRYPT), ("decrypt", DECRYPT), ("decrypt_flooded", DECRYPT_FLOODED)):
         ks, tot = chain(f, w, names)
         res[name] = {"kernels_bytes_per_call": ks, "hbm_bytes_per_ct": tot / a.cts,
                      "traffic_over_algorithmic": tot / a.cts / a.bytes_per_ct}
     json.dump(res, open(a.out, "w"), indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k in ("encrypt", "decrypt")}, indent=1))
+    print(json.dumps({k: v for k, v in res.items() if k in ("encrypt", "decrypt", "decrypt_flooded")}, indent=1))
 
 
 if __name__ == "__main__":
