@@ -76,6 +76,11 @@ def parse():
                          "modq; shelfi = the library's own RCCL communicator through the C ABI, the same "
                          "pipeline in one call (shelfi_dev_combine_arena: wavg pieces on the caller's "
                          "stream, reduce_scatter pieces on the library's comm stream)")
+    ap.add_argument("--exchange", choices=["sum", "packed"], default="sum",
+                    help="learner-sharded combine's exchange: sum = uint64 SUM reduce_scatter of the "
+                         "partials (+ mod-q fold); packed = the partials written packed (sum_t U_t bits "
+                         "per coefficient), an all-to-all, and a local unit-weight sum (DESIGN.md §6). "
+                         "At N > 1 the other one is measured in the same run (alternative_exchange)")
     ap.add_argument("--shelfi-fold", action="store_true",
                     help="--combine shelfi: fold each piece mod q after its collective (default: leave "
                          "the sums to the consumer, shelfi_dev_decrypt_sum folds them on load)")
@@ -121,7 +126,7 @@ class ShelfiCombine:
     host without PyTorch.  fold=False leaves the share as uint64 sums of the W partials: the
     mod-q fold happens in the consumer (shelfi_dev_decrypt_sum), not in a separate pass."""
 
-    def __init__(self, ck, arena, weights, K, pieces, dev, fold=False):
+    def __init__(self, ck, arena, weights, K, pieces, dev, fold=False, packed=False):
         import torch
         import torch.distributed as dist
 
@@ -130,16 +135,26 @@ class ShelfiCombine:
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.comm = SD.Comm(ck, self.rank, self.world)
-        self.arena, self.weights, self.K, self.pieces, self.fold = arena, weights, K, pieces, fold
+        self.arena, self.weights, self.K, self.pieces, self.packed = arena, weights, K, pieces, packed
+        self.fold = fold or packed  # the packed exchange's unit-weight sum folds
         self.Ks = self.comm.share_cts(K)
         shape = (2, arena.L, arena.N)
-        self.send = torch.empty((self.world * self.Ks,) + shape, dtype=torch.int64, device=dev)
+        if packed:  # shelfi_dev_combine_arena_packed: packed send / receive buffers
+            nw = self.comm.packed_buffer_words(K)
+            self.send = torch.empty(nw, dtype=torch.int64, device=dev)
+            self.recv = torch.empty(nw, dtype=torch.int64, device=dev)
+        else:
+            self.send = torch.empty((self.world * self.Ks,) + shape, dtype=torch.int64, device=dev)
         self.share = torch.empty((self.Ks,) + shape, dtype=torch.int64, device=dev)
-        self.terms = 1 if fold else self.world  # residues of the share: sums of `terms` residues
+        self.terms = 1 if self.fold else self.world  # residues of the share: sums of `terms` residues
 
     def run(self, compute_piece=None, fold_share=None):
-        self.comm.combine_arena(self.arena, self.weights, self.K, self.send, self.share, pieces=self.pieces,
-                                fold=self.fold)
+        if self.packed:
+            self.comm.combine_arena_packed(self.arena, self.weights, self.K, self.send, self.recv, self.share,
+                                           pieces=self.pieces)
+        else:
+            self.comm.combine_arena(self.arena, self.weights, self.K, self.send, self.share, pieces=self.pieces,
+                                    fold=self.fold)
         a, b = self.rank * self.Ks, min(self.K, (self.rank + 1) * self.Ks)
         return [(a, b, self.share[:b - a])] if b > a else []
 
@@ -357,12 +372,23 @@ def main():
                          "chosen": cand_ms.index(min(cand_ms))}
         else:
             out = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
-        if shard == "learners" and args.combine == "torch":
-            comb = SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
-        elif shard == "learners":
+        def make_comb(exchange):
+            """The learner-sharded combine: torch.distributed or the C ABI, uint64 SUM
+            reduce_scatter or the packed share exchange."""
+            if exchange == "packed" and args.layout != "arena":
+                raise SystemExit("--exchange packed aggregates the resident arena (--layout arena)")
+            if args.combine == "torch" and exchange == "sum":
+                return SD.PipelinedCombine(K, (2, L, N), pieces=args.pieces, device=dev)
+            if args.combine == "torch":
+                return SD.PackedPipelinedCombine(K, (2, L, N), D.packed_words(ck, 1), pieces=args.pieces,
+                                                 device=dev)
             if args.layout != "arena":
                 raise SystemExit("--combine shelfi aggregates the resident arena (--layout arena)")
-            comb = ShelfiCombine(ck, arena, weights, K, args.pieces, dev, fold=args.shelfi_fold)
+            return ShelfiCombine(ck, arena, weights, K, args.pieces, dev, fold=args.shelfi_fold,
+                                 packed=exchange == "packed")
+
+        if shard == "learners":
+            comb = make_comb(args.exchange)
 
         def kernel_into(dst):
             if args.layout == "arena":
@@ -379,18 +405,30 @@ def main():
             else:
                 D.wavg(ck, [c[k0:k1] for c in cts], weights, out=view)
 
-        def step():
-            if comb is None:
-                kernel()
-                return [(k_lo, k_hi, out)]
-            return comb.run(piece, lambda s_: D.modq(ck, s_))
+        def piece_packed(k0, k1, words):
+            arena.wavg_packed(weights, out=words, k0=k0, k1=k1)
+
+        def sum_share(stk, G, n, stride, share):
+            D.sum_packed(ck, stk, G, n, stride, out=share)
+
+        def step_of(cb):
+            def step():
+                if cb is None:
+                    kernel()
+                    return [(k_lo, k_hi, out)]
+                if isinstance(cb, SD.PackedPipelinedCombine):
+                    return cb.run(piece_packed, sum_share)
+                return cb.run(piece, lambda s_: D.modq(ck, s_))
+            return step
+
+        step = step_of(comb)
 
         # the launch's input bytes: the packed arena or C uint64 batches
         in_bytes = arena.buf.numel() * 8 if args.layout == "arena" else C_loc * K_loc * 2 * L * N * 8
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
                 "in_bytes": in_bytes,
                 "enc_times": enc_times, "kernel": kernel, "kernel_into": kernel_into, "step": step, "piece": piece, "comb": comb, "weights": weights,
-                "cts": cts, "placement": placement}
+                "cts": cts, "placement": placement, "make_comb": make_comb, "step_of": step_of}
 
     def timed(mode):
         """warmup, then exactly `steps` steps between barrier + sync; max over ranks.
@@ -528,6 +566,26 @@ def main():
         if not args.no_check:
             alt["check"] = checked(alt_mode)
         del alt_mode
+        torch.cuda.empty_cache()
+    # the other exchange of the learner-sharded combine (uint64 SUM reduce_scatter vs the packed
+    # share all-to-all), on the same arena, measured in the same run: the 8-GPU run picks
+    alt_x = None
+    if distributed and not args.no_alt and main_mode["shard"] == "learners":
+        other = "packed" if args.exchange == "sum" else "sum"
+        try:
+            cb2 = main_mode["make_comb"](other)
+            xm = dict(main_mode, comb=cb2, step=main_mode["step_of"](cb2))
+            x_el, _, _ = timed(xm)
+            alt_x = {"exchange": other, "combine": args.combine,
+                     "value": round(units / (x_el / args.steps), 1), "unit": "client-ciphertexts/s",
+                     "ms_per_step": round(x_el * 1e3 / args.steps, 4)}
+            if not args.no_check:
+                alt_x["check"] = checked(xm)
+            del xm, cb2
+        except SystemExit:
+            raise
+        except Exception as e:  # reported, never fatal to the headline
+            alt_x = {"exchange": other, "error": repr(e)[:300]}
         torch.cuda.empty_cache()
     out, K_loc, C_loc = main_mode["out"], main_mode["K_loc"], main_mode["C_loc"]
     enc_times, cts, weights = main_mode["enc_times"], main_mode["cts"], main_mode["weights"]
@@ -767,7 +825,10 @@ def main():
                                    if args.combine == "torch" or args.shelfi_fold else
                                    "learner-sharded dp%d + RCCL reduce_scatter over xGMI (C ABI; fold in decrypt)"
                                    % world),
-                   "layout": args.layout, "output_placement": main_mode["placement"]},
+                   "layout": args.layout, "output_placement": main_mode["placement"],
+                   "exchange": None if not distributed or cts_mode else
+                   ("uint64 SUM reduce_scatter" if args.exchange == "sum" else
+                    "packed partials (sum_t U_t bits/coeff) all-to-all + unit-weight sum")},
         "roofline": roofline,
         "encode_encrypt_ms_per_ct": round(enc_ms, 5),
         "encode_encrypt_per_learner_call_ms_per_ct": round(enc_first_ms, 5),
@@ -816,6 +877,8 @@ def main():
         res["check"] = check
     if alt:
         res["alternative_partitioning"] = alt
+    if alt_x:
+        res["alternative_exchange"] = alt_x
     if api:
         res["api_bytes_path"] = api
     if f4:

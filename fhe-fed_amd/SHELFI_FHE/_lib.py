@@ -124,6 +124,10 @@ SIGNATURES = {
     "shelfi_dev_arena_put_blob": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_arena_release": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "shelfi_dev_wavg_arena_packed": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
+                                               C.c_void_p]),
+    "shelfi_dev_sum_packed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p,
+                                        C.c_void_p]),
     "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
     "shelfi_dev_wavg_arena_pick_output": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t,
@@ -140,6 +144,8 @@ SIGNATURES = {
     "shelfi_combine_share_cts": (C.c_size_t, [C.c_void_p, C.c_size_t]),
     "shelfi_dev_combine_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_size_t,
                                            C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "shelfi_dev_combine_arena_packed": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "shelfi_dev_encrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "shelfi_dev_decrypt": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_size_t,
                                      C.c_void_p, C.c_void_p]),

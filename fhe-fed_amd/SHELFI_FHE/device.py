@@ -173,6 +173,28 @@ class Arena:
         return out
 
 
+    def wavg_packed(self, weights: Sequence[float], out=None, k0: int = 0, k1: int | None = None):
+        """wavg() with the aggregate written packed (the slice format with C = 1; a flat int64
+        tensor of packed_words(k1 - k0) words): the packed share exchange's send form."""
+        torch = _torch()
+        self._check_gen()
+        if len(weights) != self.C:
+            raise ValueError("need one weight per learner")
+        k1 = self.K if k1 is None else int(k1)
+        if not (0 <= k0 <= k1 <= self.K):
+            raise ValueError("bad ciphertext range")
+        need = packed_words(self.ckks, k1 - k0)
+        if out is None:
+            out = torch.empty(need, dtype=torch.int64, device=self.buf.device)
+        if not out.is_cuda or out.dtype != torch.int64 or out.numel() < need or not out.is_contiguous():
+            raise ValueError("out must be a contiguous int64 CUDA tensor of >= %d words" % need)
+        w = (C.c_float * self.C)(*[float(x) for x in weights])
+        base = self.buf.data_ptr() + k0 * self.ct_words * 8
+        check(_lib.load().shelfi_dev_wavg_arena_packed(self.ckks._ctx, C.c_void_p(base), w, self.C, k1 - k0,
+                                                       C.c_void_p(out.data_ptr()),
+                                                       C.c_void_p(_stream_ptr(out))), "dev_wavg_arena_packed")
+        return out
+
     def place_output(self, weights: Sequence[float], candidates: int = 8, launches: int = 2, include=()):
         """A [K][2][L][N] output buffer placed well for this arena.  The launch time
         depends on where the output lands in physical HBM relative to the arena (up to
@@ -197,6 +219,28 @@ class Arena:
         out = cands[best.value]
         del cands
         return out, [round(float(x), 4) for x in ms]
+
+
+def packed_words(ckks, K: int) -> int:
+    """64-bit words of K ciphertexts in the packed C = 1 slice format (the packed wire / exchange)."""
+    return int(_lib.load().shelfi_arena_words(ckks._ctx, 1, int(K)))
+
+
+def sum_packed(ckks, stacked, G: int, K: int, stride: int, out=None):
+    """sum_g x_g mod q_t of G packed (C = 1) batches of K ciphertexts stacked `stride` words apart
+    in the int64 tensor `stacked` -> [K][2][L][N] (shelfi_dev_sum_packed)."""
+    torch = _torch()
+    if not stacked.is_cuda or stacked.dtype != torch.int64 or not stacked.is_contiguous():
+        raise ValueError("stacked must be a contiguous int64 CUDA tensor")
+    if K and (stride < packed_words(ckks, K) or stacked.numel() < (G - 1) * stride + packed_words(ckks, K)):
+        raise ValueError("stacked is smaller than G batches of K ciphertexts at that stride")
+    if out is None:
+        out = empty_ct(ckks, K, device=stacked.device)
+    _check_ct(out, ckks, K)
+    check(_lib.load().shelfi_dev_sum_packed(ckks._ctx, C.c_void_p(stacked.data_ptr()), int(G), int(K), int(stride),
+                                            C.c_void_p(out.data_ptr()), C.c_void_p(_stream_ptr(out))),
+          "dev_sum_packed")
+    return out
 
 
 def modq(ckks, buf):

@@ -170,6 +170,66 @@ class PipelinedCombine:
         return owned
 
 
+class PackedPipelinedCombine:
+    """PipelinedCombine with the packed share exchange (round 4) instead of the
+    uint64 SUM reduce_scatter.  Piece [k0, k1) of every rank's partial is written packed -- the
+    arena's slice format with C = 1, sum_t U_t bits per coefficient (218 of 256 at 2^15 / L4) --
+    into a send buffer of `world` equal chunks; one all_to_all_single hands chunk h to rank h;
+    rank h sums the `world` chunks it received with unit weights (EvalAdd, mod q) into its share.
+    Per rank (world - 1) / world of the packed partial crosses the links instead of the uint64
+    one; the result is bit-identical to the reduce_scatter combine and to one process.
+    `packed_words_per_ct` is the packed size of one ciphertext in 64-bit words
+    (shelfi_arena_words(ctx, 1, 1))."""
+
+    def __init__(self, K: int, ct_shape, packed_words_per_ct: int, pieces: int = 4, device=None, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > max_world():
+            raise ValueError("more than %d ranks: the unit-weight sum takes at most %d partials"
+                             % (max_world(), max_world()))
+        self.K, self.pw = K, int(packed_words_per_ct)
+        self.pieces = pipeline_pieces(K, self.world, pieces)
+        self.padded = [-(-(k1 - k0) // self.world) * self.world for k0, k1 in self.pieces]
+        tot = sum(self.padded)
+        # zero padding (packed zeros are zero residues) is written only here
+        self.send = torch.zeros(tot * self.pw, dtype=torch.int64, device=device)
+        self.recv = torch.empty(tot * self.pw, dtype=torch.int64, device=device)
+        self.sends, self.recvs, self.shares, off = [], [], [], 0
+        for (k0, k1), p in zip(self.pieces, self.padded):
+            self.sends.append(self.send[off * self.pw:(off + p) * self.pw])
+            self.recvs.append(self.recv[off * self.pw:(off + p) * self.pw])
+            self.shares.append(torch.empty((p // self.world,) + tuple(ct_shape), dtype=torch.int64, device=device))
+            off += p
+
+    owned_ranges = PipelinedCombine.owned_ranges
+
+    def run(self, compute_piece_packed, sum_share):
+        """compute_piece_packed(k0, k1, out_words) writes the packed local partial of ciphertexts
+        [k0, k1) into out_words[:(k1 - k0) * pw]; sum_share(stacked, world, n, stride, out) sums
+        `world` packed batches of n ciphertexts stride words apart into out[:n] (canonical).
+        Returns [(k0, k1, share_view)] owned by this rank."""
+        import torch.distributed as dist
+
+        works = []
+        for (k0, k1), snd, rcv in zip(self.pieces, self.sends, self.recvs):
+            compute_piece_packed(k0, k1, snd[:(k1 - k0) * self.pw])
+            works.append(dist.all_to_all_single(rcv, snd, group=self.group, async_op=True))
+        owned = []
+        for (k0, k1), p, rcv, share, w in zip(self.pieces, self.padded, self.recvs, self.shares, works):
+            w.wait()
+            per = p // self.world
+            a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
+            if b > a:
+                sv = share[:b - a]
+                sum_share(rcv, self.world, b - a, per * self.pw, sv)
+                owned.append((a, b, sv))
+        return owned
+
+
 def slice_of_rank(K: int, world: int, rank: int):
     """Ciphertext range [start, stop) a rank holds after reduce_scatter (equal padded
     slices, the last rank possibly shorter)."""
@@ -276,6 +336,33 @@ class Comm:
                    C.c_void_p(send.data_ptr()), C.c_void_p(share.data_ptr()), 1 if fold else 0,
                    C.c_void_p(_stream_ptr(share)))
         return share
+
+    def combine_arena_packed(self, arena, weights, K: int, send, recv, share, pieces: int = 8):
+        """combine_arena with the packed share exchange (shelfi_dev_combine_arena_packed): the
+        pieces' partials are written packed, exchanged by a grouped send/recv all-to-all and
+        summed on the comm stream.  `send`/`recv` are int64 scratch of
+        shelfi_arena_words(ctx, 1, world * share_cts(K)) words each (packed_buffer_words)."""
+        import ctypes as C
+        from .device import _check_ct, _stream_ptr
+
+        Ks = self.share_cts(K)
+        _check_ct(share, self._ckks, Ks)
+        need = self.packed_buffer_words(K)
+        for b in (send, recv):
+            if not b.is_cuda or b.dtype.itemsize != 8 or b.numel() < need or not b.is_contiguous():
+                raise ValueError("send/recv must be contiguous 64-bit CUDA buffers of >= %d words" % need)
+        if len(weights) != arena.C or arena.K != K:
+            raise ValueError("one weight per arena learner, and the arena's K")
+        w = (C.c_float * arena.C)(*[float(x) for x in weights])
+        self._call("shelfi_dev_combine_arena_packed", C.c_void_p(arena.buf.data_ptr()), w, arena.C, int(K),
+                   int(pieces), C.c_void_p(send.data_ptr()), C.c_void_p(recv.data_ptr()),
+                   C.c_void_p(share.data_ptr()), C.c_void_p(_stream_ptr(share)))
+        return share
+
+    def packed_buffer_words(self, K: int) -> int:
+        from ._lib import load
+
+        return int(load().shelfi_arena_words(self._ckks._ctx, 1, self.world * self.share_cts(K)))
 
     def close(self):
         if self._ckks is not None and self._ckks._ctx:

@@ -632,6 +632,7 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
       if (ctx->wl_done[i]) (void)hipEventDestroy(ctx->wl_done[i]);
       if (ctx->wl_dev[i]) (void)hipFree(ctx->wl_dev[i]);
     }
+    dfree_t(ctx->unit_wl);
     dfree(ctx->scratch);
     dfree(ctx->io);
     dfree_t(ctx->dev_flag);
@@ -1648,6 +1649,37 @@ void wavg_arena_enqueue(shelfi_ctx* ctx, const uint64_t* arena_dev, const float*
   SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], s));
 }
 
+// The same aggregation with its result written in the packed C = 1 layout (the packed share
+// exchange's send buffer): out_packed receives K ciphertexts, arena_ct_words(p, 1) words each.
+void wavg_arena_enqueue_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                               uint64_t* out_packed, hipStream_t s) {
+  const Params& p = ctx->p;
+  const int slot = arena_weight_slot(ctx, w, C, s);
+  launch_wavg_packed_ex(reinterpret_cast<const uint32_t*>(arena_dev), ctx->wl_dev[slot], (uint32_t)C, (uint32_t)C,
+                        0, (uint64_t)K * 2 * p.L, p.L, p.logN, arena_pack(p), ctx->dt.tc, nullptr,
+                        reinterpret_cast<uint32_t*>(out_packed), s);
+  SHELFI_HIP(hipEventRecord(ctx->wl_done[slot], s));
+}
+
+// sum_g x_g mod q_t over G packed C = 1 batches of K ciphertexts stacked `stride` uint64 words apart
+// (the packed share exchange's receive buffer) -> uint64 [K][2][L][N] canonical: wavg_packed with
+// unit weight limbs (w0 = 1, w1 = 0), so the fold is the mod-q reduction.
+void sum_packed_enqueue(shelfi_ctx* ctx, const uint64_t* stacked, size_t G, size_t K, size_t stride,
+                        uint64_t* out, hipStream_t s) {
+  const Params& p = ctx->p;
+  if (!G || G > (size_t)kMaxCommRanks) throw Error{SHELFI_ERR_ARG, "sum_packed: 1..16 batches"};
+  if (stride < (size_t)arena_ct_words(p, 1) * K) throw Error{SHELFI_ERR_ARG, "sum_packed: stride below the batch"};
+  if (!ctx->unit_wl) {
+    std::vector<uint32_t> one((size_t)kMaxCommRanks * kMaxTowers * 2, 0);
+    for (size_t i = 0; i < one.size(); i += 2) one[i] = 1;
+    SHELFI_HIP(hipMalloc(&ctx->unit_wl, one.size() * sizeof(uint32_t)));
+    SHELFI_HIP(hipMemcpy(ctx->unit_wl, one.data(), one.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  if (!K) return;
+  launch_wavg_packed_ex(reinterpret_cast<const uint32_t*>(stacked), ctx->unit_wl, (uint32_t)G, 1, 2ull * stride,
+                        (uint64_t)K * 2 * p.L, p.L, p.logN, arena_pack(p), ctx->dt.tc, out, nullptr, s);
+}
+
 void check_wavg_weights(const float* w, size_t C, double delta) { check_weights(w, C, delta); }
 }  // namespace shelfi
 
@@ -1756,6 +1788,29 @@ int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const floa
     arena_require_valid_locked(ctx, arena_dev, (size_t)arena_ct_words(ctx->p, C) * K);
     DeviceGuard g(ctx->device);
     wavg_arena_enqueue(ctx, arena_dev, w, C, K, out_dev, (hipStream_t)stream);
+  });
+}
+
+int shelfi_dev_wavg_arena_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                                 uint64_t* out_packed, void* stream) {
+  if (!ctx || (K && !out_packed) || (C && (!arena_dev || !w))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    if (!C) throw Error{SHELFI_ERR_ARG, "no learners"};
+    check_weights(w, C, ctx->p.delta);
+    arena_require_valid_locked(ctx, arena_dev, (size_t)arena_ct_words(ctx->p, C) * K);
+    DeviceGuard g(ctx->device);
+    wavg_arena_enqueue_packed(ctx, arena_dev, w, C, K, out_packed, (hipStream_t)stream);
+  });
+}
+
+int shelfi_dev_sum_packed(shelfi_ctx* ctx, const uint64_t* stacked, size_t G, size_t K, size_t stride_words,
+                          uint64_t* out_dev, void* stream) {
+  if (!ctx || (K && (!stacked || !out_dev))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    DeviceGuard g(ctx->device);
+    sum_packed_enqueue(ctx, stacked, G, K, stride_words, out_dev, (hipStream_t)stream);
   });
 }
 

@@ -35,6 +35,10 @@ struct Rccl {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclReduceScatter) reduce_scatter = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   std::string load_error;
 };
 
@@ -65,6 +69,10 @@ const Rccl& rccl() {
     SHELFI_SYM(all_reduce, ncclAllReduce)
     SHELFI_SYM(reduce_scatter, ncclReduceScatter)
     SHELFI_SYM(error_string, ncclGetErrorString)
+    SHELFI_SYM(send, ncclSend)
+    SHELFI_SYM(recv, ncclRecv)
+    SHELFI_SYM(group_start, ncclGroupStart)
+    SHELFI_SYM(group_end, ncclGroupEnd)
 #undef SHELFI_SYM
   });
   if (!r.handle) throw Error{SHELFI_ERR_DEVICE, "RCCL unavailable: " + r.load_error};
@@ -279,6 +287,72 @@ int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const f
       uint64_t* dst = share_dev + kj0 * ctw;
       check(rccl().reduce_scatter(send, dst, kn * ctw, ncclUint64, ncclSum, c, cs), "ncclReduceScatter");
       if (fold) launch_modq(dst, (uint64_t)kn * 2 * p.L, p.L, p.logN, ctx->dt.tc, cs);
+    }
+    SHELFI_HIP(hipEventRecord(ctx->comm_events[P], cs));
+    SHELFI_HIP(hipStreamWaitEvent(s, ctx->comm_events[P], 0));  // the share is ready on `stream`
+  });
+}
+
+// The packed share exchange (round 4): the same pieces as
+// shelfi_dev_combine_arena, but each rank's partial of piece j is written PACKED (the C = 1 slice
+// format, sum_t U_t bits per coefficient: 218 of 256 at 2^15 / L4) into send [W][kn], exchanged by
+// one grouped ncclSend / ncclRecv all-to-all (rank h's block of every rank lands in recv [W][kn]),
+// and summed locally with unit weights (sum_packed_enqueue: the mod-q fold included) into share.
+// The xGMI bytes per rank are (W - 1) / W of the packed partial instead of the uint64 one (0.85x at
+// 2^15 / L4); the local sum reads W packed blocks and writes the uint64 share.  Bit-identical to the
+// reduce-scatter combine (EvalAdd is order-independent).  send and recv hold W * Ks packed
+// ciphertexts (shelfi_arena_words(ctx, 1, W * Ks) uint64 words each).
+int shelfi_dev_combine_arena_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                                    size_t pieces, uint64_t* send_dev, uint64_t* recv_dev, uint64_t* share_dev,
+                                    void* stream) {
+  if (!ctx || !w || !C || (K && (!arena_dev || !send_dev || !recv_dev || !share_dev))) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return guarded_comm([&] {
+    ncclComm_t c = comm_of(ctx);
+    check_wavg_weights(w, C, ctx->p.delta);
+    const Params& p = ctx->p;
+    const size_t ctw = 2ull * p.L * p.N;
+    const size_t pcw = (size_t)arena_ct_words(p, 1);  // packed uint64 words per ciphertext (C = 1)
+    const size_t acw = (size_t)arena_ct_words(p, C);
+    arena_require_valid_locked(ctx, arena_dev, acw * K);
+    if (!K) return;
+    DevGuard g(ctx->device);
+    const size_t W = (size_t)ctx->comm_world;
+    const size_t Ks = (K + W - 1) / W;
+    const size_t P = std::max<size_t>(1, std::min(pieces ? pieces : 1, Ks));
+    const size_t Kp = (Ks + P - 1) / P;
+    hipStream_t s = (hipStream_t)stream;
+    if (!ctx->comm_stream) SHELFI_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    while (ctx->comm_events.size() < P + 1) {
+      hipEvent_t e = nullptr;
+      SHELFI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->comm_events.push_back(e);
+    }
+    hipStream_t cs = ctx->comm_stream;
+    SHELFI_HIP(hipEventRecord(ctx->comm_events[P], s));
+    SHELFI_HIP(hipStreamWaitEvent(cs, ctx->comm_events[P], 0));
+    for (size_t j = 0; j < P; ++j) {
+      const size_t kj0 = j * Kp;
+      if (kj0 >= Ks) break;
+      const size_t kn = std::min(Kp, Ks - kj0);
+      uint64_t* send = send_dev + W * kj0 * pcw;  // [W][kn] packed ciphertexts
+      uint64_t* recv = recv_dev + W * kj0 * pcw;
+      for (size_t gr = 0; gr < W; ++gr) {
+        const size_t a = gr * Ks + kj0;
+        const size_t cnt = a < K ? std::min(kn, K - a) : 0;
+        if (cnt) wavg_arena_enqueue_packed(ctx, arena_dev + a * acw, w, C, cnt, send + gr * kn * pcw, s);
+        if (cnt < kn)  // padding past K: packed zeros, the additive identity
+          SHELFI_HIP(hipMemsetAsync(send + (gr * kn + cnt) * pcw, 0, (kn - cnt) * pcw * 8, s));
+      }
+      SHELFI_HIP(hipEventRecord(ctx->comm_events[j], s));
+      SHELFI_HIP(hipStreamWaitEvent(cs, ctx->comm_events[j], 0));
+      check(rccl().group_start(), "ncclGroupStart");
+      for (size_t h = 0; h < W; ++h) {
+        check(rccl().send(send + h * kn * pcw, kn * pcw, ncclUint64, (int)h, c, cs), "ncclSend");
+        check(rccl().recv(recv + h * kn * pcw, kn * pcw, ncclUint64, (int)h, c, cs), "ncclRecv");
+      }
+      check(rccl().group_end(), "ncclGroupEnd");
+      sum_packed_enqueue(ctx, recv, W, kn, kn * pcw, share_dev + kj0 * ctw, cs);
     }
     SHELFI_HIP(hipEventRecord(ctx->comm_events[P], cs));
     SHELFI_HIP(hipStreamWaitEvent(s, ctx->comm_events[P], 0));  // the share is ready on `stream`

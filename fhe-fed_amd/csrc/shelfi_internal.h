@@ -210,6 +210,7 @@ struct shelfi_ctx {
   hipEvent_t wl_done[kWeightRing] = {};
   std::vector<uint32_t> wl_host[kWeightRing];
   int wl_next = 0, wl_last_slot = -1;
+  uint32_t* unit_wl = nullptr;   // [16][kMaxTowers][2] limbs (1, 0): the packed exchange's unit-weight sum
   // scratch arena (grown on demand, never shrunk)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -254,6 +255,12 @@ uint64_t arena_ct_words(const Params& p, uint64_t C);  // uint64 words per ciphe
 // wl_dev [C][L][2]; rows = K * 2 * L ciphertext polynomials
 void launch_wavg_packed(const uint64_t* arena, const uint32_t* wl_dev, uint32_t C, uint64_t rows, uint32_t L,
                         uint32_t logN, const ArenaPack& ap, const TowerConst* tc, uint64_t* out, hipStream_t s);
+// The general form: C inputs whose rows are laid out for `crow` learners (C for an arena; 1 for C
+// stacked C = 1 packed batches lstride dwords apart -- lstride 0 = the arena's adjacent slices);
+// the result as uint64 [K][2][L][N] at out, or (pout != null) packed in the C = 1 layout.
+void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t C, uint32_t crow, uint64_t lstride,
+                           uint64_t rows, uint32_t L, uint32_t logN, const ArenaPack& ap, const TowerConst* tc,
+                           uint64_t* out, uint32_t* pout, hipStream_t s);
 // Packs rows [row0, row0 + rows) of learner `learner`'s [K][2][L][N] batch (src holds exactly those
 // rows' residues, 512 per row) into its arena slices; *bad |= 1 when a residue is >= q_t.
 void launch_arena_pack(const uint64_t* src, uint64_t row0, uint64_t rows, uint32_t C, uint32_t learner,
@@ -296,6 +303,10 @@ size_t keygen_scratch_bytes(const Params& p);
 // api.cpp: the arena aggregation (ctx lock held, weights checked), refused-slot check, weights
 void wavg_arena_enqueue(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
                         uint64_t* out_dev, hipStream_t s);
+void wavg_arena_enqueue_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
+                               uint64_t* out_packed, hipStream_t s);
+void sum_packed_enqueue(shelfi_ctx* ctx, const uint64_t* stacked, size_t G, size_t K, size_t stride,
+                        uint64_t* out, hipStream_t s);
 void arena_require_valid_locked(const shelfi_ctx* ctx, const uint64_t* a, size_t words);
 void check_wavg_weights(const float* w, size_t C, double delta);
 // comm.cpp: drop the context's RCCL communicator (if any)

@@ -242,6 +242,15 @@ int shelfi_dev_arena_release(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t 
 /* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream);
+/* The same aggregation written packed: K ciphertexts in the arena's slice format with C = 1
+ * (shelfi_arena_words(ctx, 1, K) uint64 words at out_packed), the packed exchange's send form. */
+int shelfi_dev_wavg_arena_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
+                                 size_t K, uint64_t* out_packed, void* stream);
+/* sum_g x_g mod q_t of G <= 16 packed (C = 1) batches of K ciphertexts stacked stride_words uint64
+ * words apart (>= shelfi_arena_words(ctx, 1, K)) -> out_dev [K][2][L][N], canonical residues: the
+ * packed exchange's receive side (EvalAdd of the ranks' partial aggregates). */
+int shelfi_dev_sum_packed(shelfi_ctx* ctx, const uint64_t* stacked, size_t G, size_t K, size_t stride_words,
+                          uint64_t* out_dev, void* stream);
 /* Output placement for a resident arena (no reference counterpart: a property of where
  * the aggregate lands in HBM).  The arena launch's time depends on the physical
  * placement of its output buffer relative to the arena (up to 12%,
@@ -290,6 +299,15 @@ int shelfi_dev_reduce_scatter(shelfi_ctx* ctx, const uint64_t* partial_dev, size
 size_t shelfi_combine_share_cts(const shelfi_ctx* ctx, size_t K);
 int shelfi_dev_combine_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C, size_t K,
                              size_t pieces, uint64_t* send_dev, uint64_t* share_dev, int fold, void* stream);
+/* The same step with the packed share exchange (no reference counterpart): each
+ * piece's partial is written packed (the arena's slice format with C = 1, sum_t U_t bits per
+ * coefficient) into send_dev, exchanged by one grouped ncclSend/ncclRecv all-to-all into
+ * recv_dev, and summed on the comm stream with unit weights (the mod-q fold included) into
+ * share_dev.  (W - 1) / W of the packed partial crosses xGMI per rank instead of the uint64 one.
+ * send_dev and recv_dev hold shelfi_arena_words(ctx, 1, W * Ks) uint64 words each. */
+int shelfi_dev_combine_arena_packed(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
+                                    size_t K, size_t pieces, uint64_t* send_dev, uint64_t* recv_dev,
+                                    uint64_t* share_dev, void* stream);
 
 /* encode + encrypt n doubles (device) into K = ceil(n/batch) ciphertexts. */
 int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t* ct_dev,

@@ -155,3 +155,112 @@ def test_decrypt_of_unfolded_sums_equals_decrypt(ck, tmp_path, ring):
     assert torch.equal(got, D.decrypt(c, ct, 3 * B, delta))
     with pytest.raises(ValueError, match="1..16"):
         D.decrypt_sum(c, lz, 17, 3 * B, delta)
+
+
+@pytest.mark.parametrize("C,K", [(4, 3), (20, 2)])
+def test_packed_output_and_stacked_sum(ck, C, K):
+    """The packed exchange's two kernels on one GPU: Arena.wavg_packed writes the aggregate in the
+    C = 1 slice format (the same residues as Arena.wavg: summing that one batch with unit weight
+    gives them back), and sum_packed of G stacked packed batches equals their mod-q sum (oracle)."""
+    import oracle as O
+
+    inf = ck.info()
+    B = inf["batch"]
+    q = np.array(inf["moduli"], np.uint64)
+    rng = np.random.default_rng(C + K)
+    cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B)).cuda()) for _ in range(C)]
+    w = list(rng.dirichlet(np.ones(C)))
+    ar = D.Arena(ck, C, K)
+    for i, c in enumerate(cts):
+        ar.put(i, c)
+    ref = ar.wavg(w)
+    pw = D.packed_words(ck, K)
+    packed = ar.wavg_packed(w)
+    assert packed.numel() == pw
+    assert torch.equal(D.sum_packed(ck, packed, 1, K, pw), ref)
+    # G stacked batches with a gap between them (stride > the batch)
+    G, stride = 3, pw + 40
+    stk = torch.zeros(G * stride, dtype=torch.int64, device="cuda")
+    parts = []
+    for g in range(G):
+        wg = list(rng.dirichlet(np.ones(C)))
+        ar.wavg_packed(wg, out=stk[g * stride:g * stride + pw])
+        parts.append(ar.wavg(wg).cpu().numpy().view(np.uint64))
+    got = D.sum_packed(ck, stk, G, K, stride).cpu().numpy().view(np.uint64)
+    exp = np.zeros_like(parts[0])
+    for p in parts:
+        for t in range(len(q)):
+            exp[:, :, t] = (exp[:, :, t] + p[:, :, t]) % q[t]
+    assert np.array_equal(got, exp)
+    # a sub-range of the arena, packed
+    if K > 1:
+        sub = ar.wavg_packed(w, k0=1, k1=K)
+        assert torch.equal(D.sum_packed(ck, sub, 1, K - 1, D.packed_words(ck, K - 1)), ref[1:])
+
+
+@pytest.mark.parametrize("C,K,pieces", [(4, 7, 1), (5, 9, 3), (20, 5, 2)])
+def test_packed_exchange_c_abi_combine_one_rank(ck, C, K, pieces):
+    """shelfi_dev_combine_arena_packed (packed partials, grouped ncclSend/ncclRecv all-to-all,
+    unit-weight sum on the comm stream) on a one-rank communicator: the share equals the arena
+    aggregate bit for bit, and equals the reduce-scatter combine's share."""
+    B = ck.info()["batch"]
+    rng = np.random.default_rng(C * 10 + K)
+    cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B - 5)).cuda()) for _ in range(C)]
+    w = list(rng.dirichlet(np.ones(C)))
+    ar = D.Arena(ck, C, K)
+    for i, c in enumerate(cts):
+        ar.put(i, c)
+    ref = ar.wavg(w)
+    comm = X.Comm(ck, rank=0, world=1)
+    try:
+        Ks = comm.share_cts(K)
+        nw = comm.packed_buffer_words(K)
+        send = torch.empty(nw, dtype=torch.int64, device="cuda")
+        recv = torch.empty(nw, dtype=torch.int64, device="cuda")
+        share = D.empty_ct(ck, Ks)
+        for _ in range(2):
+            comm.combine_arena_packed(ar, w, K, send, recv, share, pieces=pieces)
+        torch.cuda.synchronize()
+        assert torch.equal(share, ref)
+        s2, sh2 = D.empty_ct(ck, Ks), D.empty_ct(ck, Ks)
+        comm.combine_arena(ar, w, K, s2, sh2, pieces=pieces, fold=True)
+        torch.cuda.synchronize()
+        assert torch.equal(sh2, share)
+    finally:
+        comm.close()
+
+
+def test_packed_pipelined_combine_torch_one_rank(ck, tmp_path):
+    """dist.PackedPipelinedCombine over torch.distributed (nccl = RCCL, one rank): the packed
+    all_to_all_single path with the device kernels gives the single-GPU aggregate."""
+    import socket
+
+    import torch.distributed as dist_
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist_.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        inf = ck.info()
+        B = inf["batch"]
+        C, K = 6, 5
+        rng = np.random.default_rng(77)
+        cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B)).cuda()) for _ in range(C)]
+        w = list(rng.dirichlet(np.ones(C)))
+        ar = D.Arena(ck, C, K)
+        for i, c in enumerate(cts):
+            ar.put(i, c)
+        ref = ar.wavg(w)
+        comb = X.PackedPipelinedCombine(K, (2, inf["num_towers"], inf["ring_dim"]), D.packed_words(ck, 1),
+                                        pieces=2, device="cuda")
+        owned = comb.run(lambda k0, k1, out: ar.wavg_packed(w, out=out, k0=k0, k1=k1),
+                         lambda stk, G, n, stride, out: D.sum_packed(ck, stk, G, n, stride, out=out))
+        torch.cuda.synchronize()
+        assert [(a, b) for a, b, _ in owned] == [(0, 3), (3, 5)]
+        for a, b, sv in owned:
+            assert torch.equal(sv, ref[a:b])
+    finally:
+        dist_.destroy_process_group()

@@ -330,3 +330,82 @@ def test_packed_arena_layout_restatement_round_trips():
         back = AL.unpack_arena(words, C, K, L, N, q)
         for a, b in zip(cts, back):
             assert np.array_equal(a, b)
+
+
+def _gloo_packed_worker(rank, world, port, pieces, result_q, K=7, C_=5):
+    """The packed share exchange (dist.PackedPipelinedCombine) on gloo: each rank's partial of a
+    piece packed in the C = 1 slice format (tests/arena_layout.py restates the kernels' layout),
+    all_to_all_single, unit-weight sum mod q of the received chunks."""
+    import sys
+
+    import torch
+    import torch.distributed as dist_
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import arena_layout as AL
+    import oracle as O_
+    from SHELFI_FHE import dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist_.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, L = 1024, 2
+        q, psi = O_.params_generate(N, L, 40, 50)  # 50 / 41 bits: a 52-bit field and a flag-plane tower
+        delta = float(int(q[-1]))
+        qi = [int(x) for x in q]
+        pw = 2 * N * sum(AL.widths(qi)) // 64  # packed 64-bit words per ciphertext (C = 1)
+        rng = np.random.default_rng(5)
+        cts = []
+        for _ in range(C_):
+            a = np.empty((K, 2, L, N), np.uint64)
+            for t in range(L):
+                a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
+            cts.append(a)
+        w = list(rng.dirichlet(np.ones(C_)))
+        mine = dist.learner_shard(C_, rank, world)
+        comb = dist.PackedPipelinedCombine(K, (2, L, N), pw, pieces=pieces)
+
+        def compute(k0, k1, words):  # Arena.wavg_packed's job: the oracle partial, packed
+            part = O_.wavg([cts[i][k0:k1] for i in mine], [w[i] for i in mine], q, delta)
+            packed = AL.pack_arena([part], qi, N).view(np.int64)
+            assert packed.size == (k1 - k0) * pw
+            words.copy_(torch.from_numpy(packed.copy()))
+
+        def sum_share(stacked, G, n, stride, out):  # device.sum_packed's job
+            acc = np.zeros((n, 2, L, N), np.uint64)
+            for g in range(G):
+                chunk = stacked[g * stride:g * stride + n * pw].numpy().view(np.uint32)
+                (x,) = AL.unpack_arena(chunk, 1, n, L, N, qi)
+                for t in range(L):
+                    acc[:, :, t, :] = (acc[:, :, t, :] + x[:, :, t, :]) % q[t]
+            out.copy_(torch.from_numpy(acc.view(np.int64)))
+
+        owned = comb.run(compute, sum_share)
+        full = O_.wavg(cts, w, q, delta)
+        ok = all(np.array_equal(s.numpy().view(np.uint64), full[a:b]) for a, b, s in owned)
+        ok &= [(a, b) for a, b, _ in owned] == comb.owned_ranges()
+        allr = [None] * world
+        dist_.all_gather_object(allr, comb.owned_ranges())
+        cover = sorted(x for r in allr for a, b in r for x in range(a, b))
+        ok &= cover == list(range(K))
+        result_q.put((rank, bool(ok)))
+    finally:
+        dist_.destroy_process_group()
+
+
+@pytest.mark.parametrize("pieces", [1, 3])
+def test_packed_exchange_combine_gloo_world2(pieces):
+    """the packed share exchange (all-to-all of packed partial shares, then a
+    local unit-weight sum) equals the single-process aggregation bit for bit, and the ranks'
+    shares tile [0, K)."""
+    pytest.importorskip("torch")
+    assert _spawn_world(2, _gloo_packed_worker, pieces) == [(0, True), (1, True)]
+
+
+def test_packed_exchange_combine_gloo_world8_rehearsal():
+    """The driver's N = 8 shape in miniature with the packed exchange: 8 gloo ranks, 11 learners,
+    K = 13 in 3 pieces (padded pieces, ranks owning nothing of a piece): bit-exact vs one process."""
+    pytest.importorskip("torch")
+    res = _spawn_world(8, _gloo_packed_worker, 3, K=13, C_=11)
+    assert res == [(r, True) for r in range(8)]
