@@ -991,10 +991,11 @@ __device__ __forceinline__ void fft_chunk(const double2* __restrict__ tw, Load l
 // §LDS), which reproduces the measured SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS of round 3 exactly
 // (10.0 for fft_fwd_blocks_ct<10,...>, 5.33 for fft_inv_blocks_ct<10,...>): swizzled, 0 and 1.33
 // (the DIF A = 2 chunk's stores keep a 2-way conflict), and 0 for both BL = 11 passes.
-__device__ __forceinline__ uint32_t fft_swz(uint32_t j) { return j ^ ((j >> 3) & 15u); }
+template <bool SWZ = true>
+__device__ __forceinline__ uint32_t fft_swz(uint32_t j) { return SWZ ? j ^ ((j >> 3) & 15u) : j; }
 
 // FFTSpecialInv's second pass (encode, after fft_inv_cols): DIF half-sizes 2^(BL-1) .. 1.
-template <int BL, int K1, int K2, int K3, int K4>
+template <int BL, int K1, int K2, int K3, int K4, bool SWZ = true>
 __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __restrict__ buf, uint32_t logS,
                                                                   const double2* __restrict__ tw) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan");
@@ -1003,8 +1004,8 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __re
   const uint64_t k = blockIdx.x >> sh;
   const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   double2* __restrict__ g = buf + k * S + ((uint64_t)b << BL);
-  const auto lds_ld = [&](uint32_t j) { return sm[fft_swz(j)]; };
-  const auto lds_st = [&](uint32_t j, double2 v) { sm[fft_swz(j)] = v; };
+  const auto lds_ld = [&](uint32_t j) { return sm[fft_swz<SWZ>(j)]; };
+  const auto lds_st = [&](uint32_t j, double2 v) { sm[fft_swz<SWZ>(j)] = v; };
   fft_chunk<BL, K1, BL - K1, false>(tw, [&](uint32_t j) { return g[j]; }, lds_st);
   __syncthreads();
   fft_chunk<BL, K2, BL - K1 - K2, false>(tw, lds_ld, lds_st);
@@ -1445,9 +1446,13 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t nb = K * ((p.batch >> logR) / 256);
     FFT_DISPATCH(logR, fft_inv_cols, dim3((uint32_t)nb), dim3(256), 0, s, x, n, fbuf, logS,
                  dt.fft_inv);
-    const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switch (read per launch)
+    const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switches (read per launch)
     const bool fct = !(fenv && *fenv == '0');
-    if (fct && blkLog == 10)
+    const char* zenv = getenv("SHELFI_FFT_SWZ");
+    if (fct && blkLog == 10 && zenv && *zenv == '0')
+      hipLaunchKernelGGL((fft_inv_blocks_ct<10, 3, 3, 2, 2, false>), dim3((uint32_t)(K << logR)), dim3(128), 0, s,
+                         fbuf, logS, dt.fft_inv);
+    else if (fct && blkLog == 10)
       hipLaunchKernelGGL((fft_inv_blocks_ct<10, 3, 3, 2, 2>), dim3((uint32_t)(K << logR)), dim3(128), 0, s, fbuf,
                          logS, dt.fft_inv);
     else if (fct && blkLog == 11)
@@ -2070,7 +2075,7 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
 // FFTSpecial's first pass (decode, not the final pass): block b of ciphertext k, DIT half-sizes
 // 1 .. 2^(BL-1); K1 = 3, so the first chunk's set is 8 consecutive positions = one ChaCha block
 // of the flooding stream.
-template <int BL, int K1, int K2, int K3, int K4, bool FLOOD>
+template <int BL, int K1, int K2, int K3, int K4, bool FLOOD, bool SWZ = true>
 __global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __restrict__ buf, uint32_t logS,
                                                                   const double2* __restrict__ tw, FloodArgs fa) {
   static_assert(K1 == 3 && K1 + K2 + K3 + K4 == BL, "chunk plan");
@@ -2079,8 +2084,8 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __re
   const uint64_t k = blockIdx.x >> sh;
   const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   double2* __restrict__ g = buf + k * S + ((uint64_t)b << BL);
-  const auto lds_ld = [&](uint32_t j) { return sm[fft_swz(j)]; };
-  const auto lds_st = [&](uint32_t j, double2 v) { sm[fft_swz(j)] = v; };
+  const auto lds_ld = [&](uint32_t j) { return sm[fft_swz<SWZ>(j)]; };
+  const auto lds_st = [&](uint32_t j, double2 v) { sm[fft_swz<SWZ>(j)] = v; };
   if (FLOOD) {
     const double nsd = flood_nsd(fa, k, b, S);
     const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
@@ -2207,7 +2212,15 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switch (read per launch)
   const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && !(fenv && *fenv == '0');
   const dim3 fg((uint32_t)(K << flogR));
-  if (fct && fblkLog == 10 && fused_flood)
+  const char* zenv = getenv("SHELFI_FFT_SWZ");
+  const bool noswz = zenv && *zenv == '0';
+  if (fct && fblkLog == 10 && noswz && fused_flood)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd,
+                       fa);
+  else if (fct && fblkLog == 10 && noswz)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false, false>), fg, dim3(128), 0, s, fbuf, logS,
+                       dt.fft_fwd, fa);
+  else if (fct && fblkLog == 10 && fused_flood)
     hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
   else if (fct && fblkLog == 10)
     hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
