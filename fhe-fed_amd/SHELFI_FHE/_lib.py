@@ -11,6 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libshelfi.so")
+# A/B probes only (tools/*_ab*.sh): another build of the library, e.g. the previous commit's
+LIB_PATH = os.environ.get("SHELFI_LIB_AB", LIB_PATH)
 
 SHELFI_OK = 0
 SHELFI_ERR_ARG = -1

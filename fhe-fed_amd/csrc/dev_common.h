@@ -54,6 +54,18 @@ __device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t 
   asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(lo >> 32)), "v"(c1), "v"(c2));
   return ((uint64_t)hi << 32) | (uint32_t)lo;
 }
+// a + (x * w mod q up to 3 extra q), for a + 4q < 2^64: the addend rides in the first
+// v_mad_u64_u32 (x0 w0 + a), so the forward butterfly's X = x + t costs nothing extra.
+__device__ __forceinline__ uint64_t shoup_lazy_add(uint64_t x, uint64_t w, uint64_t wp, uint64_t q, uint64_t a) {
+  const uint64_t h = umulhi_approx(x, wp), nq = (uint64_t)0 - q;
+  const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+  const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+  const uint64_t lo = (uint64_t)h0 * n0 + ((uint64_t)x0 * w0 + a);  // mod 2^64
+  const uint32_t c1 = x1 * w0 + x0 * w1, c2 = h1 * n0 + h0 * n1;
+  uint32_t hi;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(lo >> 32)), "v"(c1), "v"(c2));
+  return ((uint64_t)hi << 32) | (uint32_t)lo;
+}
 // Same bound, as x*w - h*q (the form the inverse butterflies schedule better).
 __device__ __forceinline__ uint64_t shoup_lazy_sub(uint64_t x, uint64_t w, uint64_t wp, uint64_t q) {
   return x * w - umulhi_approx(x, wp) * q;
@@ -122,13 +134,16 @@ constexpr int fwd_bound(int S) {
 // Forward (CT) butterfly with the input reduction scheduled by the caller: inputs
 // x < 16q (RED: x -= 8q when x >= 8q, so x < 8q) or x < 12q (no reduction), any y;
 // outputs X = x + t, Y = x + 4q - t with t = y w mod q in [0, 4q): below 16q (q < 2^60).
+// (Round 4: X = x + t comes out of the product's first multiply-add, and Y = 2x + 4q - X is one
+// v_lshl_add_u64 and a 64-bit subtraction -- 3 VALU for the pair instead of 4; the same values,
+// Y wraps mod 2^64 only in between: x + 4q - t itself is below 20q.)
 template <bool RED>
 __device__ __forceinline__ void ct_bfly_s(uint64_t& X, uint64_t& Y, uint64_t W, uint64_t Wp,
                                           uint64_t q, uint64_t n8q) {
   const uint64_t x = RED ? csub_neg(X, n8q) : X;
-  const uint64_t t = shoup_lazy(Y, W, Wp, q);
-  X = x + t;
-  Y = x + (q << 2) - t;
+  const uint64_t s = shoup_lazy_add(Y, W, Wp, q, x);  // x + t
+  Y = (x << 1) + (q << 2) - s;                        // x + 4q - t
+  X = s;
 }
 
 // Inverse (GS) butterfly, [0, 4q) in and out, borrow-free reduction of the sum (the generic
