@@ -255,20 +255,21 @@ __device__ __forceinline__ uint64_t wavg_fold3(uint64_t s0, uint64_t sm, uint64_
 }
 
 // Learner k's slice of the row sits `step` dwords after learner 0's: S::SLICE in an arena (the C
-// slices side by side), or a caller's stride between stacked C = 1 batches (the packed share
-// exchange, sum_packed).  PO: the row's result is written packed (the C = 1 slice format, 16 U
-// dwords at po) instead of as uint64 at o.
-template <int UB, int UR, bool PO, bool STK>
-__device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl, uint32_t C, uint64_t lstride,
-                                                const uint32_t* __restrict__ wlt,
+// slices side by side), or a caller's stride between stacked C = 1 batches (STK: the packed share
+// exchange's sum_packed).  Learners [kbeg, kend) are summed; the row's 8 residues per lane come
+// back in x (canonical; zero for an empty range).
+template <int UB, int UR, bool STK>
+__device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl, uint32_t kbeg, uint32_t kend,
+                                                uint64_t lstride, const uint32_t* __restrict__ wlt,
                                                 uint32_t wl_stride, const TowerConst& c, uint32_t lane,
-                                                uint64_t* __restrict__ run, uint64_t* __restrict__ o,
-                                                uint32_t* __restrict__ po) {
+                                                uint64_t* __restrict__ run, uint64_t (&x)[8]) {
   using S = PackShape<UB>;
   constexpr int B = S::B, G = pack_group<UB>();
   const uint64_t step = STK ? lstride : (uint64_t)S::SLICE;
-  for (uint32_t k0 = 0; k0 < C; k0 += G) {
-    const uint32_t k1 = min(C, k0 + (uint32_t)G);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = 0;
+  for (uint32_t k0 = kbeg; k0 < kend; k0 += G) {
+    const uint32_t k1 = min(kend, k0 + (uint32_t)G);
     uint64_t s0[8], sm[8], s1[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s0[j] = sm[j] = s1[j] = 0;
@@ -288,75 +289,97 @@ __device__ __forceinline__ void wavg_packed_row(const uint32_t* __restrict__ sl,
         s1[j] += (uint64_t)x1 * w1;
       }
     }
-    const bool first = k0 == 0, last = k1 >= C;
-    if (PO && last) {
-      uint64_t x[8];
+    const bool first = k0 == kbeg, last = k1 >= kend;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        x[j] = wavg_fold3(s0[j], sm[j], s1[j], c);
-        if (!first) x[j] = addmod(x[j], run[64 * j + lane], c.q);
-      }
-      uint32_t w[S::D], fl;
-      pk_pack<UB>(x, w, fl);
-      pk_store<UB>(po, lane, w, fl);
-      continue;
+    for (int j = 0; j < 8; ++j) {
+      uint64_t r = wavg_fold3(s0[j], sm[j], s1[j], c);
+      if (!first) r = addmod(r, run[64 * j + lane], c.q);
+      if (last) x[j] = r;
+      else run[64 * j + lane] = r;
     }
+  }
+}
+
+// A row's 8 residues per lane as uint64 (4 coalesced 16-byte non-temporal stores per lane).
+__device__ __forceinline__ void store_row_u64(uint64_t* __restrict__ o, uint32_t lane, const uint64_t (&x)[8]) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      uint64_t r[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = 2 * g + h;
-        r[h] = wavg_fold3(s0[j], sm[j], s1[j], c);
-        if (!first) r[h] = addmod(r[h], run[64 * j + lane], c.q);
-        if (!last) run[64 * j + lane] = r[h];
-      }
-      if (last) {
-        u32x4 v;
-        v.x = (uint32_t)r[0];
-        v.y = (uint32_t)(r[0] >> 32);
-        v.z = (uint32_t)r[1];
-        v.w = (uint32_t)(r[1] >> 32);
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + 128 * g + 2 * lane));
-      }
-    }
+  for (int g = 0; g < 4; ++g) {
+    u32x4 v;
+    v.x = (uint32_t)x[2 * g];
+    v.y = (uint32_t)(x[2 * g] >> 32);
+    v.z = (uint32_t)x[2 * g + 1];
+    v.w = (uint32_t)(x[2 * g + 1] >> 32);
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + 128 * g + 2 * lane));
   }
 }
 
 constexpr int kPackedWaves = 4;  // waves per block, one row each
 
 // crow: the learner count of the input's row layout (C for an arena, 1 for stacked C = 1 batches
-// lstride dwords apart); out (uint64) or pout (packed, C = 1 layout) receives the result.
-template <int UR, int WV = kPackedWaves, bool PO = false, bool STK = false>
+// lstride dwords apart); out (uint64) or, with PO, pout (packed, C = 1 layout) receives the result.
+// SP = 2 (small launches): two waves per row, each summing half of the learners; the second hands its
+// 8 residues per lane to the first through LDS, which adds them and stores -- twice the waves (and
+// bytes in flight) for a grid too small to fill the chip, one extra fold per row.
+template <int UR, int WV = kPackedWaves, bool PO = false, bool STK = false, int SP = 1>
 __global__ __launch_bounds__(64 * WV) void wavg_packed(const uint32_t* __restrict__ arena,
                                                       const uint32_t* __restrict__ wl, uint32_t C, uint32_t crow,
                                                       uint64_t lstride, uint64_t rows, uint32_t L, uint32_t logN,
                                                       ArenaPack ap, const TowerConst* __restrict__ tcs,
                                                       uint64_t* __restrict__ out, uint32_t* __restrict__ pout,
                                                       uint32_t xcd) {
+  static_assert(SP == 1 || (SP == 2 && !PO && WV % 2 == 0), "row split");
   // the running sum of the rows' residues across learner groups (C > 16): 8 x 64 per wave
   __shared__ uint64_t run_lds[WV][8 * 64];
+  __shared__ uint64_t xch_lds[SP == 2 ? WV / 2 : 1][SP == 2 ? 8 * 64 : 1];
   // xcd: consecutive blocks land on the 8 XCDs in turn; remap so each XCD walks one contiguous
   // eighth of the rows (probe switch SHELFI_PACK_XCD; needs gridDim.x % 8 == 0)
   const uint32_t b = xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t r = (uint64_t)b * WV + wave;
-  if (r >= rows) return;
+  const uint32_t part = SP == 2 ? (wave & 1u) : 0u, slot = wave / SP;
+  const uint64_t r = (uint64_t)b * (WV / SP) + slot;
+  const bool valid = r < rows;
+  if (SP == 1 && !valid) return;  // (SP == 2: every wave reaches the exchange barrier)
   const uint32_t lane = threadIdx.x & 63;
-  const PackedRow pr = packed_row(r, crow, L, logN, ap);
-  const TowerConst c = tcs[pr.t];
-  const uint32_t* __restrict__ sl = arena + pr.base;
-  const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
-  uint64_t* __restrict__ o = PO ? nullptr : out + r * kArenaChunk;
-  uint32_t* __restrict__ po = PO ? pout + packed_row(r, 1, L, logN, ap).base : nullptr;
-  switch (pr.U) {
-#define WPR(UU) \
-  case UU: wavg_packed_row<UU, UR, PO, STK>(sl, C, lstride, wlt, 2 * L, c, lane, run_lds[wave], o, po); break;
-    SHELFI_PACK_WIDTHS(WPR)
+  uint64_t x[8];
+  uint64_t q = 0;
+  if (valid) {
+    const PackedRow pr = packed_row(r, crow, L, logN, ap);
+    const TowerConst c = tcs[pr.t];
+    q = c.q;
+    const uint32_t* __restrict__ sl = arena + pr.base;
+    const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
+    const uint32_t half = (C + 1) / 2;
+    const uint32_t kbeg = SP == 2 ? part * half : 0u, kend = SP == 2 ? min(C, (part + 1) * half) : C;
+    uint32_t* __restrict__ po = PO ? pout + packed_row(r, 1, L, logN, ap).base : nullptr;
+    switch (pr.U) {
+#define WPR(UU)                                                                                     \
+  case UU:                                                                                          \
+    wavg_packed_row<UU, UR, STK>(sl, kbeg, kend, lstride, wlt, 2 * L, c, lane, run_lds[wave], x);   \
+    if (PO) {                                                                                       \
+      uint32_t pw[PackShape<UU>::D], pf;                                                            \
+      pk_pack<UU>(x, pw, pf);                                                                       \
+      pk_store<UU>(po, lane, pw, pf);                                                               \
+    }                                                                                               \
+    break;
+      SHELFI_PACK_WIDTHS(WPR)
 #undef WPR
-    default:
-      break;
+      default:
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = 0;
+        break;
+    }
+    if (SP == 2 && part == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xch_lds[slot][64 * j + lane] = x[j];
+    }
   }
+  if (SP == 2) {
+    __syncthreads();  // every wave of the block, valid or not: the one barrier of the kernel
+    if (!valid || part == 1) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = addmod(x[j], xch_lds[slot][64 * j + lane], q);
+  }
+  if (!PO) store_row_u64(out + r * kArenaChunk, lane, x);
 }
 
 // Round 3's form (four accumulators, running sum in registers; 134-145 VGPRs, 3 waves per SIMD),
@@ -509,14 +532,21 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   const char* wenv = getenv("SHELFI_PACK_WAVES");
   const int wv = wenv ? atoi(wenv) : kPackedWaves;
   const char* xenv = getenv("SHELFI_PACK_XCD");
+  const char* senv = getenv("SHELFI_PACK_SPLIT");
+  const bool split = senv && *senv == '2' && !po && !stk;
   const int wvs = (wv == 2 || wv == 8) && u == 2 && !po && !stk ? wv : kPackedWaves;
-  const uint64_t blocks = (nrows + wvs - 1) / wvs;
+  const uint64_t rows_per_block = split ? kPackedWaves / 2 : wvs;
+  const uint64_t blocks = (nrows + rows_per_block - 1) / rows_per_block;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   const uint32_t xcd = xenv && *xenv == '1' && blocks % 8 == 0 ? 1u : 0u;
 #define WPK(UU, WW, PO, STK)                                                                                 \
   hipLaunchKernelGGL((wavg_packed<UU, WW, PO, STK>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s, in, wl_dev,  \
                      C, crow, lstride, nrows, L, logN, ap, tc, out, pout, xcd)
-  if (stk && po)
+  if (split)
+    hipLaunchKernelGGL((wavg_packed<2, kPackedWaves, false, false, 2>), dim3((uint32_t)blocks),
+                       dim3(64 * kPackedWaves), 0, s, in, wl_dev, C, crow, lstride, nrows, L, logN, ap, tc, out,
+                       pout, xcd);
+  else if (stk && po)
     throw Error{SHELFI_ERR_ARG, "stacked inputs with a packed output"};
   else if (stk)
     WPK(2, 4, false, true);

@@ -205,14 +205,16 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
             ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
     w = list(rng.uniform(-1, 1, C))
     ref = O.wavg(cts, w, q, delta)
-    for unroll in ("1", "2", "4"):
+    for unroll in ("1", "2", "4", "8"):
         monkeypatch.setenv("SHELFI_PACK_UNROLL", unroll)
         got = ar.wavg(w)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), unroll
     monkeypatch.delenv("SHELFI_PACK_UNROLL")
-    # the probe switches: rows per block, XCD-contiguous block order
-    for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_XCD", "1")):
+    # the probe switches: rows per block, XCD-contiguous block order, two waves per row (learners
+    # split), round 3's four-accumulator kernel
+    for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_XCD", "1"),
+                     ("SHELFI_PACK_SPLIT", "2"), ("SHELFI_PACK_KERNEL", "r3")):
         monkeypatch.setenv(env, val)
         got = ar.wavg(w)
         torch.cuda.synchronize()

@@ -14,8 +14,10 @@ mkdir -p $out
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
 AB_ENV=SHELFI_PACK_KERNEL AB_VARIANTS=r3,v4 run 300 python tools/wavg_packed_ab.py 7 20 > $out/wavg_kernel_ab.txt 2>&1
 cat $out/wavg_kernel_ab.txt
-AB_ENV=SHELFI_PACK_UNROLL AB_VARIANTS=1,2,4,8 AB_SHAPES=cfg2,cfg5,cfg3 run 300 python tools/wavg_packed_ab.py 5 20 > $out/wavg_unroll_ab.txt 2>&1
+AB_ENV=SHELFI_PACK_UNROLL AB_VARIANTS=1,2,4,8 AB_SHAPES=cfg2,cfg5,cfg3,cfg4 run 300 python tools/wavg_packed_ab.py 5 20 > $out/wavg_unroll_ab.txt 2>&1
 cat $out/wavg_unroll_ab.txt
+AB_ENV=SHELFI_PACK_SPLIT AB_VARIANTS=1,2 run 300 python tools/wavg_packed_ab.py 7 20 > $out/wavg_split_ab.txt 2>&1
+cat $out/wavg_split_ab.txt
 VAR=SHELFI_FFT_SWZ VALS=0,1 K=714 run 200 python tools/enc_variant_probe.py > $out/fft_swz_ab.txt 2>&1
 VAR=SHELFI_FFT_SWZ VALS=0,1 K=714 FLOOD=1 run 200 python tools/enc_variant_probe.py >> $out/fft_swz_ab.txt 2>&1
 cat $out/fft_swz_ab.txt
