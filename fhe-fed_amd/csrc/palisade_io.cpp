@@ -10,6 +10,7 @@
 // and key vectors by (length == N, trailing modulus == q_t, all residues < q_t).
 #include <cstring>
 
+#include "palisade_codec.h"
 #include "palisade_io.h"
 #include "shelfi_internal.h"
 
@@ -22,10 +23,32 @@ static T rd(const std::string& s, size_t off) {
   return v;
 }
 
+// A tower as the context stores it: q prime, q = 1 mod 2N, psi a primitive 2N-th root (psi^N = -1).
+static bool valid_tower(uint32_t N, uint64_t q, uint64_t psi) {
+  return q > 2ull * N && q < (1ull << 60) && q % (2ull * N) == 1 && is_prime(q) && psi < q &&
+         powmod(psi, N, q) == q - 1;
+}
+
 PalisadeContext palisade_read_context(const std::string& s) {
   if (s.size() < 64 || (uint8_t)s[0] != 0x01 || s.find("lbcrypto::") == std::string::npos)
     throw Error{SHELFI_ERR_FORMAT, "cryptocontext.txt is neither a SHELFI nor a PALISADE context"};
   PalisadeContext pc;
+  // the structured grammar first (palisade_codec.h: every tower object in order, whatever the
+  // moduli's size -- a 14-bit scale gives a 17-bit last tower, below the scan's guard)
+  try {
+    const PalisadeCtxParams cp = palisade_parse_context_file(s);
+    bool ok = cp.L >= 1 && cp.L <= (uint32_t)kMaxTowers && cp.q.size() == cp.L && cp.psi.size() == cp.L;
+    for (uint32_t t = 0; ok && t < cp.L; ++t) ok = valid_tower(cp.N, cp.q[t], cp.psi[t]);
+    if (ok) {
+      pc.N = cp.N;
+      pc.q = cp.q;
+      pc.psi = cp.psi;
+      return pc;
+    }
+  } catch (const Error&) {
+  }
+  // other 1.11 layouts: locate the towers by their invariants (the scan's 2^20 floor on q keeps
+  // stray byte patterns out)
   for (size_t off = 0; off + 16 <= s.size(); ++off) {
     const uint32_t M = rd<uint32_t>(s, off), N = rd<uint32_t>(s, off + 4);
     if (N < 1024 || N > (1u << 17) || (N & (N - 1)) || M != 2 * N) continue;

@@ -174,6 +174,28 @@ def test_pickled_encrypt_archives_match_params_results(batch):
 
 
 @pytest.mark.parametrize("batch,sb", SWEEP)
+def test_sweep_context_and_key_files_read_back(tmp_path, batch, sb):
+    """loadCryptoParams of what genCryptoContextAndKeyGen writes for every sweep row: the context
+    and key files (the writers of ckks.cpp:41-55) read back through the product's PALISADE reader
+    with the same towers and residues -- the 14-bit row's 17-bit last tower (0x10001) included,
+    which the reader's invariant scan alone refused (its q >= 2^20 guard)."""
+    N, q, psi = m.params_generate(batch, sb, 1)
+    d = str(tmp_path) + os.sep
+    ctx_file = m.palisade_context_file(N, q, psi, sb, batch)
+    open(d + "cryptocontext.txt", "wb").write(ctx_file)
+    ctx_obj = m.palisade_embed_context(ctx_file)
+    rng = np.random.default_rng(sb + batch)
+    pk = np.stack([np.stack([rng.integers(0, qt, N, dtype=np.uint64) for qt in q]) for _ in range(2)])
+    sk = np.stack([rng.integers(0, qt, N, dtype=np.uint64) for qt in q])
+    tag = "%032x" % (sb * 1000003 + batch)
+    open(d + "key-public.txt", "wb").write(m.palisade_key_file(ctx_obj, tag, pk, True))
+    open(d + "key-private.txt", "wb").write(m.palisade_key_file(ctx_obj, tag, sk, False))
+    n2, q2, psi2, pk2, sk2 = _read_keys(d)
+    assert (n2, q2, psi2) == (N, q, psi)
+    assert np.array_equal(pk2, pk) and np.array_equal(sk2, sk)
+
+
+@pytest.mark.parametrize("batch,sb", SWEEP)
 def test_sweep_contexts_match_params_results(batch, sb):
     """Every row of code/params_results.csv:2-16 through this library's ParamsGen:
     genCryptoContextCKKS(1, sb, batch) (ckks.cpp:26-28) must land on N = 8192 (the ring
