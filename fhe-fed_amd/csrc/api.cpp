@@ -603,6 +603,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
     SHELFI_HIP(hipMalloc(&ctx->dev_flag, 32));
+    SHELFI_HIP(hipHostMalloc((void**)&ctx->host_flag, 32, hipHostMallocDefault));
     set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
   });
   if (rc != SHELFI_OK) {
@@ -636,6 +637,8 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     dfree(ctx->scratch);
     dfree(ctx->io);
     dfree_t(ctx->dev_flag);
+    if (ctx->host_flag) (void)hipHostFree(ctx->host_flag);
+    ctx->host_flag = nullptr;
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -1050,11 +1053,11 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
     SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
     sr.s.poll();
   }
+  SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, pp.b));  // pinned
   sr.finish();
   pp.sync();
   std::memset(key, 0, sizeof(key));
-  uint32_t flag = 0;
-  SHELFI_HIP(hipMemcpy(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost));
+  const uint32_t flag = ctx->host_flag[0];
   if (flag)
     throw Error{SHELFI_ERR_RANGE,
                 "encrypt: non-finite input or |value * scale| > 2^61 (PALISADE approxFactor range)"};
@@ -1321,8 +1324,17 @@ static DecodeNoise decode_noise_begin(shelfi_ctx* ctx, uint64_t K, hipStream_t s
   dn.p_bits = ctx->p.scale_bits;
   draw_key(ctx, K, dn.key, &dn.g0);
   dn.flags = ctx->dev_flag;
-  SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 1, 0, 8, s));
+  // flags [1], [2] are reset by the first chunk's flooding (launch_decrypt: inside
+  // decode_stats_kernel, or a fill before the small-ring decode_flood_kernel)
+  (void)s;
   return dn;
+}
+
+// Enqueue the flags' readback into pinned host memory on `s`, before the caller's one stream
+// synchronisation (a synchronous pageable hipMemcpy after it cost a second round trip per call).
+static void decode_noise_readback(shelfi_ctx* ctx, const DecodeNoise& dn, hipStream_t s) {
+  if (!dn.enabled) return;
+  SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 1, ctx->dev_flag + 1, 8, hipMemcpyDeviceToHost, s));
 }
 
 // After the decrypt's stream work has completed: record logError, raise PALISADE's
@@ -1330,8 +1342,7 @@ static DecodeNoise decode_noise_begin(shelfi_ctx* ctx, uint64_t K, hipStream_t s
 static void decode_noise_end(shelfi_ctx* ctx, DecodeNoise& dn) {
   if (!dn.enabled) return;
   std::memset(dn.key, 0, sizeof(dn.key));
-  uint32_t f[2] = {0, 0};
-  SHELFI_HIP(hipMemcpy(f, ctx->dev_flag + 1, 8, hipMemcpyDeviceToHost));
+  const uint32_t f[2] = {ctx->host_flag[1], ctx->host_flag[2]};  // decode_noise_readback, synchronised
   ctx->last_log_error = (int)f[1];
   if (f[0])
     throw Error{SHELFI_ERR_PRECISION,
@@ -1420,12 +1431,14 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       dn.g0 += (ci ? kc : 0);
       launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
                      scratch, pp.b, &dn);
+      dn.reset = 0;
       SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
       SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
       sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
       SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
       sr.s.poll();
     }
+    decode_noise_readback(ctx, dn, pp.b);
     sr.finish();
     pp.sync();
     decode_noise_end(ctx, dn);
@@ -1900,10 +1913,9 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
                      key, g0 + k0, ctx->dev_flag, s);
     }
     std::memset(key, 0, sizeof(key));
-    uint32_t flag = 0;
-    SHELFI_HIP(hipMemcpyAsync(&flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));
+    SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));  // pinned
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
-    if (flag)
+    if (ctx->host_flag[0])
       throw Error{SHELFI_ERR_RANGE, "encrypt: |value * scale| exceeds 2^61 (approxFactor range)"};
   });
 }
@@ -1936,7 +1948,9 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
       dn.g0 = g0 + k0;
       launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
                      sum_in, towers);
+      dn.reset = 0;  // the flags are reset by the first chunk's flooding only
     }
+    decode_noise_readback(ctx, dn, s);
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);
   });

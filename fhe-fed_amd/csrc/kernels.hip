@@ -1942,8 +1942,12 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
 // (slot 0) and 1 (slot S/2) are their own partners.
 constexpr uint32_t kFloodPairsPerWg = 1024;
 __global__ __launch_bounds__(256) void decode_stats_kernel(const double2* __restrict__ fbuf, uint32_t logS,
-                                                           uint32_t G, double2* __restrict__ part) {
+                                                           uint32_t G, double2* __restrict__ part,
+                                                           uint32_t* __restrict__ reset_flags) {
   __shared__ double red[2][4];
+  // the call's precision / logError flags, reset here (the FFT pass that sets them runs after this
+  // kernel on the same stream) instead of by a separate fill launch
+  if (reset_flags && blockIdx.x == 0 && threadIdx.x < 2) reset_flags[1 + threadIdx.x] = 0;
   const uint32_t S = 1u << logS, half = S >> 1;
   const uint64_t k = blockIdx.x / G;
   const uint32_t wg = blockIdx.x % G;
@@ -2202,8 +2206,9 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       double2* part = fbuf + K * (uint64_t)p.batch;
       fa.part = part;
       hipLaunchKernelGGL(decode_stats_kernel, dim3((uint32_t)(K * fa.G)), dim3(256), 0, s, fbuf, logS, fa.G,
-                         part);
+                         part, dn->reset ? dn->flags : (uint32_t*)nullptr);
     } else {
+      if (dn->reset) SHELFI_HIP(hipMemsetAsync(dn->flags + 1, 0, 8, s));
       hipLaunchKernelGGL(decode_flood_kernel, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, logS, p.logN,
                          fa.two_p, fa.p_bits, fa.m_factor, fa.key, fa.g0, fa.flags);
     }

@@ -182,6 +182,7 @@ struct shelfi_ctx {
   uint64_t params_id = 0;
   uint64_t seed = 0;          // 0 -> OS entropy per call
   uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
+  uint32_t* host_flag = nullptr; // pinned host mirror of dev_flag (async readback before one sync)
   uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
                                  // [2] max decode logError (noise flooding), [3] bytes-API
                                  // upload residue >= q, [4] arena upload residue >= q
@@ -290,6 +291,7 @@ struct DecodeNoise {
   uint32_t key[8] = {};    // ChaCha20 key, nonce (3 << 56) | (g0 + ciphertext)
   uint64_t g0 = 0;
   uint32_t* flags = nullptr;  // device: [1] |= precision failure, [2] = max logError
+  int reset = 1;              // the launch's flooding resets flags [1], [2] first (a call's first chunk)
 };
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,

@@ -514,19 +514,14 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   if (!nrows) return;
   if (nrows > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   const bool po = pout != nullptr, stk = lstride != 0;
-  // A/B probe switches, read per launch (profiles/probes/r03_wavg_packed_ab.txt): learners unrolled
-  // per iteration SHELFI_PACK_UNROLL=1|2|4|8, waves (rows) per block SHELFI_PACK_WAVES=2|4|8,
-  // XCD-contiguous block order SHELFI_PACK_XCD=1, round 3's four-accumulator kernel
-  // SHELFI_PACK_KERNEL=r3 (arena layout, uint64 output only)
+  // A/B probe switches, read per launch (profiles/probes/r03_wavg_packed_ab.txt,
+  // profiles/r04a/probes/): learners unrolled per iteration SHELFI_PACK_UNROLL=1|2|4(|8), waves (rows)
+  // per block SHELFI_PACK_WAVES=2|4|8, XCD-contiguous block order SHELFI_PACK_XCD=1, the round-4
+  // three-accumulator kernel SHELFI_PACK_KERNEL=v4 (the packed-output and stacked forms always use
+  // it) and its two-waves-per-row form SHELFI_PACK_SPLIT=2.  Default: round 3's four-accumulator
+  // kernel, 2 learners per iteration, 4 rows per block -- 0.5-2.5% faster than v4 on every BASELINE
+  // shape in the same-process A/B (profiles/r04a/probes/wavg_kernel_ab.txt).
   const char* kenv = getenv("SHELFI_PACK_KERNEL");
-  if (kenv && kenv[0] == 'r' && kenv[1] == '3' && !po && crow == C && !lstride) {
-    const uint64_t blocks = (nrows + kPackedWaves - 1) / kPackedWaves;
-    if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-    hipLaunchKernelGGL((wavg_packed_r3<2, kPackedWaves>), dim3((uint32_t)blocks), dim3(64 * kPackedWaves), 0, s,
-                       in, wl_dev, C, nrows, L, logN, ap, tc, out, 0u);
-    SHELFI_HIP(hipGetLastError());
-    return;
-  }
   const char* env = getenv("SHELFI_PACK_UNROLL");
   const int u = env ? atoi(env) : 2;
   const char* wenv = getenv("SHELFI_PACK_WAVES");
@@ -534,7 +529,29 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   const char* xenv = getenv("SHELFI_PACK_XCD");
   const char* senv = getenv("SHELFI_PACK_SPLIT");
   const bool split = senv && *senv == '2' && !po && !stk;
+  const bool v4 = po || stk || split || (kenv && kenv[0] == 'v' && kenv[1] == '4');
   const int wvs = (wv == 2 || wv == 8) && u == 2 && !po && !stk ? wv : kPackedWaves;
+  if (!v4) {
+    const uint64_t blocks = (nrows + wvs - 1) / wvs;
+    if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+    const uint32_t xcd = xenv && *xenv == '1' && blocks % 8 == 0 ? 1u : 0u;
+#define WPK3(UU, WW)                                                                                         \
+  hipLaunchKernelGGL((wavg_packed_r3<UU, WW>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s, in, wl_dev, C, nrows, \
+                     L, logN, ap, tc, out, xcd)
+    if (wvs == 2)
+      WPK3(2, 2);
+    else if (wvs == 8)
+      WPK3(2, 8);
+    else if (u == 1)
+      WPK3(1, 4);
+    else if (u == 4)
+      WPK3(4, 4);
+    else
+      WPK3(2, 4);
+#undef WPK3
+    SHELFI_HIP(hipGetLastError());
+    return;
+  }
   const uint64_t rows_per_block = split ? kPackedWaves / 2 : wvs;
   const uint64_t blocks = (nrows + rows_per_block - 1) / rows_per_block;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};

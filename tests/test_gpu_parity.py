@@ -210,11 +210,18 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
         got = ar.wavg(w)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), unroll
+    monkeypatch.setenv("SHELFI_PACK_KERNEL", "v4")
+    for unroll in ("1", "2", "4", "8"):
+        monkeypatch.setenv("SHELFI_PACK_UNROLL", unroll)
+        got = ar.wavg(w)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), ("v4", unroll)
+    monkeypatch.delenv("SHELFI_PACK_KERNEL")
     monkeypatch.delenv("SHELFI_PACK_UNROLL")
     # the probe switches: rows per block, XCD-contiguous block order, two waves per row (learners
-    # split), round 3's four-accumulator kernel
+    # split), the round-4 three-accumulator kernel (also under every unroll depth)
     for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_XCD", "1"),
-                     ("SHELFI_PACK_SPLIT", "2"), ("SHELFI_PACK_KERNEL", "r3")):
+                     ("SHELFI_PACK_SPLIT", "2"), ("SHELFI_PACK_KERNEL", "v4")):
         monkeypatch.setenv(env, val)
         got = ar.wavg(w)
         torch.cuda.synchronize()

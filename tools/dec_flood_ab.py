@@ -30,8 +30,12 @@ def main():
     dec = D.decrypt(ck, ct, K * B, delta)
     torch.cuda.synchronize()
     res = {False: [], True: []}
-    for r in range(rounds):
-        for flood in ((False, True) if r % 2 == 0 else (True, False)):
+    # ORDER=block: every exact call first, then every flooded one (bench.py's order before round 4)
+    block = os.environ.get("ORDER", "alt") == "block"
+    seq = ([False] * rounds + [True] * rounds) if block else \
+        [f for r in range(rounds) for f in ((False, True) if r % 2 == 0 else (True, False))]
+    for flood in seq:
+        if True:
             ck.set_decode_noise(flood)
             t0 = time.perf_counter()
             D.decrypt(ck, ct, K * B, delta, out=dec)

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Effective clock per dispatch of the decrypt chain (MI355X_MICROARCH.md 'DVFS': GRBM_GUI_ACTIVE / 8
+XCDs / wall time), from one rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace run: counter_collection.csv
+joined with kernel_trace.csv on the dispatch id.  Each decrypt call is labelled exact or flooded by its
+FFT pass (fft_fwd_blocks_ct<..., false|true>); prints per call the INTT / CRT / FFT kernels' us and GHz,
+then the medians per label.
+  python tools/grbm_clock.py DIR"""
+import collections
+import csv
+import glob
+import os
+import statistics
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not cc or not kt:
+        sys.exit("no counter_collection.csv / kernel_trace.csv under %s" % d)
+    grbm = collections.defaultdict(float)
+    for r in csv.DictReader(open(cc[0])):
+        if r.get("Counter_Name") == "GRBM_GUI_ACTIVE":
+            grbm[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    rows = []
+    for r in csv.DictReader(open(kt[0])):
+        did = r["Dispatch_Id"]
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        ghz = grbm[did] / 8 / (us * 1e3) if did in grbm and us > 0 else float("nan")
+        rows.append((int(r["Start_Timestamp"]), r["Kernel_Name"], us, ghz))
+    rows.sort()
+    short = lambda n: n.replace("void ", "").replace("shelfi::", "").split("(")[0]
+    calls, cur = [], []
+    for t, name, us, ghz in rows:
+        nm = short(name)
+        if nm.startswith("ntt_inv_blocks_dec") and cur:
+            calls.append(cur)
+            cur = []
+        cur.append((nm, us, ghz))
+    if cur:
+        calls.append(cur)
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for c in calls:
+        names = [n for n, _, _ in c]
+        if not names[0].startswith("ntt_inv_blocks_dec"):
+            continue
+        # fft_fwd_blocks_ct<BL, K1, K2, K3, K4, FLOOD[, SWZ]>: the sixth template argument
+        def flood_arg(n):
+            args = n[n.index("<") + 1:n.rindex(">")].split(",")
+            return len(args) >= 6 and args[5].strip() == "true"
+        label = "flooded" if any(n.startswith("fft_fwd_blocks_ct") and flood_arg(n) for n in names) else "exact"
+        print("%-8s " % label + "  ".join("%s %.1fus %.2fGHz" % (n.split("<")[0], us, g) for n, us, g in c
+                                         if not n.startswith("__amd")))
+        for n, us, g in c:
+            per[label][n.split("<")[0]].append((us, g))
+    for label, ks in per.items():
+        print("median %s:" % label)
+        for n, v in ks.items():
+            print("   %-26s %8.1f us  %.2f GHz  (%d calls)" % (n, statistics.median(x for x, _ in v),
+                                                             statistics.median(g for _, g in v), len(v)))
+
+
+if __name__ == "__main__":
+    main()

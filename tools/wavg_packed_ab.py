@@ -5,6 +5,8 @@ events around each round, outputs compared bit for bit.  Prints achieved TB/s (t
 arena's bytes + the uint64 aggregate per launch) per shape and variant, median over rounds.
 
 usage: AB_ENV=SHELFI_PACK_UNROLL AB_VARIANTS=1,2,4 python tools/wavg_packed_ab.py [rounds] [launches]
+A variant may set several switches: AB_VARIANTS="SHELFI_PACK_KERNEL=r3,SHELFI_PACK_KERNEL=v4+SHELFI_PACK_UNROLL=8"
+(a variant containing '=' names its own VAR=VAL pairs, joined by '+').
 """
 import os
 import sys
@@ -27,6 +29,21 @@ SHAPES = [  # name, batch, multDepth, C, K
 ENV = os.environ.get("AB_ENV", "SHELFI_PACK_UNROLL")
 VARIANTS = os.environ.get("AB_VARIANTS", "1,2,4").split(",")
 ONLY = os.environ.get("AB_SHAPES")
+
+
+_SET = set()
+
+
+def set_variant(v):
+    for k in _SET:
+        os.environ.pop(k, None)
+    _SET.clear()
+    if not v:
+        return
+    pairs = [p.split("=", 1) for p in v.split("+")] if "=" in v else [(ENV, v)]
+    for k, val in pairs:
+        os.environ[k] = val
+        _SET.add(k)
 
 
 def main():
@@ -58,7 +75,7 @@ def main():
         ref = None
         for r in range(rounds):
             for v in VARIANTS if r % 2 == 0 else VARIANTS[::-1]:
-                os.environ[ENV] = v
+                set_variant(v)
                 ar.wavg(w, out=out)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
@@ -74,11 +91,12 @@ def main():
         line = [name]
         for v in VARIANTS:
             ms = float(np.median(res[v]))
-            line.append("%s=%s %.4f ms %.3f TB/s (%.3f of 8)" % (ENV, v, ms, nbytes / ms / 1e9, nbytes / ms / 8e9))
+            line.append("%s %.4f ms %.3f TB/s (%.3f of 8)" % (v if "=" in v else "%s=%s" % (ENV, v), ms,
+                                                               nbytes / ms / 1e9, nbytes / ms / 8e9))
         print(" | ".join(line), flush=True)
         del ar, out, ref
         torch.cuda.empty_cache()
-    os.environ.pop(ENV, None)
+    set_variant("")
 
 
 if __name__ == "__main__":
