@@ -86,6 +86,9 @@ def parse():
                          "the sums to the consumer, shelfi_dev_decrypt_sum folds them on load)")
     ap.add_argument("--layout", choices=["arena", "separate"], default="arena",
                     help="resident layout of the learners' ciphertexts (arena = interleaved)")
+    ap.add_argument("--arena-layout", choices=["auto", "packed", "uint64"], default="auto",
+                    help="--layout arena: Arena's layout (auto = uint64 learner batches for arenas of at most "
+                         "Arena.AUTO_U64_ROWS rows per learner, e.g. cfg2; packed otherwise)")
     ap.add_argument("--place-output", type=int, default=16,
                     help="arena layout, no collective: time this many candidate output buffers before "
                          "the timed region and keep the fastest placement (Arena.place_output; the "
@@ -349,7 +352,10 @@ def main():
             del x
         weights = [weight] * C_loc
         # the aggregator's resident layout: learners interleaved in one arena
-        arena = D.Arena(ck, C_loc, K_loc, device=dev)
+        lay = args.arena_layout
+        if shard == "learners" and (args.combine == "shelfi" or args.exchange == "packed"):
+            lay = "packed"  # the C-ABI combine and the packed exchange read the packed layout
+        arena = D.Arena(ck, C_loc, K_loc, device=dev, layout=lay)
         for i, ct in enumerate(cts):
             arena.put(i, ct)
         torch.cuda.synchronize()
@@ -357,7 +363,7 @@ def main():
             cts = None
         comb = None
         placement = None
-        if args.layout == "arena" and shard != "learners" and args.place_output > 0:
+        if args.layout == "arena" and arena.layout == "packed" and shard != "learners" and args.place_output > 0:
             # where the aggregate lands in HBM relative to the arena moves the launch time by
             # up to 12%: keep the fastest of a few candidate buffers; the penalty
             # follows ~3 GiB address ranges (probes/r03_placement_alloc.txt), so 16 candidates
@@ -423,12 +429,14 @@ def main():
 
         step = step_of(comb)
 
-        # the launch's input bytes: the packed arena or C uint64 batches
+        # the launch's input bytes: the packed arena or C uint64 batches (the separate
+        # layout, or an arena small enough for Arena's uint64 layout)
         in_bytes = arena.buf.numel() * 8 if args.layout == "arena" else C_loc * K_loc * 2 * L * N * 8
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
                 "in_bytes": in_bytes,
                 "enc_times": enc_times, "kernel": kernel, "kernel_into": kernel_into, "step": step, "piece": piece, "comb": comb, "weights": weights,
-                "cts": cts, "placement": placement, "make_comb": make_comb, "step_of": step_of}
+                "cts": cts, "placement": placement, "make_comb": make_comb, "step_of": step_of,
+                "arena_layout": arena.layout}
 
     def timed(mode):
         """warmup, then exactly `steps` steps between barrier + sync; max over ranks.
@@ -763,12 +771,13 @@ def main():
     # (K * 2 * N * sum_t U_t / 8 each, U_t ~ bitlength(q_t)) read once
     # + the uint64 aggregate K * 2 * L * N * 8 written once
     bytes_per_launch = main_mode["in_bytes"] + K_loc * 2 * L * N * 8
+    packed = args.layout == "arena" and main_mode["arena_layout"] == "packed"
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        kname = "wavg_packed" if args.layout == "arena" else "wavg_kernel"
+        kname = "wavg_packed" if packed else "wavg_kernel"
         if (tj.get("workload") == args.workload and tj.get("learners") == C_loc and K_loc == K
                 and str(tj.get("kernel", "")).startswith(kname)
                 and int(tj.get("algorithmic_bytes_per_launch", -1)) == bytes_per_launch):
@@ -777,10 +786,12 @@ def main():
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "wavg_packed" if args.layout == "arena" else "wavg_kernel",
+                "kernel": "wavg_packed" if packed else "wavg_kernel",
                 "bytes_per_launch": bytes_per_launch,
                 "launch_ms_avg": round(kern_avg_ms, 4), "launch_ms_min": round(kern_ms[0], 4)}
     if args.layout == "arena":
+        roofline["arena_layout"] = main_mode["arena_layout"]
+    if packed:
         # the packed arena's widths and what the same launch amounts to in uint64
         # residues (the rounds-1/2 arena's bytes): an effective rate, not a fraction of any peak
         bits = [int(x).bit_length() for x in ck.info()["moduli"]]

@@ -130,6 +130,7 @@ SIGNATURES = {
                                                C.c_void_p]),
     "shelfi_dev_sum_packed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
+    "shelfi_dev_check_residues": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "shelfi_dev_wavg_arena": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t, C.c_void_p,
                                         C.c_void_p]),
     "shelfi_dev_wavg_arena_pick_output": (C.c_int, [C.c_void_p, C.c_void_p, f32p, C.c_size_t, C.c_size_t,

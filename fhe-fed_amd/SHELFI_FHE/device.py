@@ -90,17 +90,35 @@ class Arena:
     packs and validates each learner's batch once per round; wavg() then reads one
     contiguous C-slice region per row and writes the [K][2][L][N] uint64 aggregate."""
 
-    def __init__(self, ckks, num_learners: int, K: int, device=None):
+    # layout="auto": arenas of at most this many 512-residue rows per learner (K * 2 * L * N / 512)
+    # take the uint64 layout.  A packed launch is one wave per row over all C learners; a grid of
+    # a few thousand rows (cfg2: 2,048 rows = 2 waves per SIMD) cannot hide its ramp and tail, and
+    # wavg_kernel's 4x as many shorter waves over uint64 batches run it 9% faster (bench.py cfg2:
+    # 24.2 vs 26.5 us per step, profiles/r04b); from cfg5's 79,872 rows on, the packed bytes win.
+    AUTO_U64_ROWS = 4096
+
+    def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "auto"):
         torch = _torch()
         self.ckks, self.C, self.K = ckks, int(num_learners), int(K)
         inf = ckks.info()
         self.L, self.N = inf["num_towers"], inf["ring_dim"]
         if device is None:
             device = "cuda:%d" % inf["device"]
+        if layout == "auto":
+            layout = "uint64" if self.K * 2 * self.L * (self.N // 512) <= self.AUTO_U64_ROWS else "packed"
+        if layout not in ("packed", "uint64"):
+            raise ValueError("layout must be 'packed', 'uint64' or 'auto'")
+        self.layout = layout
         lib = _lib.load()
         # the packed layout is sized by the context's moduli: an arena belongs to this parameter
         # generation (loadCryptoParams / genCryptoContextAndKeyGen start a new one)
         self._gen = getattr(ckks, "_params_gen", 0)
+        if layout == "uint64":
+            # C learner batches [K][2][L][N] one after the other, aggregated by wavg_kernel
+            self.ct_words = 2 * self.L * self.N
+            self.buf = torch.empty((self.C, self.K, 2, self.L, self.N), dtype=torch.int64, device=device)
+            self._refused = set()
+            return
         self.ct_words = lib.shelfi_arena_words(ckks._ctx, self.C, 1)  # packed words per ciphertext
         words = lib.shelfi_arena_words(ckks._ctx, self.C, self.K)
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
@@ -111,7 +129,7 @@ class Arena:
         if buf is None:
             return
         ctx = getattr(self.ckks, "_ctx", None)
-        if ctx is not None and getattr(ctx, "value", None):
+        if self.layout == "packed" and ctx is not None and getattr(ctx, "value", None):
             _lib.load().shelfi_dev_arena_release(ctx, C.c_void_p(buf.data_ptr()), buf.numel())
         self.buf = None
 
@@ -135,6 +153,9 @@ class Arena:
         every put then checks that each placed residue is < q_t, and a refused slot keeps
         wavg() failing until a valid put replaces it (shelfi_dev_arena_put[_blob])."""
         self._check_gen()
+        if self.layout == "uint64":
+            self._put_u64(int(learner), ct)
+            return
         if isinstance(ct, (bytes, bytearray, memoryview)):
             import numpy as np
 
@@ -151,6 +172,28 @@ class Arena:
                                                int(learner), self.C, C.c_void_p(self.buf.data_ptr()),
                                                C.c_void_p(_stream_ptr(ct))), "arena_put")
 
+    def _put_u64(self, learner: int, ct):
+        """uint64 layout: the batch lands in its slot and is checked (residues < q_t); an upload is
+        validated exactly as the packed layout's (header against the context, then residues) by
+        placing it in a one-learner packed arena and summing that with unit weight into the slot."""
+        if not (0 <= learner < self.C):
+            raise ValueError("learner index outside the arena")
+        self._refused.add(learner)  # until this put has landed and passed its checks
+        if isinstance(ct, (bytes, bytearray, memoryview)):
+            tmp = Arena(self.ckks, 1, self.K, device=self.buf.device, layout="packed")
+            tmp.put(0, ct)
+            sum_packed(self.ckks, tmp.buf, 1, self.K, tmp.ct_words * self.K, out=self.buf[learner])
+            tmp.release()
+        else:
+            _check_ct(ct, self.ckks, self.K)
+            if ct.device != self.buf.device:
+                raise ValueError("the batch must live on the arena's device")
+            self.buf[learner].copy_(ct)
+            check(_lib.load().shelfi_dev_check_residues(self.ckks._ctx, C.c_void_p(self.buf[learner].data_ptr()),
+                                                        self.K, C.c_void_p(_stream_ptr(self.buf))),
+                  "arena_put: learner %d" % learner)
+        self._refused.discard(learner)
+
     def wavg(self, weights: Sequence[float], out=None, k0: int = 0, k1: int | None = None):
         """Aggregate ciphertexts [k0, k1) of every learner into out[:k1-k0]."""
         torch = _torch()
@@ -164,6 +207,11 @@ class Arena:
         if out is None:
             out = torch.empty((Kr, 2, self.L, self.N), dtype=torch.int64, device=self.buf.device)
         _check_ct(out, self.ckks, Kr)
+        if self.layout == "uint64":
+            if self._refused:
+                raise _lib.ShelfiError(_lib.SHELFI_ERR_STATE, "dev_wavg_arena: the arena holds a refused upload "
+                                       "for learner %d; put a valid batch first" % min(self._refused))
+            return wavg(self.ckks, [self.buf[c, k0:k1] for c in range(self.C)], weights, out=out)
         w = (C.c_float * self.C)(*[float(x) for x in weights])
         # ciphertexts [k0, k1) of an arena are themselves an arena of k1-k0 ciphertexts
         base = self.buf.data_ptr() + k0 * self.ct_words * 8
@@ -178,6 +226,8 @@ class Arena:
         tensor of packed_words(k1 - k0) words): the packed share exchange's send form."""
         torch = _torch()
         self._check_gen()
+        if self.layout != "packed":
+            raise ValueError("a packed aggregate comes from the packed layout (Arena(..., layout='packed'))")
         if len(weights) != self.C:
             raise ValueError("need one weight per learner")
         k1 = self.K if k1 is None else int(k1)
@@ -204,6 +254,11 @@ class Arena:
         candidates too, ahead of the new ones.  Returns (buffer, per-candidate ms)."""
         torch = _torch()
         self._check_gen()
+        if self.layout != "packed":  # separate batches: no placement search (DESIGN.md §5.2)
+            out = include[0] if include else torch.empty((self.K, 2, self.L, self.N), dtype=torch.int64,
+                                                         device=self.buf.device)
+            self.wavg(weights, out=out)
+            return out, []
         cands = list(include)
         for c in cands:
             _check_ct(c, self.ckks, self.K)

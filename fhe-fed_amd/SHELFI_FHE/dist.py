@@ -326,6 +326,8 @@ class Comm:
         import ctypes as C
         from .device import _check_ct, _stream_ptr
 
+        if getattr(arena, "layout", "packed") != "packed":
+            raise ValueError("the C-ABI combine aggregates a packed arena (Arena(..., layout='packed'))")
         Ks = self.share_cts(K)
         _check_ct(share, self._ckks, Ks)
         _check_ct(send, self._ckks, self.world * Ks)
@@ -345,6 +347,8 @@ class Comm:
         import ctypes as C
         from .device import _check_ct, _stream_ptr
 
+        if getattr(arena, "layout", "packed") != "packed":
+            raise ValueError("the C-ABI combine aggregates a packed arena (Arena(..., layout='packed'))")
         Ks = self.share_cts(K)
         _check_ct(share, self._ckks, Ks)
         need = self.packed_buffer_words(K)

@@ -1550,6 +1550,24 @@ int shelfi_dev_wavg(shelfi_ctx* ctx, const uint64_t* const* in_dev, const float*
   });
 }
 
+int shelfi_dev_check_residues(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, void* stream) {
+  if (!ctx || (K && !ct_dev)) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return guarded([&] {
+    if (!K) return;
+    DeviceGuard g(ctx->device);
+    const Params& p = ctx->p;
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* bad = ctx->dev_flag + 6;
+    SHELFI_HIP(hipMemsetAsync(bad, 0, 4, s));
+    launch_check_residues(ct_dev, (uint64_t)K * 2 * p.L, p.L, p.logN, ctx->dt.tc, bad, s);
+    SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 6, bad, 4, hipMemcpyDeviceToHost, s));
+    SHELFI_HIP(hipStreamSynchronize(s));
+    if (ctx->host_flag[6])
+      throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed batch)"};
+  });
+}
+
 size_t shelfi_arena_words(const shelfi_ctx* ctx, size_t C, size_t K) {
   if (!ctx) return 0;
   return (size_t)arena_ct_words(ctx->p, C) * K;

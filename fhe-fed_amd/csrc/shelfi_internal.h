@@ -185,7 +185,8 @@ struct shelfi_ctx {
   uint32_t* host_flag = nullptr; // pinned host mirror of dev_flag (async readback before one sync)
   uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
                                  // [2] max decode logError (noise flooding), [3] bytes-API
-                                 // upload residue >= q, [4] arena upload residue >= q
+                                 // upload residue >= q, [4] arena upload residue >= q, [5] the
+                                 // packed wire's pack check, [6] shelfi_dev_check_residues
   // arena slots whose last upload was refused (shelfi_dev_arena_put*): an aggregation
   // over an arena range holding one fails instead of summing the refused residues
   // (an entry names the arena by its base, its shelfi_arena_words(C, K) span and C, so a later
@@ -275,6 +276,9 @@ void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t lo
                         uint64_t* dst, hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
+// *bad |= 1 when a residue of the [rows / (2 L)][2][L][N] batch is >= its tower's q
+void launch_check_residues(const uint64_t* ct, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
+                           uint32_t* bad, hipStream_t s);
 void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                 const DeviceTables& dt, hipStream_t s);
 void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,

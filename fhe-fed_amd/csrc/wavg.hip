@@ -701,6 +701,27 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   SHELFI_HIP(hipGetLastError());
 }
 
+// Every residue of a [K][2][L][N] batch < q_t? (*bad |= 1 otherwise): the uint64 arena layout's
+// upload check (the packed layout checks while packing, arena_pack_kernel).
+__global__ __launch_bounds__(256) void check_residues_kernel(const uint64_t* __restrict__ ct, uint32_t L,
+                                                             uint32_t logN, const TowerConst* __restrict__ tcs,
+                                                             uint32_t* __restrict__ bad) {
+  const uint64_t base = (uint64_t)blockIdx.x * 512;
+  const uint32_t t = (uint32_t)((base >> logN) % L);
+  const uint64_t q = tcs[t].q;
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ct + base + 2u * threadIdx.x));
+  if ((((uint64_t)v.y << 32) | v.x) >= q || (((uint64_t)v.w << 32) | v.z) >= q) atomicOr(bad, 1u);
+}
+
+void launch_check_residues(const uint64_t* ct, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
+                           uint32_t* bad, hipStream_t s) {
+  const uint64_t blocks = (rows << logN) / 512;
+  if (!blocks) return;
+  if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "batch too large"};
+  hipLaunchKernelGGL(check_residues_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ct, L, logN, tc, bad);
+  SHELFI_HIP(hipGetLastError());
+}
+
 // A collective's uint64 sum of G <= 15 partial sums (each < q < 2^60) -> [0, q).
 __global__ __launch_bounds__(256) void modq_kernel(uint64_t* buf, uint32_t L, uint32_t logN,
                                                    const TowerConst* __restrict__ tcs) {

@@ -239,6 +239,10 @@ int shelfi_dev_arena_put_blob(shelfi_ctx* ctx, const uint8_t* blob, size_t len, 
  * into a differently shaped arena over the same memory, and a parameter or key reload, drop
  * stale marks by themselves. */
 int shelfi_dev_arena_release(shelfi_ctx* ctx, const uint64_t* arena_dev, size_t words);
+/* Host-synchronous check that every residue of a [K][2][L][N] device batch is < q_t
+ * (SHELFI_ERR_FORMAT otherwise): the upload check of SHELFI_FHE.device.Arena's uint64 layout, which
+ * small launches aggregate with shelfi_dev_wavg (the packed arena checks while packing). */
+int shelfi_dev_check_residues(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, void* stream);
 /* shelfi_dev_wavg over an arena of C learners (same arithmetic and result). */
 int shelfi_dev_wavg_arena(shelfi_ctx* ctx, const uint64_t* arena_dev, const float* w, size_t C,
                           size_t K, uint64_t* out_dev, void* stream);

@@ -44,7 +44,7 @@ def test_device_api_rejects_unrepresentable_weights(ck, bad, C):
     w[-1] = bad
     with pytest.raises(ValueError, match="scaling factor"):
         D.wavg(ck, cts, w)
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for i in range(C):
         ar.put(i, cts[i])
     with pytest.raises(ValueError, match="scaling factor"):

@@ -87,7 +87,7 @@ def test_valid_blobs_aggregate_like_the_bytes_api(c2):
     xs = _xs(4, K * B - 77)
     blobs = [c2.encrypt(x) for x in xs]
     w = [0.1, 0.2, 0.3, 0.4]
-    ar = D.Arena(c2, 4, K)
+    ar = D.Arena(c2, 4, K, layout="packed")
     for i, b in enumerate(blobs):
         ar.put(i, b)
     got = ar.wavg(w).cpu().numpy().view(np.uint64)
@@ -102,7 +102,7 @@ def test_same_k_blob_of_smaller_parameters_is_refused_before_any_copy(c2, c1):
     it would fault this process."""
     small = c1.encrypt(np.linspace(-1, 1, K * 4096))
     assert m.blob_info(small)["num_cts"] == K
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     g = GuardedBuffer(small)
     rc = _put_raw(c2, ar, 0, g.ptr, g.n)
     assert rc == _lib.SHELFI_ERR_FORMAT, (rc, _err())
@@ -114,7 +114,7 @@ def test_same_k_blob_of_smaller_parameters_is_refused_before_any_copy(c2, c1):
 def test_blob_under_another_key_is_refused(c2, c2_other_key):
     B = c2.info()["batch"]
     other = c2_other_key.encrypt(np.linspace(-1, 1, K * B))
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     g = GuardedBuffer(other)
     rc = _put_raw(c2, ar, 1, g.ptr, g.n)
     assert rc == _lib.SHELFI_ERR_FORMAT and "different key" in _err()
@@ -122,7 +122,7 @@ def test_blob_under_another_key_is_refused(c2, c2_other_key):
 
 def test_wrong_ciphertext_count_and_truncation_are_refused(c2):
     B = c2.info()["batch"]
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     with pytest.raises(m.ShelfiError, match="ciphertexts"):
         ar.put(0, c2.encrypt(np.zeros((K - 1) * B)))
     blob = c2.encrypt(np.zeros(K * B))
@@ -140,7 +140,7 @@ def test_non_canonical_residue_is_refused_and_poisons_the_slot(c2, where):
     xs = _xs(3, K * B)
     blobs = [c2.encrypt(x) for x in xs]
     w = [0.5, 0.25, 0.25]
-    ar = D.Arena(c2, 3, K)
+    ar = D.Arena(c2, 3, K, layout="packed")
     for i, b in enumerate(blobs):
         ar.put(i, b)
     good = ar.wavg(w).cpu().numpy().view(np.uint64).copy()
@@ -164,7 +164,7 @@ def test_device_tensor_with_non_canonical_residue_is_refused(c2):
     cts = [D.encrypt(c2, torch.tensor(x, device="cuda")) for x in _xs(2, K * B)]
     bad = cts[0].clone()
     bad[2, 0, 3, 5] = -1  # 2^64 - 1
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     ar.put(1, cts[1])
     with pytest.raises(m.ShelfiError, match="residue"):
         ar.put(0, bad)
@@ -187,7 +187,7 @@ def test_palisade_archives_are_placed_and_other_keys_refused(c1):
     xs = _xs(3, K * 4096 - 5)
     arch = [ck.encrypt(x) for x in xs]
     w = [0.2, 0.3, 0.5]
-    ar = D.Arena(ck, 3, K)
+    ar = D.Arena(ck, 3, K, layout="packed")
     for i, a in enumerate(arch):
         ar.put(i, a)
     got = ar.wavg(w).cpu().numpy().view(np.uint64)
@@ -227,7 +227,7 @@ def test_arena_refuses_use_after_params_reload(tmp_path):
     d = str(tmp_path) + os.sep
     ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
-    ar = D.Arena(ck, 2, 1)
+    ar = D.Arena(ck, 2, 1, layout="packed")
     x = torch.zeros((1, 2, 4, 32768), dtype=torch.int64, device="cuda")
     ar.put(0, x)
     ar.put(1, x)
@@ -284,7 +284,7 @@ def test_stale_refusal_does_not_outlive_its_arena(c2):
     assert lib.shelfi_dev_arena_release(c2._ctx, ctypes.c_void_p(base), w8) == 0
     assert _raw_put(c2, base, 4, K, 2, cts[2]) == 0
     assert _raw_wavg(c2, base, w, K, out) == 0
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     with pytest.raises(m.ShelfiError):
         ar.put(0, bad)
     ar.release()
@@ -299,7 +299,7 @@ def test_refused_header_marks_the_slot(c2, c2_other_key):
     B = c2.info()["batch"]
     xs = _xs(2, K * B)
     blobs = [c2.encrypt(x) for x in xs]
-    ar = D.Arena(c2, 2, K)
+    ar = D.Arena(c2, 2, K, layout="packed")
     for i, b in enumerate(blobs):
         ar.put(i, b)
     w = [0.5, 0.5]

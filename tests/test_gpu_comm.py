@@ -110,7 +110,7 @@ def test_pipelined_c_abi_combine_one_rank(ck, C, K, pieces, fold):
     rng = np.random.default_rng(C * 100 + K)
     cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B - 3)).cuda()) for _ in range(C)]
     w = list(rng.dirichlet(np.ones(C)))
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for i, c in enumerate(cts):
         ar.put(i, c)
     ref = ar.wavg(w)
@@ -170,7 +170,7 @@ def test_packed_output_and_stacked_sum(ck, C, K):
     rng = np.random.default_rng(C + K)
     cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B)).cuda()) for _ in range(C)]
     w = list(rng.dirichlet(np.ones(C)))
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for i, c in enumerate(cts):
         ar.put(i, c)
     ref = ar.wavg(w)
@@ -207,7 +207,7 @@ def test_packed_exchange_c_abi_combine_one_rank(ck, C, K, pieces):
     rng = np.random.default_rng(C * 10 + K)
     cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B - 5)).cuda()) for _ in range(C)]
     w = list(rng.dirichlet(np.ones(C)))
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for i, c in enumerate(cts):
         ar.put(i, c)
     ref = ar.wavg(w)
@@ -250,7 +250,7 @@ def test_packed_pipelined_combine_torch_one_rank(ck, tmp_path):
         rng = np.random.default_rng(77)
         cts = [D.encrypt(ck, torch.from_numpy(rng.uniform(-1, 1, K * B)).cuda()) for _ in range(C)]
         w = list(rng.dirichlet(np.ones(C)))
-        ar = D.Arena(ck, C, K)
+        ar = D.Arena(ck, C, K, layout="packed")
         for i, c in enumerate(cts):
             ar.put(i, c)
         ref = ar.wavg(w)

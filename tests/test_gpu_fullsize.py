@@ -65,7 +65,7 @@ def test_cfg3_shard_full_size_arena_and_pointer_kernels(cfg2):
     L, C, K = len(q), 16, 714
     cts = _random_cts(C, K, L, N, q, 2024)
     w = [1.0 / C] * C
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for c in range(C):
         ar.put(c, cts[c])
     tuned, ms = ar.place_output(w, candidates=4, launches=1)  # the bench's timed kernel
@@ -83,7 +83,7 @@ def test_cfg3_ciphertext_sharded_shape_many_learners(cfg2):
     ck, q, N, delta = cfg2
     L, C, K = len(q), 128, 89
     cts = _random_cts(C, K, L, N, q, 77)
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for c in range(C):
         ar.put(c, cts[c])
     w1 = [1.0 / C] * C
@@ -101,7 +101,7 @@ def test_cfg4_full_size(tmp_path):
     L, C, K = len(q), 16, 32
     cts = _random_cts(C, K, L, N, q, 99)
     w = list(np.random.default_rng(9).dirichlet(np.ones(C)))
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for c in range(C):
         ar.put(c, cts[c])
     outs = {"arena": ar.wavg(w), "pointers": D.wavg(ck, cts, w)}

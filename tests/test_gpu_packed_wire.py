@@ -93,7 +93,7 @@ def test_packed_blob_into_arena(c2):
     xs = [np.random.default_rng(40 + i).uniform(-1, 1, 3 * S) for i in range(3)]
     u64 = [_enc(ck, x, "shelfi", 200 + i) for i, x in enumerate(xs)]
     pk = [_enc(ck, x, "packed", 200 + i) for i, x in enumerate(xs)]
-    a, b = D.Arena(ck, 3, 3), D.Arena(ck, 3, 3)
+    a, b = D.Arena(ck, 3, 3, layout="packed"), D.Arena(ck, 3, 3, layout="packed")
     for i in range(3):
         a.put(i, u64[i])
         b.put(i, pk[i])
@@ -151,7 +151,7 @@ def test_packed_blob_validation(c1, c2):
             ck.decrypt(good[:-4], 2 * S)
         with pytest.raises((ValueError, RuntimeError)):
             ck.decrypt(small, 100)
-        ar = D.Arena(ck, 2, 2)
+        ar = D.Arena(ck, 2, 2, layout="packed")
         with pytest.raises(m.ShelfiError, match="residue"):
             ar.put(0, bad)
         with pytest.raises(m.ShelfiError, match="parameters"):

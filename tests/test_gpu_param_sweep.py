@@ -87,12 +87,17 @@ def test_sweep_row_bitexact(tmp_path, batch, sb):
     assert float(np.abs(dec - exp).max()) < 2.0 ** 18 / delta
 
     # the packed resident arena (17/21-bit towers at the 32-bit width class)
-    ar = D.Arena(ck, 3, K)
+    ar = D.Arena(ck, 3, K, layout="packed")
     for c, b in enumerate(blobs):
         ar.put(c, b)
     got = ar.wavg(w)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), ref)
+    au = D.Arena(ck, 3, K)  # a small arena: the uint64 layout
+    assert au.layout == "uint64"
+    for c, b in enumerate(blobs):
+        au.put(c, b)
+    assert torch.equal(au.wavg(w), got)
 
     # the default (flooded) decrypt: no precision failure, error within twice the bound
     ck.set_decode_noise(True)

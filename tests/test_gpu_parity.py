@@ -150,7 +150,7 @@ def test_wavg_arena_bitexact(cfg2, C, K):
             a[:, :, t, :] = rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
         cts.append(a)
     w = list(rng.dirichlet(np.ones(C)))
-    ar = D.Arena(cfg2, C, K)
+    ar = D.Arena(cfg2, C, K, layout="packed")
     for c in range(C):
         if c % 2:
             ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
@@ -197,7 +197,7 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
             a[:, 0, t, :7] = int(q[t]) - 1
             a[:, 1, t, -5:] = 0
         cts.append(a)
-    ar = D.Arena(ck, C, K)
+    ar = D.Arena(ck, C, K, layout="packed")
     for c in range(C):
         if c % 3 == 1:
             ar.put(c, m.blob_pack(ck, cts[c]))
@@ -250,7 +250,7 @@ def test_arena_packed_layout_bytes(cfg1):
             if b % 4 == 1:
                 a[:, :, t, 100:140:5] = 1 << (b - 1)  # top bit only (< q: q > 2^(b-1))
         cts.append(a)
-    ar = D.Arena(cfg1, C, K)
+    ar = D.Arena(cfg1, C, K, layout="packed")
     ar.put(0, torch.from_numpy(cts[0].view(np.int64)).cuda())
     ar.put(1, m.blob_pack(cfg1, cts[1]))
     torch.cuda.synchronize()
@@ -270,7 +270,7 @@ def test_wavg_arena_many_learners_ranges_and_weights(cfg2):
         for t in range(L):
             a[:, :, t, :] = (int(q[t]) - 1) if c < 16 else rng.integers(0, int(q[t]), (K, 2, N), dtype=np.uint64)
         cts.append(a)
-    ar = D.Arena(cfg2, C, K)
+    ar = D.Arena(cfg2, C, K, layout="packed")
     for c in range(C):
         ar.put(c, torch.from_numpy(cts[c].view(np.int64)).cuda())
     wa = [1.0] * 16 + list(rng.dirichlet(np.ones(C - 16)))

@@ -44,7 +44,7 @@ def main():
         if own_out:  # a fresh output buffer allocated right before each arena
             out = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
             outs.append(out)
-        ar = D.Arena(ck, C, K)
+        ar = D.Arena(ck, C, K, layout="packed")
         v = ar.buf.view(-1, N)
         for t in range(L):
             v[t::L].random_(0, q[t])

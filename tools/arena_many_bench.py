@@ -20,7 +20,7 @@ def main():
     N, L, q = inf["ring_dim"], inf["num_towers"], inf["moduli"]
     for C in [int(x) for x in os.environ.get("CS", "16,32,64,128").split(",")]:
         K = 714 * 16 // C
-        ar = D.Arena(ck, C, K)
+        ar = D.Arena(ck, C, K, layout="packed")
         v = ar.buf.view(-1, N)  # rows of N residues; towers cycle with the row index
         for t in range(L):
             v[t::L].random_(0, q[t])

@@ -41,19 +41,19 @@ def main():
     C, K = 16, 714
     w = [1.0 / C] * C
     out = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
-    a1 = D.Arena(ck, C, K)
+    a1 = D.Arena(ck, C, K, layout="packed")
     fill(a1, N, L, q)
     time_arena(a1, w, out, "arena 1 (first allocation)")
     # churn: many 1.4 GiB tensors allocated and freed
     junk = [torch.empty(K * 2 * L * N, dtype=torch.int64, device="cuda") for _ in range(16)]
     del junk
     torch.cuda.empty_cache()
-    a2 = D.Arena(ck, C, K)
+    a2 = D.Arena(ck, C, K, layout="packed")
     fill(a2, N, L, q)
     time_arena(a2, w, out, "arena 2 (after churn, cache emptied)")
     time_arena(a1, w, out, "arena 1 again")
     junk = [torch.empty(K * 2 * L * N // 7, dtype=torch.int64, device="cuda") for _ in range(60)]
-    a3 = D.Arena(ck, C, K)
+    a3 = D.Arena(ck, C, K, layout="packed")
     fill(a3, N, L, q)
     del junk
     time_arena(a3, w, out, "arena 3 (amid small allocations)")

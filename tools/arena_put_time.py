@@ -27,7 +27,7 @@ def main():
     ck.set_wire_format("palisade")
     blobs["archive"] = ck.encrypt(x)
     ck.set_wire_format("shelfi")
-    ar = D.Arena(ck, 2, K)
+    ar = D.Arena(ck, 2, K, layout="packed")
     for name, b in blobs.items():
         res = {"0": [], "1": []}
         for r in range(4):

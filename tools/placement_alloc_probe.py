@@ -28,7 +28,7 @@ def main():
     assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
     L, N, q = inf["num_towers"], inf["ring_dim"], inf["moduli"]
-    ar = D.Arena(ck, Cn, K)
+    ar = D.Arena(ck, Cn, K, layout="packed")
     x = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
     for i in range(Cn):
         for t in range(L):

@@ -61,7 +61,7 @@ def main():
         inf = ck.info()
         L, N = inf["num_towers"], inf["ring_dim"]
         q = inf["moduli"]
-        ar = D.Arena(ck, C, K)
+        ar = D.Arena(ck, C, K, layout="packed")
         x = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
         for i in range(C):
             for t in range(L):

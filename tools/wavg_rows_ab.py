@@ -44,7 +44,7 @@ def main():
         inf = ck.info()
         L, N = inf["num_towers"], inf["ring_dim"]
         q = inf["moduli"]
-        ar = D.Arena(ck, C, K)
+        ar = D.Arena(ck, C, K, layout="packed")
         for i in range(C):
             x = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
             for t in range(L):
