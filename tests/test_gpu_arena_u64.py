@@ -48,10 +48,12 @@ def test_u64_layout_matches_packed_and_oracle(c2, C, K):
     w = list(rng.dirichlet(np.ones(C)))
     au = D.Arena(c2, C, K, layout="uint64")
     ap = D.Arena(c2, C, K, layout="packed")
+    res = [c.cpu().numpy().view(np.uint64) for c in cts]
+    res[1] = m.blob_residues(blob, inf["ring_dim"], inf["num_towers"])  # learner 1 arrives as an upload
     for i, c in enumerate(cts):
-        au.put(i, c if i != 1 else blob)  # a tensor and an upload
-        ap.put(i, c)
-    ref = O.wavg([c.cpu().numpy().view(np.uint64) for c in cts], w, q, delta)
+        au.put(i, c if i != 1 else blob)
+        ap.put(i, c if i != 1 else blob)
+    ref = O.wavg(res, w, q, delta)
     got = au.wavg(w)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), ref)

@@ -19,5 +19,11 @@ for i in 1 2; do
 done
 grep -v amdgpu.ids $out/lib_ab.txt
 run 400 python bench.py > $out/bench_cfg3.json 2> $out/bench_cfg3.err
-python -c "import json; d=json.load(open('$out/bench_cfg3.json')); print(d['value'], d['roofline']['frac'], d['encode_encrypt_ms_per_ct'], d['decrypt_decode_ms_per_ct'], d['decrypt_decode_flooded_ms_per_ct'])"
+for w in cfg2 cfg5 cfg4; do
+  run 300 python bench.py --workload $w --no-cpu-baseline --api-cts 0 --f4-cts 0 > $out/bench_$w.json 2> $out/bench_$w.err
+  run 300 python bench.py --workload $w --layout separate --no-cpu-baseline --api-cts 0 --f4-cts 0 > $out/bench_${w}_separate.json 2> $out/bench_${w}_separate.err
+done
+for f in $out/bench_cfg*.json; do
+  python -c "import json; d=json.load(open('$f')); r=d['roofline']; print('$f', d['value'], d['ms_per_step'], r.get('frac'), r.get('arena_layout'), d.get('decrypt_decode_ms_per_ct'), d.get('decrypt_decode_flooded_ms_per_ct'), d.get('encode_encrypt_ms_per_ct'))"
+done
 echo probe_r04d done
