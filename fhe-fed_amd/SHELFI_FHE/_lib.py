@@ -190,7 +190,10 @@ def load():
                 "libshelfi.so not found at %s — build it with `make -C fhe-fed_amd/csrc` "
                 "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
         lib = C.CDLL(LIB_PATH)
+        ab = "SHELFI_LIB_AB" in os.environ  # an older build for an A/B probe may lack newer entries
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(lib, name):
+                continue
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args

@@ -518,18 +518,21 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   // profiles/r04a/probes/): learners unrolled per iteration SHELFI_PACK_UNROLL=1|2|4(|8), waves (rows)
   // per block SHELFI_PACK_WAVES=2|4|8, XCD-contiguous block order SHELFI_PACK_XCD=1, the round-4
   // three-accumulator kernel SHELFI_PACK_KERNEL=v4 (the packed-output and stacked forms always use
-  // it) and its two-waves-per-row form SHELFI_PACK_SPLIT=2.  Default: round 3's four-accumulator
-  // kernel, 2 learners per iteration, 4 rows per block -- 0.5-2.5% faster than v4 on every BASELINE
-  // shape in the same-process A/B (profiles/r04a/probes/wavg_kernel_ab.txt).
+  // it) and its two-waves-per-row form SHELFI_PACK_SPLIT=2.  Without switches the launch picks by
+  // shape from the same-process A/Bs (profiles/r04a/probes/wavg_kernel_ab.txt, r04d/): see auto_v4.
   const char* kenv = getenv("SHELFI_PACK_KERNEL");
   const char* env = getenv("SHELFI_PACK_UNROLL");
-  const int u = env ? atoi(env) : 2;
   const char* wenv = getenv("SHELFI_PACK_WAVES");
   const int wv = wenv ? atoi(wenv) : kPackedWaves;
   const char* xenv = getenv("SHELFI_PACK_XCD");
   const char* senv = getenv("SHELFI_PACK_SPLIT");
+  const int u = env ? atoi(env) : (!kenv && !wenv && C == 16 && nrows >= 16384 ? 8 : 2);
   const bool split = senv && *senv == '2' && !po && !stk;
-  const bool v4 = po || stk || split || (kenv && kenv[0] == 'v' && kenv[1] == '4');
+  // default: v4 with 8 learners in flight for 16-learner arenas of >= 16384 rows (cfg3's per-GPU
+  // shard, cfg4: +0.6-1.4% over r3 in the same-process A/B), round 3's kernel otherwise (cfg5's 8,
+  // the cts-sharded 128 learners, and small grids, where it leads by 1-4%)
+  const bool auto_v4 = !kenv && !env && !wenv && C == 16 && nrows >= 16384;
+  const bool v4 = po || stk || split || auto_v4 || (kenv && kenv[0] == 'v' && kenv[1] == '4');
   const int wvs = (wv == 2 || wv == 8) && u == 2 && !po && !stk ? wv : kPackedWaves;
   if (!v4) {
     const uint64_t blocks = (nrows + wvs - 1) / wvs;
