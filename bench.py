@@ -431,7 +431,7 @@ def main():
 
         # the launch's input bytes: the packed arena or C uint64 batches (the separate
         # layout, or an arena small enough for Arena's uint64 layout)
-        in_bytes = arena.buf.numel() * 8 if args.layout == "arena" else C_loc * K_loc * 2 * L * N * 8
+        in_bytes = arena.data_bytes if args.layout == "arena" else C_loc * K_loc * 2 * L * N * 8
         return {"shard": shard, "k_lo": k_lo, "k_hi": k_hi, "K_loc": K_loc, "C_loc": C_loc, "out": out,
                 "in_bytes": in_bytes,
                 "enc_times": enc_times, "kernel": kernel, "kernel_into": kernel_into, "step": step, "piece": piece, "comb": comb, "weights": weights,

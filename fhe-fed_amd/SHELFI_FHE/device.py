@@ -96,8 +96,13 @@ class Arena:
     # wavg_kernel's 4x as many shorter waves over uint64 batches run it 9% faster (bench.py cfg2:
     # 24.2 vs 26.5 us per step, profiles/r04b); from cfg5's 79,872 rows on, the packed bytes win.
     AUTO_U64_ROWS = 4096
+    # uint64 layout: words of padding after each learner's slot.  A slot of K ciphertexts at
+    # 2^15 / L4 is K * 2^21 bytes, so without it the C loads of a thread sit a power of two apart
+    # and land on the same HBM channel
+    SLOT_PAD_WORDS = 512
 
-    def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "auto"):
+    def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "auto",
+                 slot_pad: int | None = None):
         torch = _torch()
         self.ckks, self.C, self.K = ckks, int(num_learners), int(K)
         inf = ckks.info()
@@ -116,12 +121,27 @@ class Arena:
         if layout == "uint64":
             # C learner batches [K][2][L][N] one after the other, aggregated by wavg_kernel
             self.ct_words = 2 * self.L * self.N
-            self.buf = torch.empty((self.C, self.K, 2, self.L, self.N), dtype=torch.int64, device=device)
+            pad = self.SLOT_PAD_WORDS if slot_pad is None else int(slot_pad)
+            self._slot_stride = self.K * self.ct_words + pad  # words
+            self.buf = torch.empty(self.C * self._slot_stride, dtype=torch.int64, device=device)
+            self.data_bytes = self.C * self.K * self.ct_words * 8
             self._refused = set()
+            # per first ciphertext k0: the C slots' pointers, built once.  A cfg2 launch takes
+            # ~25 us; sixteen tensor slices and checks per call took longer than that on the host
+            # and left the GPU waiting (bench.py cfg2: 43 us per step, profiles/r04d)
+            self._slot_ptrs = {}
             return
         self.ct_words = lib.shelfi_arena_words(ckks._ctx, self.C, 1)  # packed words per ciphertext
         words = lib.shelfi_arena_words(ckks._ctx, self.C, self.K)
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
+        self.data_bytes = words * 8
+
+    def slot(self, learner: int):
+        """uint64 layout: learner `learner`'s [K][2][L][N] batch in the arena (a view)."""
+        if self.layout != "uint64":
+            raise ValueError("learner slots are the uint64 layout's; the packed layout interleaves learners")
+        o = int(learner) * self._slot_stride
+        return self.buf[o:o + self.K * self.ct_words].view(self.K, 2, self.L, self.N)
 
     def release(self):
         """Drop this arena's refusal marks in the context and free its memory."""
@@ -182,14 +202,15 @@ class Arena:
         if isinstance(ct, (bytes, bytearray, memoryview)):
             tmp = Arena(self.ckks, 1, self.K, device=self.buf.device, layout="packed")
             tmp.put(0, ct)
-            sum_packed(self.ckks, tmp.buf, 1, self.K, tmp.ct_words * self.K, out=self.buf[learner])
+            sum_packed(self.ckks, tmp.buf, 1, self.K, tmp.ct_words * self.K, out=self.slot(learner))
             tmp.release()
         else:
             _check_ct(ct, self.ckks, self.K)
             if ct.device != self.buf.device:
                 raise ValueError("the batch must live on the arena's device")
-            self.buf[learner].copy_(ct)
-            check(_lib.load().shelfi_dev_check_residues(self.ckks._ctx, C.c_void_p(self.buf[learner].data_ptr()),
+            dst = self.slot(learner)
+            dst.copy_(ct)
+            check(_lib.load().shelfi_dev_check_residues(self.ckks._ctx, C.c_void_p(dst.data_ptr()),
                                                         self.K, C.c_void_p(_stream_ptr(self.buf))),
                   "arena_put: learner %d" % learner)
         self._refused.discard(learner)
@@ -211,7 +232,14 @@ class Arena:
             if self._refused:
                 raise _lib.ShelfiError(_lib.SHELFI_ERR_STATE, "dev_wavg_arena: the arena holds a refused upload "
                                        "for learner %d; put a valid batch first" % min(self._refused))
-            return wavg(self.ckks, [self.buf[c, k0:k1] for c in range(self.C)], weights, out=out)
+            ptrs = self._slot_ptrs.get(k0)
+            if ptrs is None:
+                base, slot = self.buf.data_ptr() + k0 * self.ct_words * 8, self._slot_stride * 8
+                ptrs = self._slot_ptrs[k0] = (C.c_void_p * self.C)(*[base + c * slot for c in range(self.C)])
+            w = (C.c_float * self.C)(*[float(x) for x in weights])
+            check(_lib.load().shelfi_dev_wavg(self.ckks._ctx, ptrs, w, self.C, Kr, C.c_void_p(out.data_ptr()),
+                                              C.c_void_p(_stream_ptr(out))), "dev_wavg_arena")
+            return out
         w = (C.c_float * self.C)(*[float(x) for x in weights])
         # ciphertexts [k0, k1) of an arena are themselves an arena of k1-k0 ciphertexts
         base = self.buf.data_ptr() + k0 * self.ct_words * 8

@@ -46,7 +46,8 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
 // R rows per block (R = 2 for C <= 8 learners): with few learners one 512-residue row gives
 // a thread only C 16-byte loads in flight; two adjacent rows (same tower: N / 512 is even)
 // double that.
-template <bool CHECK = false, int R = 1>
+// UNR learners' loads in flight per thread (8 / R by default; SHELFI_WAVG_UNROLL=16 for an A/B).
+template <bool CHECK = false, int R = 1, int UNR = 8 / R>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
   const uint64_t row0 = (uint64_t)blockIdx.x * R;
@@ -61,7 +62,6 @@ __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[i][j] = 0;
   bool bad = false;
-  constexpr int UNR = 8 / R;
 #pragma unroll UNR
   for (uint32_t k = 0; k < a.C; ++k) {
     const uint64_t* __restrict__ p = a.ptrs[k] + base + 2u * threadIdx.x;
@@ -684,6 +684,11 @@ static int wavg_rows(uint32_t C, uint64_t rows) {
   return C >= 16 && rows >= 16384 ? 2 : 1;
 }
 
+static int wavg_unroll() {
+  const char* env = getenv("SHELFI_WAVG_UNROLL");
+  return env && atoi(env) == 16 ? 16 : 8;
+}
+
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
   const uint64_t total = a.rows << a.logN;
   const uint64_t rows = total / kWavgPerBlock;  // always even: N / 512 >= 2 rows per tower
@@ -699,6 +704,8 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
     hipLaunchKernelGGL((wavg_kernel<true, 1>), g, b, 0, s, a, tc);
   else if (R == 2)
     hipLaunchKernelGGL((wavg_kernel<false, 2>), g, b, 0, s, a, tc);
+  else if (wavg_unroll() == 16)
+    hipLaunchKernelGGL((wavg_kernel<false, 1, 16>), g, b, 0, s, a, tc);
   else
     hipLaunchKernelGGL((wavg_kernel<false, 1>), g, b, 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());
