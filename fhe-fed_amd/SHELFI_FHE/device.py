@@ -93,12 +93,14 @@ class Arena:
     # layout="auto": arenas of at most this many 512-residue rows per learner (K * 2 * L * N / 512)
     # take the uint64 layout.  A packed launch is one wave per row over all C learners; a grid of
     # a few thousand rows (cfg2: 2,048 rows = 2 waves per SIMD) cannot hide its ramp and tail, and
-    # wavg_kernel's 4x as many shorter waves over uint64 batches run it 9% faster (bench.py cfg2:
-    # 24.2 vs 26.5 us per step, profiles/r04b); from cfg5's 79,872 rows on, the packed bytes win.
+    # wavg_kernel's 4x as many shorter waves over uint64 batches run it 7% faster (cfg2: 23.3 vs
+    # 25.0 us per launch, profiles/r04f/wavg_small_ab.txt); at 4,096 rows (16 x 8 cts) the two
+    # are level (46.8 vs 46.7 us), and from cfg5's 79,872 rows on the packed bytes win.
     AUTO_U64_ROWS = 4096
     # uint64 layout: words of padding after each learner's slot.  A slot of K ciphertexts at
-    # 2^15 / L4 is K * 2^21 bytes, so without it the C loads of a thread sit a power of two apart
-    # and land on the same HBM channel
+    # 2^15 / L4 is K * 2^21 bytes: unpadded, a thread's C loads sit a power of two apart and the
+    # launch runs 15% slower (26.9 vs 23.3 us at cfg2; 4 KiB beat 256 B, 32 KiB and 512 KiB,
+    # profiles/r04f/wavg_small_ab.txt)
     SLOT_PAD_WORDS = 512
 
     def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "auto",
