@@ -30,8 +30,8 @@ def main():
     outs, decs = {}, {}
     times = {v: [] for v in vals}
     dtimes = {v: [] for v in vals}
-    for rep in range(3):
-        for v in vals:
+    for rep in range(int(os.environ.get("REPS", "3"))):
+        for v in (vals if rep % 2 == 0 else vals[::-1]):
             os.environ[var] = v
             ck.set_seed(11)
             out = D.encrypt(ck, x)  # warm (allocations)

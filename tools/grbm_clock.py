@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
-"""Effective clock per dispatch of the decrypt chain (MI355X_MICROARCH.md 'DVFS': GRBM_GUI_ACTIVE / 8
-XCDs / wall time), from one rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace run: counter_collection.csv
-joined with kernel_trace.csv on the dispatch id.  Each decrypt call is labelled exact or flooded by its
-FFT pass (fft_fwd_blocks_ct<..., false|true>); prints per call the INTT / CRT / FFT kernels' us and GHz,
-then the medians per label.
-  python tools/grbm_clock.py DIR"""
+"""Effective clock per dispatch of the encrypt and decrypt chains (MI355X_MICROARCH.md 'DVFS':
+GRBM_GUI_ACTIVE / 8 XCDs / wall time), from one rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace run:
+counter_collection.csv joined with kernel_trace.csv on the dispatch id.  A call starts at its first
+kernel (fft_inv_cols: encrypt, ntt_inv_blocks_dec: decrypt); a decrypt is labelled exact or flooded by
+its FFT pass (fft_fwd_blocks_ct<..., false|true>).  Prints per call each kernel's us and GHz, then the
+medians per label (and writes them as JSON with -o).
+  python tools/grbm_clock.py DIR [-o clock.json]"""
 import collections
 import csv
 import glob
 import os
 import statistics
+import json
 import sys
+
+STARTS = ("fft_inv_cols", "ntt_inv_blocks_dec")
 
 
 def main():
     d = sys.argv[1]
+    out = sys.argv[sys.argv.index("-o") + 1] if "-o" in sys.argv else None
     cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     if not cc or not kt:
@@ -34,7 +39,7 @@ def main():
     calls, cur = [], []
     for t, name, us, ghz in rows:
         nm = short(name)
-        if nm.startswith("ntt_inv_blocks_dec") and cur:
+        if nm.startswith(STARTS) and cur:
             calls.append(cur)
             cur = []
         cur.append((nm, us, ghz))
@@ -43,22 +48,33 @@ def main():
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for c in calls:
         names = [n for n, _, _ in c]
-        if not names[0].startswith("ntt_inv_blocks_dec"):
+        if not names[0].startswith(STARTS):
             continue
         # fft_fwd_blocks_ct<BL, K1, K2, K3, K4, FLOOD[, SWZ]>: the sixth template argument
         def flood_arg(n):
             args = n[n.index("<") + 1:n.rindex(">")].split(",")
             return len(args) >= 6 and args[5].strip() == "true"
-        label = "flooded" if any(n.startswith("fft_fwd_blocks_ct") and flood_arg(n) for n in names) else "exact"
+        if names[0].startswith("fft_inv_cols"):
+            label = "encrypt"
+        else:
+            label = "flooded" if any(n.startswith("fft_fwd_blocks_ct") and flood_arg(n) for n in names) else "exact"
         print("%-8s " % label + "  ".join("%s %.1fus %.2fGHz" % (n.split("<")[0], us, g) for n, us, g in c
                                          if not n.startswith("__amd")))
         for n, us, g in c:
             per[label][n.split("<")[0]].append((us, g))
+    res = {}
     for label, ks in per.items():
         print("median %s:" % label)
+        res[label] = {}
         for n, v in ks.items():
-            print("   %-26s %8.1f us  %.2f GHz  (%d calls)" % (n, statistics.median(x for x, _ in v),
-                                                             statistics.median(g for _, g in v), len(v)))
+            us, ghz = statistics.median(x for x, _ in v), statistics.median(g for _, g in v)
+            print("   %-26s %8.1f us  %.2f GHz  (%d calls)" % (n, us, ghz, len(v)))
+            if not n.startswith("__amd"):
+                res[label][n] = {"us": round(us, 1), "ghz": round(ghz, 3), "calls": len(v)}
+    if out:
+        with open(out, "w") as f:
+            json.dump({"what": "median per kernel over the calls of each chain: wall us and effective clock "
+                               "GRBM_GUI_ACTIVE / 8 / wall", "chains": res}, f, indent=1)
 
 
 if __name__ == "__main__":
