@@ -16,20 +16,32 @@ ENCRYPT = ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel"
            "ntt_fwd_blocks_enc")
 _DEC_COMMON = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
                "fft_fwd_cols")
-# the decode FFT's first pass is a template over FLOOD: fft_fwd_blocks<bool> (LDS loops) or
-# fft_fwd_blocks_ct<BL, K1..K4, bool> (register chunks, the default since round 3).  The exact
-# decrypt counts the `false` instantiations, the flooded one the `true` ones plus the sigma pass.
-DECRYPT = _DEC_COMMON + ("fft_fwd_blocks<false>", "fft_fwd_blocks_ct<@false>")
-DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks<true>", "fft_fwd_blocks_ct<@true>", "decode_stats_kernel",
-                                 "decode_flood_kernel")
+# the decode FFT's first pass is a template over FLOOD: fft_fwd_blocks<FLOOD> (LDS loops) or
+# fft_fwd_blocks_ct<BL, K1..K4, FLOOD, SWZ> (register chunks, the default since round 3; SWZ since
+# round 4).  The exact decrypt counts the FLOOD = false instantiations, the flooded one the true ones
+# plus the sigma pass.
+DECRYPT = _DEC_COMMON + ("fft_fwd_blocks@false",)
+DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks@true", "decode_stats_kernel", "decode_flood_kernel")
+
+
+def flood_arg(full):
+    """The FLOOD template argument of a decode-FFT first pass ('true' / 'false'), else None:
+    the first argument of fft_fwd_blocks<...>, the sixth of fft_fwd_blocks_ct<...>."""
+    head = full.split("(")[0].strip()
+    if "<" not in head:
+        return None
+    name, args = head[:head.index("<")], [a.strip() for a in head[head.index("<") + 1:head.rindex(">")].split(",")]
+    if name == "fft_fwd_blocks" and args:
+        return args[0]
+    if name == "fft_fwd_blocks_ct" and len(args) >= 6:
+        return args[5]
+    return None
 
 
 def _matches(full, n):
-    """`prefix@flag`: a template whose name starts with prefix and whose last argument is flag."""
+    """`fft_fwd_blocks@flag`: a decode-FFT first pass whose FLOOD argument is flag; else a prefix."""
     if "@" in n:
-        pre, flag = n.rstrip(">").split("@")
-        head = full.split("(")[0]
-        return head.startswith(pre) and head.rstrip().endswith(", " + flag + ">")
+        return flood_arg(full) == n.split("@")[1]
     return full.startswith(n) or n in full
 
 

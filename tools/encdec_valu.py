@@ -14,12 +14,14 @@ import csv
 import json
 import statistics
 
+from encdec_traffic import _matches  # the decode FFT's FLOOD argument, by position
+
 CHAINS = {
     "encrypt": ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
                 "ntt_fwd_blocks_enc"),
-    "decrypt": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "fft_fwd_blocks<false>", "fft_fwd_cols"),
+    "decrypt": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "fft_fwd_blocks@false", "fft_fwd_cols"),
     "decrypt_flooded": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "decode_stats_kernel",
-                        "fft_fwd_blocks<true>", "fft_fwd_cols"),
+                        "fft_fwd_blocks@true", "fft_fwd_cols"),
 }
 
 
@@ -45,7 +47,7 @@ def main():
     per = {k: statistics.median(v.values()) / a.cts for k, v in vals.items()}
     res = {"cts_per_call": a.cts, "counter": "SQ_INSTS_VALU (wave-level), median per dispatch / cts per call"}
     for name, ks in CHAINS.items():
-        part = {k: round(v) for k, v in per.items() if any(k.startswith(n) for n in ks)}
+        part = {k: round(v) for k, v in per.items() if any(_matches(k, n) for n in ks)}
         res[name] = {"kernels_wave_instr_per_ct": part, "wave_instr_per_ct": sum(part.values())}
         if before and name in before:
             b = before[name]["wave_instr_per_ct"]
