@@ -52,13 +52,15 @@ def _ln(ckks):
 
 
 def _check_ct(t, ckks, K=None, any_level=False):
+    # on the per-launch path of small aggregations (cfg2: 17 tensors per ~23 us launch): each tensor
+    # attribute is a call into torch, so the shape is read once
     L, N = _ln(ckks)
     if not t.is_cuda or not t.is_contiguous() or t.element_size() != 8:
         raise ValueError("ciphertext tensors must be contiguous 64-bit CUDA tensors")
-    towers_ok = (1 <= t.shape[2] <= L) if (any_level and t.dim() == 4) else (t.dim() == 4 and t.shape[2] == L)
-    if t.dim() != 4 or t.shape[1] != 2 or not towers_ok or t.shape[3] != N:
+    sh = t.shape
+    if len(sh) != 4 or sh[1] != 2 or sh[3] != N or not ((1 <= sh[2] <= L) if any_level else sh[2] == L):
         raise ValueError("ciphertext tensor must have shape [K][2][L][N] = [K][2][%d][%d]" % (L, N))
-    if K is not None and t.shape[0] != K:
+    if K is not None and sh[0] != K:
         raise ValueError("ciphertext tensors hold different numbers of ciphertexts")
 
 
