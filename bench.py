@@ -45,6 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "fhe-fed_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_CLOCK_GHZ = 2.4  # MI355X peak engine clock
 VALU_CYCLES_PER_INST = 4.0  # one wave64 VOP3 instruction per SIMD (tools/valu_rates.hip, profiles/r02_valu_rates.txt)
+STEADY_WARM_S = 0.05  # back-to-back warm-up before an encrypt / decrypt time (main(): warm_up)
 COMM_CHECK_TIMEOUT_S = 120  # the C-ABI communicator check at N > 1 (main(): c_abi_comm_check)
 COMM_HANG_EXIT = 3  # exit status when a collective never returned
 # name -> (slots, multDepth, params per learner, learners per GPU, description)
@@ -605,17 +606,31 @@ def main():
     local_wavg()
     torch.cuda.synchronize()
 
+    def warm_up(fn, min_s=STEADY_WARM_S, min_calls=3):
+        """Back-to-back calls until min_s of them have run (and at least min_calls): after a host-side
+        pause (an allocation, a sync) the chip's clock climbs back over ~10 calls of a 714-ct encrypt
+        (~20 ms; profiles/r04n/enc_warm.txt, r04o/), so a steady-state time starts after that."""
+        t0, n = time.perf_counter(), 0
+        while n < min_calls or time.perf_counter() - t0 < min_s:
+            fn()
+            torch.cuda.synchronize()
+            n += 1
+
     def time_decrypts():
         """Exact and flooded decrypts alternated call by call (exact, flooded / flooded, exact, ...):
         the chain is VALU-bound and the chip's clock moves 1.9-2.2 GHz from call to call under it
         (GRBM_GUI_ACTIVE / wall, profiles/r04a/probes/clock_*.txt), so timing one mode's calls as a
-        block and then the other's compared clock states, not decodes.  Median of 7 each."""
+        block and then the other's compared clock states, not decodes.  Median of 7 each, after
+        warm_up()."""
         dec = D.decrypt(ck, out, K_loc * batch, delta * delta)  # warm: sizes the scratch arena
+
+        def both():
+            for flood in (False, True):
+                ck.set_decode_noise(flood)
+                D.decrypt(ck, out, K_loc * batch, delta * delta, out=dec)
+
         res = {False: [], True: []}
-        for flood in (False, True):
-            ck.set_decode_noise(flood)
-            D.decrypt(ck, out, K_loc * batch, delta * delta, out=dec)
-        torch.cuda.synchronize()
+        warm_up(both)
         for r in range(7):
             for flood in ((False, True) if r % 2 == 0 else (True, False)):
                 ck.set_decode_noise(flood)
@@ -629,13 +644,11 @@ def main():
     dec_ms_per_ct, dec_flood_ms_per_ct = time_decrypts()
 
     def time_encrypt():
-        """Back-to-back device encrypts of K_loc ciphertexts (steady state); the build's
-        per-learner encrypts each follow host-side input generation."""
+        """Back-to-back device encrypts of K_loc ciphertexts (steady state: median of 5 after
+        warm_up()); the build's per-learner encrypts each follow host-side input generation."""
         xs = torch.rand(K_loc * batch, device=dev, dtype=torch.float64) * 2 - 1
         ce = D.empty_ct(ck, K_loc, dev)
-        for _ in range(2):
-            D.encrypt(ck, xs, out=ce)
-        torch.cuda.synchronize()
+        warm_up(lambda: D.encrypt(ck, xs, out=ce))
         ts = []
         for _ in range(5):
             t0 = time.perf_counter()

@@ -19,6 +19,10 @@ from SHELFI_FHE import device as D  # noqa: E402
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     K = 714
+    # PREALLOC_GB: HBM taken before the context's scratch is allocated (bench.py's process holds a
+    # ~22 GiB arena by the time it times encrypt), to see whether the scratch's placement matters
+    pre = float(os.environ.get("PREALLOC_GB", "0"))
+    hold = torch.empty(int(pre * (1 << 30)) // 8, dtype=torch.int64, device="cuda") if pre > 0 else None
     ck = m.CKKS("ckks", 16384, 52, "", multDepth=3, seed=7, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
@@ -45,7 +49,9 @@ def main():
             ts.append(a.elapsed_time(b) * 1e3 / K)
         print("%-22s " % tag + " ".join("%.2f" % t for t in ts), flush=True)
 
-    for rep in range(2):
+    print("prealloc %.1f GB" % pre, flush=True)
+    del hold
+    for rep in range(int(os.environ.get("REPS", "2"))):
         for _ in range(200):  # bench.py's timed aggregation loop
             ar.wavg(w, out=out)
         torch.cuda.synchronize()
