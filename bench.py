@@ -677,6 +677,7 @@ def main():
         torch.cuda.synchronize()
 
         def med(fn):
+            warm_up(fn)
             ts = []
             for _ in range(5):
                 t0 = time.perf_counter()
