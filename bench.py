@@ -116,6 +116,8 @@ def parse():
     ap.add_argument("--encdec-traffic-json", default=os.path.join(ROOT, "profiles", "encdec_traffic.json"),
                     help="PMC-derived HBM bytes per ciphertext of the encrypt / decrypt chains "
                          "(tools/encdec_traffic.py over tools/encdec_prof.py, cfg3 parameters)")
+    ap.add_argument("--encdec-clock-json", default=os.path.join(ROOT, "profiles", "encdec_clock.json"),
+                    help="effective clock per encrypt / decrypt kernel in the steady loop (tools/grbm_clock.py -o)")
     ap.add_argument("--encdec-valu-json", default=os.path.join(ROOT, "profiles", "encdec_valu.json"),
                     help="SQ_INSTS_VALU wave-instructions per ciphertext of the encrypt / decrypt chains "
                          "(tools/encdec_valu.py over tools/encdec_prof.py, cfg3 parameters)")
@@ -903,6 +905,25 @@ def main():
                 if "before_r02" in ev[name]:  # the round-2 code's count (profiles/encdec_valu_r02.json)
                     res[name + "_valu"]["wave_instr_per_ct_r02"] = ev[name]["before_r02"]
     except (OSError, ValueError, KeyError):
+        pass
+    # effective clock of each chain's kernels in the steady loop (GRBM_GUI_ACTIVE / 8 / wall, the
+    # chip holds ~2.1 GHz under these VALU-bound passes): the VALU fraction at that clock beside the
+    # one at the 2.4 GHz peak
+    try:
+        with open(args.encdec_clock_json) as f:
+            ec = json.load(f)["chains"]
+        if args.workload in ("cfg3", "cfg2", "cfg5"):
+            for name, label in (("encrypt", "encrypt"), ("decrypt", "exact"), ("decrypt_flooded", "flooded")):
+                ks = ec[label]
+                us = sum(v["us"] for v in ks.values())
+                ghz = sum(v["us"] * v["ghz"] for v in ks.values()) / us  # time-weighted
+                clk = {"kernels_ghz": {k: v["ghz"] for k, v in ks.items()}, "time_weighted_ghz": round(ghz, 3),
+                       "source": os.path.relpath(args.encdec_clock_json, ROOT)}
+                if name + "_valu" in res:
+                    v = res[name + "_valu"]
+                    clk["valu_frac_at_this_clock"] = round(v["frac"] * VALU_CLOCK_GHZ / ghz, 3)
+                res[name + "_clock"] = clk
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
         pass
     if check:
         res["check"] = check
