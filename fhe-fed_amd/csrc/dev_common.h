@@ -543,6 +543,16 @@ __device__ __forceinline__ void ntt_inv_block_stages(uint64_t* sm, uint32_t blkL
   }
 }
 
+// Orders one wave's LDS writes before its own later LDS reads (no other wave involved): the DS
+// instructions of a wave execute in order, so a wavefront-scope fence (the compiler's ordering and
+// the lgkm wait) stands in for a workgroup barrier when every element a wave reads next was written
+// by that same wave.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Padded LDS blocks of the compile-time passes: 4 spare u64 after every 32, so that the
 // set patterns of the chunk plans (element distance 1, 4 or 8 inside a run of 32, or a
 // multiple of 32) fall on distinct banks for ds_read_b64 / ds_write_b64 (unpadded, the

@@ -317,7 +317,13 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
 // Same arithmetic and outputs as ntt_fwd_blocks_enc_ct.
 // NR: the launch covers towers [t0, t0 + nt) whose columns pass ran unreduced (q < kNoRedQ,
 // enc_cols_fused's t_split): no reductions in the block stages either (fwd_set_ct).
-template <int BL, int K1, int K2, int K3, int K4, bool NR>
+// WL (round 4): only the first chunk's exchange crosses waves.  After the stages of half-size
+// 2^(BL-1) .. 2^(BL-K1) the block falls apart into 2^K1 independent sub-blocks; the middle chunks'
+// sets already keep each wave inside 512 contiguous elements, and the last chunk's sets are dealt
+// so that they do too (set g = 2 * 64 w + 64 r + lane), so the exchanges between the middle chunks
+// and into the last one need only the wave's own LDS ordering (wave_lds_sync), not a workgroup
+// barrier: 2 barriers per polynomial instead of 4.
+template <int BL, int K1, int K2, int K3, int K4, bool NR, bool WL = false>
 __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
     const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
     const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk, const uint64_t* __restrict__ pksh,
@@ -325,8 +331,14 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
   constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
+  // WL needs every middle-chunk set of a wave inside its 64 * 2^(BL-8) contiguous elements
+  static_assert(!WL || (BL == 11 && K1 == 3 && K2 == 3 && K3 == 3 && K4 == 2), "wave-local plan");
   __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  // the last chunk's set r of this thread
+  const auto last_g = [&](int r) -> uint32_t {
+    return WL ? ((threadIdx.x >> 6) * (64u * NSL) + 64u * r + (threadIdx.x & 63u)) : threadIdx.x + 256u * r;
+  };
   const uint32_t sstart = logN - BL;
   const uint32_t ncombo = nt << sstart;
   const uint32_t combo = blockIdx.x % ncombo;
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
   const auto fetch_key = [&](int poly) {  // poly 1: b, poly 2: a
 #pragma unroll
     for (int r = 0; r < NSL; ++r) {
-      const uint64_t e = (poly == 1 ? 0 : LN) + off + ((threadIdx.x + 256u * r) << K4);
+      const uint64_t e = (poly == 1 ? 0 : LN) + off + (last_g(r) << K4);
 #pragma unroll
       for (int m = 0; m < ML; m += 2) {
         P[r][m / 2] = *reinterpret_cast<const ulonglong2*>(pk + e + m);
@@ -364,6 +376,12 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
   if (k < K) fetch(k, 0);
   __syncthreads();  // the twiddle slice is in LDS
   const auto lds_ld = [&](uint32_t, uint32_t pj) { return sm[pj]; };
+  const auto mid_sync = [] {
+    if (WL)
+      wave_lds_sync();
+    else
+      __syncthreads();
+  };
 #pragma unroll 1
   for (; k < K; k += per_combo) {
 #pragma unroll 1
@@ -380,8 +398,14 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
         fetch(k + per_combo, 0);
       if (poly > 0) fetch_key(poly);
 #pragma unroll
-      for (int r = 0; r < NS1; ++r) {  // first chunk: one group, block-uniform twiddles
+      for (int r = 0; r < NS1; ++r)  // first chunk: one group, block-uniform twiddles
         fwd_set_ct<BL, BL - 1, K1, NR>(x[r], 0u, tws, q, n8q);
+      // WL: the previous polynomial's last-chunk reads must be done before LDS is refilled; with the
+      // first chunk computed in registers first, a wave that reaches this barrier early has already
+      // done that work (without WL the barrier sits at the end of the previous polynomial)
+      if (WL) __syncthreads();
+#pragma unroll
+      for (int r = 0; r < NS1; ++r) {
         const uint32_t p0 = lpad(threadIdx.x + 256u * r);
 #pragma unroll
         for (int m = 0; m < M1; ++m) sm[p0 + lofs<(1 << D1)>(m)] = x[r][m];
@@ -391,15 +415,15 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
 #pragma unroll
         for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2))>(m)] = y[m];
       });
-      __syncthreads();
+      mid_sync();
       fwd_chunk_ct<BL, BL - 1 - K1 - K2, K3, NR>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
 #pragma unroll
         for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (BL - K1 - K2 - K3))>(m)] = y[m];
       });
-      __syncthreads();
+      mid_sync();
 #pragma unroll
       for (int r = 0; r < NSL; ++r) {
-        const uint32_t g = threadIdx.x + 256u * r, j0 = g << K4, pj0 = lpad(j0);
+        const uint32_t g = last_g(r), j0 = g << K4, pj0 = lpad(j0);
         uint64_t y[ML];
 #pragma unroll
         for (int m = 0; m < ML; ++m) y[m] = sm[pj0 + m];
@@ -418,7 +442,7 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
           }
         }
       }
-      __syncthreads();  // LDS is refilled by the next polynomial
+      if (!WL) __syncthreads();  // LDS is refilled by the next polynomial
     }
   }
 }
@@ -498,7 +522,10 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_ct(uint64_t* __restric
 //  * ciphertext k + P's c0 / c1 words are loaded into registers right after ciphertext k's
 //    have been consumed, so their HBM latency hides behind k's stages.
 // Same arithmetic, same lazy bounds and same dbuf contents as ntt_inv_blocks_dec_ct.
-template <int BL, int K1, int K2, int K3, int K4, bool SUM = false>
+// WL: as ntt_fwd_blocks_enc_pp's, mirrored: the first three chunks (half-sizes 1 .. 2^(BL-K4-1))
+// stay inside 512-element sub-blocks, each wave's own once the first chunk's sets are dealt as
+// g = 2 * 64 w + 64 r + lane; only the exchange into the last chunk crosses waves.
+template <int BL, int K1, int K2, int K3, int K4, bool SUM = false, bool WL = false>
 __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restrict__ dbuf, uint32_t L,
                                                              uint32_t logN,
                                                              const ulonglong2* __restrict__ twb,
@@ -509,8 +536,13 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
                                                              uint32_t per_combo, uint32_t ctL) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256;
+  static_assert(!WL || (BL == 11 && K1 == 2 && K2 == 3 && K3 == 3 && K4 == 3), "wave-local plan");
   __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  // the first chunk's set r of this thread (its elements g 2^K1 + m)
+  const auto first_g = [&](int r) -> uint32_t {
+    return WL ? ((threadIdx.x >> 6) * (64u * NS1) + 64u * r + (threadIdx.x & 63u)) : threadIdx.x + 256u * r;
+  };
   const uint32_t sstart = logN - BL;
   const uint32_t ncombo = L << sstart;
   const uint32_t combo = blockIdx.x % ncombo;
@@ -529,7 +561,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
   for (int r = 0; r < NS1; ++r)
 #pragma unroll
     for (int m = 0; m < M1; ++m) {
-      const uint32_t j = ((threadIdx.x + 256u * r) << K1) + m;
+      const uint32_t j = (first_g(r) << K1) + m;
       sv[r][m] = sk[off + j];
       sw[r][m] = sksh[off + j];
     }
@@ -541,7 +573,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
     for (int r = 0; r < NS1; ++r)
 #pragma unroll
       for (int m = 0; m < M1; ++m) {
-        const uint32_t j = ((threadIdx.x + 256u * r) << K1) + m;
+        const uint32_t j = (first_g(r) << K1) + m;
         p0[r][m] = __builtin_nontemporal_load(c0 + j);
         p1[r][m] = __builtin_nontemporal_load(c0 + CLN + j);
       }
@@ -562,7 +594,7 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
     if (k + per_combo < K) fetch(k + per_combo);  // lands while this ciphertext is transformed
 #pragma unroll
     for (int r = 0; r < NS1; ++r) {  // first chunk: stages i < K1 of the contiguous sets
-      const uint32_t g = threadIdx.x + 256u * r;
+      const uint32_t g = first_g(r);
 #pragma unroll
       for (int i = 0; i < K1; ++i) {
         const int hm = 1 << i;
@@ -579,16 +611,34 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
           }
         }
       }
-      const uint32_t pj0 = lpad(g << K1);
+      if (!WL) {
+        const uint32_t pj0 = lpad(g << K1);
 #pragma unroll
-      for (int m = 0; m < M1; ++m) sm[pj0 + lofs<1>(m)] = x[r][m];
+        for (int m = 0; m < M1; ++m) sm[pj0 + lofs<1>(m)] = x[r][m];
+      }
     }
-    __syncthreads();
+    if (WL) {
+      // the previous ciphertext's last-chunk reads (every wave's) must be done before this wave
+      // refills its sub-block; the first chunk above already ran in registers meanwhile
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < NS1; ++r) {
+        const uint32_t pj0 = lpad(first_g(r) << K1);
+#pragma unroll
+        for (int m = 0; m < M1; ++m) sm[pj0 + lofs<1>(m)] = x[r][m];
+      }
+      wave_lds_sync();
+    } else {
+      __syncthreads();
+    }
     inv_chunk_ct<BL, K1, K2, true>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
 #pragma unroll
       for (int m = 0; m < (1 << K2); ++m) sm[pj0 + lofs<(1 << K1)>(m)] = y[m];
     });
-    __syncthreads();
+    if (WL)
+      wave_lds_sync();
+    else
+      __syncthreads();
     inv_chunk_ct<BL, K1 + K2, K3, true>(tws, q, n8q, lds_ld, [&](int, uint32_t, uint32_t pj0, auto& y) {
 #pragma unroll
       for (int m = 0; m < (1 << K3); ++m) sm[pj0 + lofs<(1 << (K1 + K2))>(m)] = y[m];
@@ -599,8 +649,16 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
 #pragma unroll
       for (int m = 0; m < (1 << K4); ++m) dst[j0 + (m << (BL - K4))] = y[m];
     });
-    __syncthreads();  // sm is rewritten by the next ciphertext's first chunk
+    if (!WL) __syncthreads();  // sm is rewritten by the next ciphertext's first chunk
   }
+}
+
+// Wave-local exchanges in the persistent block passes (the default since round 4; SHELFI_NTT_WL=0,
+// read per launch, keeps the four-barrier form): bit-identical, decrypt 2-3% and flooded decrypt ~2%
+// faster, encrypt within 1% (profiles/r04r/wl_ab*.txt).
+static bool ntt_wave_local() {
+  const char* env = getenv("SHELFI_NTT_WL");
+  return !(env && *env == '0');
 }
 
 // Workgroups of the persistent decrypt / encrypt block passes: LDS-bound residency per CU
@@ -1544,18 +1602,28 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   if (nbb > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "encrypt batch too large"};
   const uint32_t xg = xcd_combos(p.L << nlogR);
   if (pp) {  // one launch per tower class, each spread over all CUs
+    const bool wl = ntt_wave_local();
     if (t_split > 0) {
       const uint32_t ncombo = t_split << nlogR;
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
-      hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
-                         p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
+      if (wl)
+        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false, true>), dim3(ncombo * pc), dim3(256), 0, s,
+                           pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
+      else
+        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
+                           p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
     }
     if (t_split < p.L) {
       const uint32_t ncombo = (p.L - t_split) << nlogR;
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
-      hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
-                         p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
-                         p.L - t_split);
+      if (wl)
+        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true, true>), dim3(ncombo * pc), dim3(256), 0, s,
+                           pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
+                           p.L - t_split);
+      else
+        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
+                           p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
+                           p.L - t_split);
     }
   } else if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
@@ -2151,6 +2219,9 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       if (sum_in)
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, true>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
                            p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+      else if (ntt_wave_local())
+        hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false, true>), dim3(ncombo * pc), dim3(256), 0, s,
+                           dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
                            p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
