@@ -1,0 +1,86 @@
+"""Every A/B switch on the device encrypt / decrypt / aggregation paths selects between two
+implementations of the same arithmetic ("None changes an output bit"): under
+each switch the seeded encryptions, the exact decode and the aggregate are bit-identical to the
+default path's.  The switches are read per launch or per call, so one process flips them.
+
+Encrypt-side switches are checked at both ring shapes the kernels dispatch on (2^15 / L4: NORED
+towers and fused columns; 2^16 / L6: 60-bit towers, the generic columns) with an odd K so the
+persistent passes' uneven tails run; the flooded decode is covered by test_gpu_decode_noise."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import SHELFI_FHE as m  # noqa: E402
+from SHELFI_FHE import device as D  # noqa: E402
+
+ENC_DEC_SWITCHES = [
+    ("SHELFI_NTT_WL", "0"),          # workgroup barrier at every block-pass exchange
+    ("SHELFI_FFT_SWZ", "0"),         # plain LDS index in the FFT block passes
+    ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
+    ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
+    ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
+    ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
+    ("SHELFI_ENC_TAB", "0"),         # butterflies instead of the small-polynomial tables
+    ("SHELFI_ENC_TWL", "0"),         # scalar-loaded column twiddles
+    ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
+    ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
+    ("SHELFI_XCD_ORDER", "0"),       # natural block order
+    ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
+]
+WAVG_SWITCHES = [("SHELFI_WAVG_ROWS", "1"), ("SHELFI_WAVG_ROWS", "2"), ("SHELFI_WAVG_UNROLL", "16")]
+SEED = 2024
+
+
+@pytest.fixture(scope="module", params=[(16384, 3), (32768, 5)], ids=["2^15-L4", "2^16-L6"])
+def ctx(request, tmp_path_factory):
+    batch, depth = request.param
+    d = str(tmp_path_factory.mktemp("keys_sw")) + os.sep
+    ck = m.CKKS("ckks", batch, 52, d, multDepth=depth, seed=5, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    inf = ck.info()
+    K = 7
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.rand(K * inf["batch"] - 3, generator=g, device="cuda", dtype=torch.float64) * 2 - 1
+    ck.set_seed(SEED)
+    ct = D.encrypt(ck, x)
+    dec = D.decrypt(ck, ct, x.numel(), inf["delta"])
+    torch.cuda.synchronize()
+    assert float((dec - x).abs().max()) < 1e-8
+    return ck, x, ct, dec
+
+
+@pytest.mark.parametrize("var,val", ENC_DEC_SWITCHES, ids=lambda v: str(v))
+def test_encrypt_decrypt_switch_bitexact(ctx, monkeypatch, var, val):
+    ck, x, ct_ref, dec_ref = ctx
+    monkeypatch.setenv(var, val)
+    ck.set_seed(SEED)
+    ct = D.encrypt(ck, x)
+    dec = D.decrypt(ck, ct_ref, x.numel(), ck.info()["delta"])
+    torch.cuda.synchronize()
+    assert torch.equal(ct, ct_ref), var
+    assert torch.equal(dec, dec_ref), var
+
+
+@pytest.mark.parametrize("var,val", WAVG_SWITCHES, ids=lambda v: str(v))
+@pytest.mark.parametrize("C", [3, 16])
+def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
+    ck, x, ct_ref, _ = ctx
+    inf = ck.info()
+    q = inf["moduli"]
+    K, L, N = ct_ref.shape[0], inf["num_towers"], inf["ring_dim"]
+    cts = []
+    for i in range(C):
+        a = torch.empty((K, 2, L, N), dtype=torch.int64, device="cuda")
+        for t in range(L):
+            a[:, :, t, :].random_(0, q[t])
+        cts.append(a)
+    w = list(np.random.default_rng(C).dirichlet(np.ones(C)))
+    ref = D.wavg(ck, cts, w)
+    monkeypatch.setenv(var, val)
+    got = D.wavg(ck, cts, w)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), var
