@@ -1266,8 +1266,12 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 // WV: waves per SIMD the register budget is cut for.  TWL: the tower's column-stage twiddles are
 // staged in LDS per tower instead of scalar-loaded (the scalar loads of 15 {w, w'} pairs per polynomial
 // were spilling SGPRs).
-template <int LOGR, bool TAB, int WV = 4, bool TWL = false>
-__global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
+// TS (round 4, small batches): wave w of a workgroup takes tower w (L = 4) of 64 columns, each wave
+// sampling its columns itself (4x the sampler work, no cross-wave traffic): a K = 4 call's 8192
+// columns become 512 waves instead of 128, for calls too small to fill the chip one column per thread
+// (register budget for 2 waves per SIMD: a small call has no more to give it).
+template <int LOGR, bool TAB, int WV = 4, bool TWL = false, bool TS = false>
+__global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
                                                       double delta, const uint64_t* __restrict__ cdt,
                                                       int T, Key8 key, uint64_t g0,
@@ -1278,15 +1282,26 @@ __global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restr
                                                       uint32_t* __restrict__ flag, uint32_t t_split,
                                                       const uint64_t* __restrict__ enc_tab) {
   constexpr int R = 1 << LOGR, IS = 16 / R, G = R / 4;
+  constexpr int NTW = TS ? 4 : 1;  // towers with their own LDS tables in one workgroup
   static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
   __shared__ uint32_t thi[64], tlo[64];
-  __shared__ uint64_t tabs[kEncTab];  // this tower's DeviceTables::enc_tab slice
-  __shared__ ulonglong2 twl[1 << LOGR];  // TWL: this tower's {w, w'} for column stages (index m + i)
+  __shared__ uint64_t tabs_all[NTW][kEncTab];  // the tower's DeviceTables::enc_tab slice
+  __shared__ ulonglong2 twl_all[NTW][1 << LOGR];  // TWL: the tower's {w, w'} for column stages (index m + i)
   static_assert(!TWL || TAB, "LDS twiddles ride on the table path's per-tower barrier");
+  const uint32_t wave = TS ? (threadIdx.x >> 6) : 0u, tid = TS ? (threadIdx.x & 63u) : threadIdx.x;
+  uint64_t* tabs = tabs_all[wave];
+  ulonglong2* twl = twl_all[wave];
+  // TS: each wave's tables are its own, so ordering its LDS writes before its reads needs no barrier
+  const auto tower_sync = [] {
+    if (TS)
+      wave_lds_sync();
+    else
+      __syncthreads();
+  };
   load_cdt32(cdt, T, thi, tlo);
   __syncthreads();
   const uint32_t N = 1u << logN, BLK = N >> LOGR, N16 = N >> 4, V0 = N >> 6;
-  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t gid = TS ? (uint64_t)blockIdx.x * 64 + tid : (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = gid >> (logN - LOGR);
   if (k >= K) return;
   const uint32_t c = (uint32_t)(gid & (BLK - 1));
@@ -1378,6 +1393,7 @@ __global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restr
     const auto small_polys = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
       for (uint32_t t = ta; t < tb; ++t) {
+        if (TS && t != wave) continue;  // wave-uniform
         const TowerConst cst = tcs[t];
         if constexpr (!TAB) {  // A/B reference: every stage as butterflies (SHELFI_ENC_TAB=0)
 #pragma unroll 1
@@ -1390,13 +1406,13 @@ __global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restr
           }
           continue;
         }
-        __syncthreads();  // the previous tower's lookups are done (every thread runs every tower)
-        for (uint32_t i = threadIdx.x; i < (uint32_t)kEncTab; i += 256) tabs[i] = enc_tab[(size_t)t * kEncTab + i];
+        tower_sync();  // the previous tower's lookups are done (every thread runs every tower)
+        for (uint32_t i = tid; i < (uint32_t)kEncTab; i += (TS ? 64u : 256u)) tabs[i] = enc_tab[(size_t)t * kEncTab + i];
         if constexpr (TWL) {
-          if (threadIdx.x < (uint32_t)R)
-            twl[threadIdx.x] = make_ulonglong2(tw[((uint64_t)t << logN) + threadIdx.x], twp[((uint64_t)t << logN) + threadIdx.x]);
+          if (tid < (uint32_t)R)
+            twl[tid] = make_ulonglong2(tw[((uint64_t)t << logN) + tid], twp[((uint64_t)t << logN) + tid]);
         }
-        __syncthreads();
+        tower_sync();
         {
           uint64_t x[R];
 #pragma unroll
@@ -1455,11 +1471,12 @@ __global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restr
   const auto message_poly = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
     for (uint32_t t = ta; t < tb; ++t) {
+      if (TS && t != wave) continue;  // wave-uniform
       if constexpr (TWL) {
-        __syncthreads();  // every thread runs every tower
-        if (threadIdx.x < (uint32_t)R)
-          twl[threadIdx.x] = make_ulonglong2(tw[((uint64_t)t << logN) + threadIdx.x], twp[((uint64_t)t << logN) + threadIdx.x]);
-        __syncthreads();
+        tower_sync();  // every thread runs every tower
+        if (tid < (uint32_t)R)
+          twl[tid] = make_ulonglong2(tw[((uint64_t)t << logN) + tid], twp[((uint64_t)t << logN) + tid]);
+        tower_sync();
       }
       const TowerConst cst = tcs[t];
       uint64_t x[R];
@@ -1482,6 +1499,10 @@ __global__ __launch_bounds__(256, WV) void enc_cols_fused(const double2* __restr
   message_poly(0, t_split, std::false_type{});
   message_poly(t_split, L, std::true_type{});
 }
+
+// enc_cols_fused's tower-split form up to this many ciphertexts per call: K = 4 21.1 vs 24.6 us/ct,
+// K = 16 6.7 vs 7.3, but K = 64 4.1 vs 3.3 and K = 714 3.5 vs 2.6 (profiles/r04u/ts_k*.txt)
+constexpr uint64_t kEncTsMaxK = 24;
 
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
   // FFT buffer | pbuf [K][3][L][N] | me0 [K][N] int64 | ve [K][N] int16
@@ -1556,7 +1577,16 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   hipLaunchKernelGGL((enc_cols_fused<LR, TB, ##__VA_ARGS__>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L, \
                      p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split,  \
                      dt.enc_tab)
-    if (nlogR == 3 && tab)
+    // small calls (K <= kEncTsMaxK at 4 towers): one wave per tower (TS), so a call of a few
+    // ciphertexts spreads over 4x the waves; SHELFI_ENC_TS=0 / 1 forces either (A/B switch)
+    const char* tsenv = getenv("SHELFI_ENC_TS");
+    const bool ts = nlogR == 4 && tab && twl && p.L == 4 &&
+                    (tsenv ? *tsenv == '1' : K <= kEncTsMaxK);
+    if (ts)
+      hipLaunchKernelGGL((enc_cols_fused<4, true, 3, true, true>), dim3((uint32_t)(nb * 4)), dim3(256), 0, s, fbuf, K,
+                         p.logN, logS, p.L, p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh,
+                         pbuf, flag, t_split, dt.enc_tab);
+    else if (nlogR == 3 && tab)
       ENC_COLS(3, true);
     else if (nlogR == 3)
       ENC_COLS(3, false);

@@ -30,6 +30,7 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
     ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
+    ("SHELFI_ENC_TS", "0"),          # one column per thread over every tower (K = 7 defaults to one wave per tower)
 ]
 WAVG_SWITCHES = [("SHELFI_WAVG_ROWS", "1"), ("SHELFI_WAVG_ROWS", "2"), ("SHELFI_WAVG_UNROLL", "16")]
 SEED = 2024
