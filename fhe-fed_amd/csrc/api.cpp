@@ -1151,9 +1151,13 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
                                 const size_t* lens) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
-  // chunk: ~64 MiB of input per learner-group buffer, at least 1 ciphertext
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
-  uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / (ct_bytes * group));
+  // chunk: ~128 MiB of input per learner-group buffer (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 /
+  // 48.2 / 48.7 ms for 16 learners x 64 cts, uint64 blobs; packed wire 54.6 / 46.0 / 42.1 / 42.5 ms,
+  // profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch, read per call)
+  const char* ck_env = getenv("SHELFI_WAVG_CHUNK_MIB");
+  const uint64_t chunk_mib = ck_env && atoll(ck_env) > 0 ? (uint64_t)atoll(ck_env) : 128;
+  uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
   // packed wire (version-2 blobs): uploads land packed and are unpacked on the device; a packed

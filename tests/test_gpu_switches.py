@@ -85,3 +85,22 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
     got = D.wavg(ck, cts, w)
     torch.cuda.synchronize()
     assert torch.equal(got, ref), var
+
+
+@pytest.mark.parametrize("wire", ["shelfi", "packed"])
+def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire):
+    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default chunk (128 MiB of
+    input per learner group: one chunk here) and forced to one ciphertext per chunk (9 chunks through
+    the two device buffer sets): the same aggregate, byte for byte."""
+    ck, x, _, _ = ctx
+    xs = x.cpu().numpy()
+    ck.set_wire_format(wire)
+    try:
+        blobs = [ck.encrypt(xs * (i + 1) / 4) for i in range(3)]
+        w = [0.5, 0.25, 0.25]
+        ref = ck.computeWeightedAverage(blobs, w)
+        monkeypatch.setenv("SHELFI_WAVG_CHUNK_MIB", "1")
+        got = ck.computeWeightedAverage(blobs, w)
+    finally:
+        ck.set_wire_format("shelfi")
+    assert got == ref
