@@ -102,6 +102,14 @@ def parse():
                     help="N>1: skip measuring the other partitioning in the same run")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the end-to-end check (decrypt of owned aggregate cts vs plain FedAvg)")
+    ap.add_argument("--comm-check", action="store_true",
+                    help="N>1: after the measurements, cross-check the library's own C-ABI RCCL communicator "
+                         "against the torch combine on the same partial sums (a second communicator per rank; "
+                         "opt-in, watchdog-guarded)")
+    ap.add_argument("--spawn", action="store_true",
+                    help="start the ranks through torch.distributed.run even at --gpus 1 (the launcher path)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher test: every rank reports its rendezvous and exits before any GPU call")
     ap.add_argument("--api-cts", type=int, default=64,
                     help="ciphertexts per learner for the bytes-API (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
@@ -276,8 +284,50 @@ def cpu_baseline(N, L, q, psi, delta, slots, C, seconds):
             "host": {"cpu_model": _cpu_model(), "usable_cores": cores}}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, nproc: int, port: int):
+    """The one-process-per-GPU launch of this script (what tools/scale_recipe.sh runs):
+    torch.distributed.run on one node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(nproc: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start the N ranks as children
+    through torch.distributed.run and return its exit status (non-zero when any rank failed).
+    This parent never touches the GPU and never re-execs: the children inherit stdout, where
+    rank 0 writes the one JSON line."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL across processes)
+    # torch.distributed.run would pin every rank to 1 OpenMP thread; keep the launcher's share
+    env.setdefault("OMP_NUM_THREADS", str(len(os.sched_getaffinity(0))))
+    return subprocess.run(launch_command(argv, nproc, _free_port()), env=env).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.dry_run:
+        # the launcher test: no torch, no GPU; rank 0 writes the line
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "world": world, "rank": rank, "local_rank": local,
+                              "master_addr": os.environ.get("MASTER_ADDR"), "gpus": args.gpus}))
+        return
     # exactly one line on stdout: libraries (RCCL prints a version banner) write to fd 1,
     # so fd 1 becomes stderr for the run and the JSON line goes to the saved stdout
     sys.stdout.flush()
@@ -287,12 +337,6 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     distributed = world > 1 or args.force_dist
     if distributed:
@@ -952,12 +996,13 @@ def main():
 
         def watchdog():
             if not finished.wait(COMM_CHECK_TIMEOUT_S):
-                res["c_abi_comm_check"] = {"ok": False, "error": "no result within %d s; exited with status %d"
-                                           % (COMM_CHECK_TIMEOUT_S, COMM_HANG_EXIT)}
+                res["c_abi_comm_check" if args.comm_check else "final_barrier"] = {
+                    "ok": False, "error": "no result within %d s; exited with status %d"
+                    % (COMM_CHECK_TIMEOUT_S, COMM_HANG_EXIT)}
                 emit()
                 os._exit(COMM_HANG_EXIT)  # the line is written, but a hung collective fails the run
         threading.Thread(target=watchdog, daemon=True).start()
-        if main_mode["shard"] == "learners":
+        if main_mode["shard"] == "learners" and args.comm_check:
             res["c_abi_comm_check"] = c_abi_comm_check()
     emit()
     if distributed:

@@ -50,7 +50,7 @@ def test_bench_distributed_path_one_rank():
     communicator cross-checked on the same partial sums."""
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
-              "--force-dist", "--pieces", "3"] + COMMON)
+              "--force-dist", "--pieces", "3", "--comm-check"] + COMMON)
     assert "reduce_scatter" in r["config"]["workload"] and "RCCL" in r["config"]["parallelism"]
     assert r["c_abi_comm_check"]["ok"], r["c_abi_comm_check"]
     assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
@@ -80,7 +80,17 @@ def test_bench_learner_sharded_c_abi_combine_one_rank():
         r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "1",
                   "--force-dist", "--shard", "learners", "--combine", "shelfi", "--pieces", "3",
-                  "--no-alt"] + extra + COMMON)
+                  "--no-alt", "--comm-check"] + extra + COMMON)
         assert r["check"]["max_abs_err"] < 1e-8 and r["check"]["cts_checked_per_rank"] == 4
         assert r["c_abi_comm_check"]["ok"], r["c_abi_comm_check"]
         assert "shelfi_dev_combine_arena" in r["config"]["workload"]
+
+
+def test_bench_spawns_its_own_ranks():
+    """Bare `bench.py --gpus N` (no launcher, WORLD_SIZE unset) starts its ranks itself through
+    torch.distributed.run before any GPU call; --spawn takes that path at N = 1 on this box.
+    The child's line (one rank: the local step) is relayed unchanged on stdout."""
+    r = _run([sys.executable, "bench.py", "--gpus", "1", "--spawn", "--no-alt"] + COMMON)
+    assert r["n_gpus"] == 1 and r["value"] > 0
+    assert "c_abi_comm_check" not in r
+    assert r["check"]["max_abs_err"] < 1e-8

@@ -1,10 +1,12 @@
 #!/bin/bash
-# Multi-GPU launch recipe for bench.py on ONE node (the driver's SCALE protocol):
-# torch.distributed.run starts one child process per GPU (no exec after GPU init).
+# Multi-GPU launch recipe for bench.py on ONE node (the driver's SCALE protocol).
+# Equivalent to a bare `python bench.py --gpus N ...`, which spawns the same
+# torch.distributed.run itself (bench.py spawn_ranks: one child process per GPU, the parent
+# never touches the GPU).
 #   tools/scale_recipe.sh 8                      # headline: learner-sharded + pipelined RCCL reduce_scatter
 #   tools/scale_recipe.sh 8 --combine shelfi     # the same pipelined combine inside libshelfi (C ABI)
 #   tools/scale_recipe.sh 8 --shard cts          # ciphertext-sharded, no collective
-# The default run also cross-checks the C-ABI communicator (c_abi_comm_check in the JSON).
+#   tools/scale_recipe.sh 8 --comm-check         # + cross-check of the C-ABI communicator (opt-in)
 set -euo pipefail
 N=${1:-8}
 shift || true
