@@ -757,75 +757,57 @@ def main():
         del xf, yf, fa, fb, fp, fr, got
         torch.cuda.empty_cache()
 
-    # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`
+    # bytes -> bytes API (what code/benchmark.py calls): PCIe-inclusive, never `value`.  The
+    # headline sample is in the default wire format of an unmodified CKKS(...) after keygen: the
+    # reference's own PALISADE cereal archives (ckks.cpp:98-103); the library's uint64 blob and
+    # packed blob ride along
     api = None
     if args.api_cts > 0 and rank == 0:
         Ka = min(K_loc, args.api_cts)
-        if args.layout == "arena":
-            src = [out[:Ka].clone() for _ in range(Cl)]  # any valid ciphertexts of this key
-        else:
-            src = [c[:Ka] for c in cts]
-        blobs = [m.blob_pack(ck, s.cpu().numpy().view(np.uint64)) for s in src]
-        del src
-        ck.computeWeightedAverage(blobs, weights)  # warm (allocates staging)
-        t0 = time.perf_counter()
         reps = 3
-        for _ in range(reps):
-            res_blob = ck.computeWeightedAverage(blobs, weights)
-        dt_api = (time.perf_counter() - t0) / reps
-        api = {"value": round(Cl * Ka / dt_api, 1), "unit": "client-ciphertexts/s",
-               "sample": "%d learners x %d cts, bytes in -> bytes out through "
-                         "SHELFI_FHE.CKKS.computeWeightedAverage (H2D + wavg + D2H)" % (Cl, Ka),
-               "ms_per_call": round(dt_api * 1e3, 2),
-               "input_GB_per_s": round(Cl * Ka * 2 * L * N * 8 / dt_api / 1e9, 2)}
-        # the aggregate back through decrypt(bytes) (H2D of the decode's tower prefix + decrypt + D2H)
-        ck.decrypt(res_blob, Ka * batch)  # warm
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ck.decrypt(res_blob, Ka * batch)
-        dt_dec = (time.perf_counter() - t0) / reps
-        api["decrypt"] = {"ms_per_call": round(dt_dec * 1e3, 2), "cts_per_s": round(Ka / dt_dec, 1),
-                          "blob_GB_per_s": round(len(res_blob) / dt_dec / 1e9, 2)}
-        del blobs, res_blob
-        # the same in the reference's own wire format (PALISADE cereal archives, §8 f1):
-        # the learners' uploads encrypted with set_wire_format("palisade")
-        try:
-            ck.set_wire_format("palisade")
-            xa = np.random.default_rng(7).uniform(-1, 1, Ka * batch)
-            pblobs = [ck.encrypt(xa) for _ in range(Cl)]
-            ck.computeWeightedAverage(pblobs, weights)  # warm
+        default_wire = ck.wire_format()
+
+        def api_sample(blobs):
+            ck.computeWeightedAverage(blobs, weights)  # warm (allocates staging)
             t0 = time.perf_counter()
             for _ in range(reps):
-                res_p = ck.computeWeightedAverage(pblobs, weights)
-            dt_p = (time.perf_counter() - t0) / reps
-            api["palisade_wire"] = {"value": round(Cl * Ka / dt_p, 1), "ms_per_call": round(dt_p * 1e3, 2),
-                                    "archive_bytes_per_learner": len(pblobs[0]),
-                                    "aggregate_bytes": len(res_p)}
-            del pblobs, res_p
-        finally:
-            ck.set_wire_format("shelfi")
-        # and in the packed wire format (version-2 blobs at the moduli's widths)
+                res_b = ck.computeWeightedAverage(blobs, weights)
+            dt = (time.perf_counter() - t0) / reps
+            ck.decrypt(res_b, Ka * batch)  # warm
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ck.decrypt(res_b, Ka * batch)
+            dtd = (time.perf_counter() - t0) / reps
+            nb = sum(len(b) for b in blobs)
+            return {"value": round(Cl * Ka / dt, 1), "unit": "client-ciphertexts/s", "ms_per_call": round(dt * 1e3, 2),
+                    "input_GB_per_s": round(nb / dt / 1e9, 2),
+                    "uint64_residue_GB_per_s": round(Cl * Ka * 2 * L * N * 8 / dt / 1e9, 2),
+                    "bytes_per_learner": len(blobs[0]), "aggregate_bytes": len(res_b),
+                    "decrypt": {"ms_per_call": round(dtd * 1e3, 2), "cts_per_s": round(Ka / dtd, 1),
+                                "blob_GB_per_s": round(len(res_b) / dtd / 1e9, 2)}}
+
+        xa = np.random.default_rng(7).uniform(-1, 1, Ka * batch)
+        pblobs = [ck.encrypt(xa) for _ in range(Cl)]
+        api = api_sample(pblobs)
+        api.update(wire_format=default_wire,
+                   sample="%d learners x %d cts, bytes in -> bytes out through SHELFI_FHE.CKKS."
+                          "computeWeightedAverage (H2D + wavg + D2H) in the default wire format (%s)"
+                          % (Cl, Ka, default_wire))
+        del pblobs
+        # the library's uint64 blob (64-byte header + raw [K][2][L][N])
+        src = [out[:Ka].clone() for _ in range(Cl)]  # any valid ciphertexts of this key
+        blobs = [m.blob_pack(ck, s_.cpu().numpy().view(np.uint64)) for s_ in src]
+        del src
+        api["shelfi_wire"] = api_sample(blobs)
+        del blobs
+        # and the packed wire format (version-2 blobs at the moduli's widths)
         try:
             ck.set_wire_format("packed")
-            xa = np.random.default_rng(7).uniform(-1, 1, Ka * batch)
             kblobs = [ck.encrypt(xa) for _ in range(Cl)]
-            ck.computeWeightedAverage(kblobs, weights)  # warm
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                res_k = ck.computeWeightedAverage(kblobs, weights)
-            dt_k = (time.perf_counter() - t0) / reps
-            ck.decrypt(res_k, Ka * batch)  # warm
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ck.decrypt(res_k, Ka * batch)
-            dt_kd = (time.perf_counter() - t0) / reps
-            api["packed_wire"] = {"value": round(Cl * Ka / dt_k, 1), "ms_per_call": round(dt_k * 1e3, 2),
-                                  "blob_bytes_per_learner": len(kblobs[0]), "aggregate_bytes": len(res_k),
-                                  "input_GB_per_s": round(Cl * len(kblobs[0]) / dt_k / 1e9, 2),
-                                  "decrypt_ms_per_call": round(dt_kd * 1e3, 2)}
-            del kblobs, res_k
+            api["packed_wire"] = api_sample(kblobs)
+            del kblobs
         finally:
-            ck.set_wire_format("shelfi")
+            ck.set_wire_format(default_wire)
 
     # roofline of the dominant kernel: algorithmic bytes = the C learners' packed residues
     # (K * 2 * N * sum_t U_t / 8 each, U_t ~ bitlength(q_t)) read once

@@ -10,9 +10,12 @@ Extensions over the reference (keyword-only, defaults reproduce it):
 ``multDepth`` (L = multDepth + 1 towers; reference fixes 1, ckks.cpp:26),
 ``firstModBits`` (60), ``ringDim`` (0 = PALISADE's choice), ``device``
 (HIP ordinal; default LOCAL_RANK or 0), ``seed`` (deterministic encryption
-randomness for parity tests; 0 = OS entropy) and ``decodeNoise`` (PALISADE's decode
+randomness for parity tests; 0 = OS entropy), ``decodeNoise`` (PALISADE's decode
 noise flooding, on by default like the reference's Decrypt; False = the exact,
-deterministic decode the parity tests compare bit for bit).
+deterministic decode the parity tests compare bit for bit) and ``wireFormat``
+(encrypt's bytes: "palisade" = the reference's own cereal archives, the default once keys
+are generated or loaded, as ckks.cpp:98-103 writes them; "shelfi" / "packed" = this
+library's blobs, opt-in).
 """
 from __future__ import annotations
 
@@ -27,6 +30,8 @@ from ._lib import ShelfiError, check
 
 __version__ = "0.1.0"
 __all__ = ["Scheme", "CKKS", "ShelfiError", "__version__"]
+
+_WIRE_CODES = {"shelfi": 0, "palisade": 1, "packed": 2}  # shelfi_set_wire_format's numbering
 
 
 _PyBytes_FromStringAndSize = C.pythonapi.PyBytes_FromStringAndSize
@@ -84,10 +89,13 @@ class CKKS(Scheme):
     def __init__(self, scheme: str = "ckks", batchSize: int = 4096, scaleFactorBits: int = 52,
                  cryptodir: str = "../resources/cryptoparams/", *, multDepth: int = 1,
                  firstModBits: int = 60, ringDim: int = 0, device: int | None = None,
-                 seed: int = 0, decodeNoise: bool = True):
+                 seed: int = 0, decodeNoise: bool = True, wireFormat: str = "palisade"):
         super().__init__(scheme)
         if scheme.lower() != "ckks":
             raise ValueError("only the 'ckks' scheme is implemented")
+        if wireFormat not in _WIRE_CODES:
+            raise ValueError("wireFormat must be 'palisade', 'shelfi' or 'packed'")
+        self._wire = wireFormat
         self.batchSize = int(batchSize)
         self.scaleFactorBits = int(scaleFactorBits)
         self.cryptodir = str(cryptodir)
@@ -133,16 +141,30 @@ class CKKS(Scheme):
 
     def set_wire_format(self, fmt: str = "palisade") -> None:
         """Bytes format of encrypt's output: "palisade" = the reference's own cereal
-        archive of vector<Ciphertext<DCRTPoly>> (ckks.cpp:98-100; needs keys loaded from
-        the reference's PALISADE files), "shelfi" = this library's blob (default),
-        "packed" = this library's blob with the residues at their moduli's bit widths
-        (version 2; 15% fewer bytes at 2^15/L4 over the network and PCIe).
+        archive of vector<Ciphertext<DCRTPoly>> (ckks.cpp:98-100; the default, in effect
+        once keys are generated or loaded in PALISADE's files), "shelfi" = this library's
+        blob, "packed" = this library's blob with the residues at their moduli's bit widths
+        (version 2; 15% fewer bytes at 2^15/L4 over the network and PCIe).  The choice
+        sticks across later loadCryptoParams / genCryptoContextAndKeyGen calls.
         computeWeightedAverage and decrypt accept all three and computeWeightedAverage
         answers in its inputs' format."""
-        codes = {"shelfi": 0, "palisade": 1, "packed": 2}
-        if fmt not in codes:
+        if fmt not in _WIRE_CODES:
             raise ValueError("wire format must be 'palisade', 'shelfi' or 'packed'")
-        check(self._lib.shelfi_set_wire_format(self._ctx, codes[fmt]), "set_wire_format")
+        check(self._lib.shelfi_set_wire_format(self._ctx, _WIRE_CODES[fmt]), "set_wire_format")
+        self._wire = fmt
+
+    def wire_format(self) -> str:
+        """The bytes format encrypt answers in right now."""
+        return {v: k for k, v in _WIRE_CODES.items()}[int(self._lib.shelfi_get_wire_format(self._ctx))]
+
+    def _apply_wire(self) -> None:
+        """After keys are generated or loaded: the chosen format; "palisade" needs the
+        PALISADE context object the keys came with — keys from this library's own SHCC/SHPK
+        files (or set_keys) carry none, and then encrypt answers in the library blob."""
+        rc = self._lib.shelfi_set_wire_format(self._ctx, _WIRE_CODES[self._wire])
+        if rc == _lib.SHELFI_ERR_STATE and self._wire == "palisade":
+            rc = self._lib.shelfi_set_wire_format(self._ctx, _WIRE_CODES["shelfi"])
+        check(rc, "wire format")
 
     def set_decode_noise(self, enabled: bool = True, m_factor: float = 1.0) -> None:
         """PALISADE 1.11's decode noise flooding (CKKSPackedEncoding::Decode): Gaussian
@@ -169,6 +191,8 @@ class CKKS(Scheme):
         if rc != 0:
             print("Could not read serialization from %scryptocontext.txt: %s"
                   % (self.cryptodir, self._lib.shelfi_last_error().decode(errors="replace")))
+            return
+        self._apply_wire()
 
     def genCryptoContextAndKeyGen(self) -> int:
         """ckks.cpp:25-59: returns 1 on success, 0 on a file-write error."""
@@ -179,6 +203,7 @@ class CKKS(Scheme):
                   % self._lib.shelfi_last_error().decode(errors="replace"))
             return 0
         check(rc, "genCryptoContextAndKeyGen")
+        self._apply_wire()
         return 1
 
     def set_keys(self, pk: np.ndarray, sk: np.ndarray) -> None:
@@ -330,7 +355,19 @@ def special_primes(ringDim: int, moduli) -> dict:
             "special_roots": [int(sr[i]) for i in range(k)]}
 
 
+def _is_palisade_archive(b) -> bool:
+    """A cereal PortableBinary archive starts with its endianness byte 0x01; this library's
+    blobs with the magic "SHCT"."""
+    return len(b) > 0 and bytes(b[:4]) != b"SHCT" and bytes(b[:1]) == b"\x01"
+
+
 def blob_info(blob: bytes) -> dict:
+    """Ciphertext count, depth and scale of encrypt / computeWeightedAverage bytes in any wire
+    format: a library blob (+ its key id) or a PALISADE archive (+ its key tag)."""
+    if _is_palisade_archive(blob):
+        d, _ = palisade_parse(blob, residues=False)
+        return {"num_cts": d["num_cts"], "depth": d["depth"], "scale": d["scale"], "key_id": None,
+                "keytag": d["keytag"], "format": "palisade"}
     lib = _lib.load()
     k = C.c_uint64()
     d = C.c_uint32()
@@ -339,7 +376,8 @@ def blob_info(blob: bytes) -> dict:
     check(lib.shelfi_blob_info(C.cast(C.c_char_p(blob), _lib.u8p), len(blob), C.byref(k),
                                C.byref(d), C.byref(s), C.byref(kid)), "blob_info")
     return {"num_cts": int(k.value), "depth": int(d.value), "scale": float(s.value),
-            "key_id": int(kid.value)}
+            "key_id": int(kid.value),
+            "format": "packed" if int.from_bytes(bytes(blob[4:6]), "little") == 2 else "shelfi"}
 
 
 def blob_pack(ckks: "CKKS", residues: np.ndarray, depth: int = 1, scale: float | None = None) -> bytes:
@@ -359,8 +397,15 @@ def blob_pack(ckks: "CKKS", residues: np.ndarray, depth: int = 1, scale: float |
 
 
 def blob_residues(blob: bytes, ring_dim: int, num_towers: int, ckks: "CKKS | None" = None) -> np.ndarray:
-    """A blob's residues as [K][2][L][N] uint64 (host): a view of a version-1 payload, or (with
-    the context that made it, whose moduli fix the widths) a packed version-2 payload unpacked."""
+    """Ciphertext bytes' residues as [K][2][L][N] uint64 (host), in any wire format: a view of a
+    version-1 payload, a PALISADE archive parsed, or (with the context that made it, whose moduli
+    fix the widths) a packed version-2 payload unpacked."""
+    if _is_palisade_archive(blob):
+        d, r = palisade_parse(blob)
+        if (d["ring_dim"], d["num_towers"]) != (int(ring_dim), int(num_towers)):
+            raise ValueError("blob_residues: archive shape (N=%d, L=%d) is not (N=%d, L=%d)"
+                             % (d["ring_dim"], d["num_towers"], ring_dim, num_towers))
+        return r
     lib = _lib.load()
     hdr = lib.shelfi_blob_header_bytes()
     version = int.from_bytes(bytes(blob[4:6]), "little")

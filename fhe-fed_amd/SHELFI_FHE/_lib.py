@@ -11,8 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libshelfi.so")
-# A/B probes only (tools/*_ab*.sh): another build of the library, e.g. the previous commit's
-LIB_PATH = os.environ.get("SHELFI_LIB_AB", LIB_PATH)
+# A/B probes only (tools/*_ab*.sh): SHELFI_LIB_AB names another build of the library, e.g. the
+# previous commit's.  load() warns whenever it is set and lists the entry points that build lacks.
+_AB_PATH = os.environ.get("SHELFI_LIB_AB")
 
 SHELFI_OK = 0
 SHELFI_ERR_ARG = -1
@@ -92,6 +93,7 @@ SIGNATURES = {
     "shelfi_get_keys": (C.c_int, [C.c_void_p, u64p, u64p]),
     "shelfi_encrypt": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "shelfi_set_wire_format": (C.c_int, [C.c_void_p, C.c_int]),
+    "shelfi_get_wire_format": (C.c_int, [C.c_void_p]),
     "shelfi_palisade_parse": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(PalisadeInfo), u64p]),
     "shelfi_palisade_write": (C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_uint32, C.c_uint32, u64p,
                                         C.c_uint64, u64p, C.c_uint64, C.c_uint64, C.c_double, C.c_int,
@@ -185,18 +187,26 @@ def load():
     """Load libshelfi.so (raises OSError if it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = _AB_PATH or LIB_PATH
+        if not os.path.exists(path):
             raise OSError(
                 "libshelfi.so not found at %s — build it with `make -C fhe-fed_amd/csrc` "
-                "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
-        lib = C.CDLL(LIB_PATH)
-        ab = "SHELFI_LIB_AB" in os.environ  # an older build for an A/B probe may lack newer entries
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback" % path)
+        lib = C.CDLL(path)
+        missing = []
         for name, (res, args) in SIGNATURES.items():
-            if ab and not hasattr(lib, name):
+            if _AB_PATH and not hasattr(lib, name):
+                missing.append(name)  # an older build for an A/B probe may lack newer entries
                 continue
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
+        if _AB_PATH:
+            import warnings
+
+            warnings.warn("SHELFI_LIB_AB: loaded %s instead of the in-tree libshelfi.so (A/B probe build)%s"
+                          % (path, "; entry points it lacks: " + ", ".join(missing) if missing else ""),
+                          RuntimeWarning, stacklevel=2)
         _lib = lib
     return _lib
 

@@ -105,7 +105,7 @@ class Arena:
     # profiles/r04f/wavg_small_ab.txt)
     SLOT_PAD_WORDS = 512
 
-    def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "auto",
+    def __init__(self, ckks, num_learners: int, K: int, device=None, layout: str = "packed",
                  slot_pad: int | None = None):
         torch = _torch()
         self.ckks, self.C, self.K = ckks, int(num_learners), int(K)
@@ -140,12 +140,19 @@ class Arena:
         self.buf = torch.empty(words, dtype=torch.int64, device=device)
         self.data_bytes = words * 8
 
-    def slot(self, learner: int):
-        """uint64 layout: learner `learner`'s [K][2][L][N] batch in the arena (a view)."""
+    def _slot(self, learner: int):
+        """uint64 layout: learner `learner`'s [K][2][L][N] batch in the arena (a writable view; only
+        put() writes through it, so every placed residue is validated)."""
         if self.layout != "uint64":
             raise ValueError("learner slots are the uint64 layout's; the packed layout interleaves learners")
         o = int(learner) * self._slot_stride
         return self.buf[o:o + self.K * self.ct_words].view(self.K, 2, self.L, self.N)
+
+    def slot(self, learner: int):
+        """uint64 layout: a copy of learner `learner`'s placed [K][2][L][N] batch.  A copy, not a
+        view: writes into the arena go through put(), which checks every residue < q_t (the
+        aggregation's carry-free limb sums assume canonical residues)."""
+        return self._slot(learner).clone()
 
     def release(self):
         """Drop this arena's refusal marks in the context and free its memory."""
@@ -206,13 +213,13 @@ class Arena:
         if isinstance(ct, (bytes, bytearray, memoryview)):
             tmp = Arena(self.ckks, 1, self.K, device=self.buf.device, layout="packed")
             tmp.put(0, ct)
-            sum_packed(self.ckks, tmp.buf, 1, self.K, tmp.ct_words * self.K, out=self.slot(learner))
+            sum_packed(self.ckks, tmp.buf, 1, self.K, tmp.ct_words * self.K, out=self._slot(learner))
             tmp.release()
         else:
             _check_ct(ct, self.ckks, self.K)
             if ct.device != self.buf.device:
                 raise ValueError("the batch must live on the arena's device")
-            dst = self.slot(learner)
+            dst = self._slot(learner)
             dst.copy_(ct)
             check(_lib.load().shelfi_dev_check_residues(self.ckks._ctx, C.c_void_p(dst.data_ptr()),
                                                         self.K, C.c_void_p(_stream_ptr(self.buf))),

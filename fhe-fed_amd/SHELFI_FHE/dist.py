@@ -149,25 +149,32 @@ class PipelinedCombine:
     def run(self, compute_piece, fold_share=None):
         """compute_piece(k0, k1, out_view) writes the local partial sums of
         ciphertexts [k0, k1) into out_view[:k1-k0]; fold_share(share_view) reduces a
-        summed share mod q.  Returns [(k0, k1, share_view)] owned by this rank."""
+        summed share mod q.  Returns [(k0, k1, share_view)] owned by this rank (views into this
+        object's buffers, valid until the next run())."""
         import torch.distributed as dist
 
         works = []
-        for (k0, k1), view, share in zip(self.pieces, self.views, self.shares):
-            compute_piece(k0, k1, view[:k1 - k0])
-            works.append(dist.reduce_scatter_tensor(share, view, op=dist.ReduceOp.SUM,
-                                                    group=self.group, async_op=True))
-        owned = []
-        for (k0, k1), p, share, w in zip(self.pieces, self.padded, self.shares, works):
-            w.wait()
-            per = p // self.world
-            a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
-            if b > a:
-                sv = share[:b - a]
-                if fold_share is not None:
-                    fold_share(sv)
-                owned.append((a, b, sv))
-        return owned
+        try:
+            for (k0, k1), view, share in zip(self.pieces, self.views, self.shares):
+                compute_piece(k0, k1, view[:k1 - k0])
+                works.append(dist.reduce_scatter_tensor(share, view, op=dist.ReduceOp.SUM,
+                                                        group=self.group, async_op=True))
+            owned = []
+            for i, ((k0, k1), p, share, w) in enumerate(zip(self.pieces, self.padded, self.shares, works)):
+                w.wait()
+                works[i] = None
+                per = p // self.world
+                a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
+                if b > a:
+                    sv = share[:b - a]
+                    if fold_share is not None:
+                        fold_share(sv)
+                    owned.append((a, b, sv))
+            return owned
+        finally:  # a callback that raised leaves no collective in flight
+            for w in works:
+                if w is not None:
+                    w.wait()
 
 
 class PackedPipelinedCombine:
@@ -211,23 +218,33 @@ class PackedPipelinedCombine:
         """compute_piece_packed(k0, k1, out_words) writes the packed local partial of ciphertexts
         [k0, k1) into out_words[:(k1 - k0) * pw]; sum_share(stacked, world, n, stride, out) sums
         `world` packed batches of n ciphertexts stride words apart into out[:n] (canonical).
-        Returns [(k0, k1, share_view)] owned by this rank."""
+        Returns [(k0, k1, share_view)] owned by this rank.  The share views live in this
+        object's buffers and are valid until the next run(): clone them to keep them.  If a
+        callback raises, every exchange already launched is waited for before the error
+        propagates (no collective is left in flight over buffers the caller may free)."""
         import torch.distributed as dist
 
         works = []
-        for (k0, k1), snd, rcv in zip(self.pieces, self.sends, self.recvs):
-            compute_piece_packed(k0, k1, snd[:(k1 - k0) * self.pw])
-            works.append(dist.all_to_all_single(rcv, snd, group=self.group, async_op=True))
-        owned = []
-        for (k0, k1), p, rcv, share, w in zip(self.pieces, self.padded, self.recvs, self.shares, works):
-            w.wait()
-            per = p // self.world
-            a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
-            if b > a:
-                sv = share[:b - a]
-                sum_share(rcv, self.world, b - a, per * self.pw, sv)
-                owned.append((a, b, sv))
-        return owned
+        try:
+            for (k0, k1), snd, rcv in zip(self.pieces, self.sends, self.recvs):
+                compute_piece_packed(k0, k1, snd[:(k1 - k0) * self.pw])
+                works.append(dist.all_to_all_single(rcv, snd, group=self.group, async_op=True))
+            owned = []
+            for i, ((k0, k1), p, rcv, share, w) in enumerate(zip(self.pieces, self.padded, self.recvs,
+                                                                 self.shares, works)):
+                w.wait()
+                works[i] = None
+                per = p // self.world
+                a, b = k0 + self.rank * per, min(k1, k0 + (self.rank + 1) * per)
+                if b > a:
+                    sv = share[:b - a]
+                    sum_share(rcv, self.world, b - a, per * self.pw, sv)
+                    owned.append((a, b, sv))
+            return owned
+        finally:
+            for w in works:
+                if w is not None:
+                    w.wait()
 
 
 def slice_of_rank(K: int, world: int, rank: int):

@@ -194,13 +194,24 @@ class SecureFedAvg:
 
 
 # ------------------------------------------------------- synthetic models --
-def resnet_shapes(depth: int = 18, num_classes: int = 1000) -> "OrderedDict[str, tuple]":
-    """Parameter/buffer-free state_dict shapes of torchvision's ResNet-18/50 (weights
-    and biases only, as model.parameters() counts them): 11,689,512 / 25,557,032."""
+def resnet_shapes(depth: int = 18, num_classes: int = 1000, buffers: bool = True) -> "OrderedDict[str, tuple]":
+    """torchvision ResNet-18/50 `model.state_dict()` shapes, in state_dict order: what
+    benchmark.py:457 encrypts (tensor_to_numpy_arr(model.state_dict()), :16-21).  Every BatchNorm
+    contributes weight, bias and the buffers running_mean, running_var and num_batches_tracked
+    (a 0-d int64 tensor, flattened to one element); 20 BNs in ResNet-18, 53 in ResNet-50.
+    buffers=False keeps the parameters alone (model.parameters(): 11,689,512 / 25,557,032)."""
     shapes = OrderedDict()
+
+    def bn(prefix, c):
+        shapes[prefix + "weight"] = (c,)
+        shapes[prefix + "bias"] = (c,)
+        if buffers:
+            shapes[prefix + "running_mean"] = (c,)
+            shapes[prefix + "running_var"] = (c,)
+            shapes[prefix + "num_batches_tracked"] = ()
+
     shapes["conv1.weight"] = (64, 3, 7, 7)
-    shapes["bn1.weight"] = (64,)
-    shapes["bn1.bias"] = (64,)
+    bn("bn1.", 64)
     if depth == 18:
         blocks, expansion = [2, 2, 2, 2], 1
     elif depth == 50:
@@ -214,31 +225,31 @@ def resnet_shapes(depth: int = 18, num_classes: int = 1000) -> "OrderedDict[str,
             stride = 2 if (bi == 0 and li > 1) else 1
             if depth == 18:
                 shapes[p + "conv1.weight"] = (planes, inplanes, 3, 3)
-                shapes[p + "bn1.weight"] = (planes,)
-                shapes[p + "bn1.bias"] = (planes,)
+                bn(p + "bn1.", planes)
                 shapes[p + "conv2.weight"] = (planes, planes, 3, 3)
-                shapes[p + "bn2.weight"] = (planes,)
-                shapes[p + "bn2.bias"] = (planes,)
+                bn(p + "bn2.", planes)
                 out = planes
             else:
                 shapes[p + "conv1.weight"] = (planes, inplanes, 1, 1)
-                shapes[p + "bn1.weight"] = (planes,)
-                shapes[p + "bn1.bias"] = (planes,)
+                bn(p + "bn1.", planes)
                 shapes[p + "conv2.weight"] = (planes, planes, 3, 3)
-                shapes[p + "bn2.weight"] = (planes,)
-                shapes[p + "bn2.bias"] = (planes,)
+                bn(p + "bn2.", planes)
                 shapes[p + "conv3.weight"] = (planes * 4, planes, 1, 1)
-                shapes[p + "bn3.weight"] = (planes * 4,)
-                shapes[p + "bn3.bias"] = (planes * 4,)
+                bn(p + "bn3.", planes * 4)
                 out = planes * 4
             if bi == 0 and (stride != 1 or inplanes != out):
                 shapes[p + "downsample.0.weight"] = (out, inplanes, 1, 1)
-                shapes[p + "downsample.1.weight"] = (out,)
-                shapes[p + "downsample.1.bias"] = (out,)
+                bn(p + "downsample.1.", out)
             inplanes = out
     shapes["fc.weight"] = (num_classes, 512 * expansion)
     shapes["fc.bias"] = (num_classes,)
     return shapes
+
+
+def cts_per_key(shapes, batch: int) -> "OrderedDict[str, int]":
+    """Ciphertexts encrypt() makes per state_dict key (benchmark.py:490-493 encrypts each key on
+    its own; ckks.cpp:65-83 chunks n values into ceil(n / batch), a 1-element buffer included)."""
+    return OrderedDict((k, -(-max(1, int(np.prod(shp))) // batch)) for k, shp in shapes.items())
 
 
 def lenet5_shapes() -> "OrderedDict[str, tuple]":
@@ -251,13 +262,21 @@ def lenet5_shapes() -> "OrderedDict[str, tuple]":
 
 
 def synthetic_states(shapes, num_clients: int, seed: int = 0, scale: float = 0.1):
-    """Client state dicts (float32 weights U(-scale, scale)) flattened to float64."""
+    """Client state dicts flattened per key (tensor_to_numpy_arr, benchmark.py:16-21): float32
+    weights U(-scale, scale) widened to float64; BatchNorm running_var U(0, 2 scale) (positive);
+    num_batches_tracked an int64 step count (kept int64: encrypt's forcecast widens it, as the
+    reference's py::array_t<double> does)."""
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(num_clients):
         st = OrderedDict()
         for k, shp in shapes.items():
             n = int(np.prod(shp))
-            st[k] = rng.uniform(-scale, scale, n).astype(np.float32).astype(np.float64)
+            if k.endswith("num_batches_tracked"):
+                st[k] = rng.integers(0, 100_000, n, dtype=np.int64)
+            elif k.endswith("running_var"):
+                st[k] = rng.uniform(0, 2 * scale, n).astype(np.float32).astype(np.float64)
+            else:
+                st[k] = rng.uniform(-scale, scale, n).astype(np.float32).astype(np.float64)
         out.append(st)
     return out

@@ -2030,6 +2030,12 @@ int shelfi_set_wire_format(shelfi_ctx* ctx, int format) {
   });
 }
 
+int shelfi_get_wire_format(const shelfi_ctx* ctx) {
+  if (!ctx) return -1;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  return ctx->wire;
+}
+
 int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
                           uint64_t* residues) {
   if (!archive || !info) return SHELFI_ERR_ARG;

@@ -156,11 +156,14 @@ typedef struct {
   uint64_t ctx_offset, ctx_length; /* the embedded context object inside the archive */
   char keytag[257];
 } shelfi_palisade_info;
-/* 0 blob (default), 1 PALISADE archive, 2 packed blob (version 2: the residues at their moduli's
- * widths, the arena's slice format with C = 1 — 218 of 256 bits per coefficient at 2^15/L4, so a
- * PCIe-bound upload carries 15% fewer bytes).  Every entry that takes ciphertext
- * bytes accepts all three. */
+/* 0 blob (the C ABI's default), 1 PALISADE archive (the Python / C++ front ends' default once keys
+ * are generated or loaded in PALISADE's files, as ckks.cpp:98-103 writes them), 2 packed blob
+ * (version 2: the residues at their moduli's widths, the arena's slice format with C = 1 — 218 of
+ * 256 bits per coefficient at 2^15/L4, so a PCIe-bound upload carries 15% fewer bytes; DESIGN.md
+ * §5.3).  Every entry that takes ciphertext bytes accepts all three. */
 int shelfi_set_wire_format(shelfi_ctx* ctx, int format);
+/* The format encrypt answers in right now (0, 1 or 2; -1 for a NULL context). */
+int shelfi_get_wire_format(const shelfi_ctx* ctx);
 /* Host-only: parse an archive; residues [K][2][L][N] copied out when non-NULL. */
 int shelfi_palisade_parse(const uint8_t* archive, size_t len, shelfi_palisade_info* info,
                           uint64_t* residues);

@@ -58,8 +58,8 @@ uint64_t or_powmod(uint64_t a, uint64_t e, uint64_t q) {
   }
   return r;
 }
-/* signed int64 -> [0,q).  PALISADE FitToNativeVector (ckkspackedencoding.cpp)
- * maps negative v via (2^62-1+v) ModSub (2^62-1-q) == v mod q [PALISADE-1.11]. */
+/* signed int64 -> [0,q) (v mod q).  Encode's own mapping, FitToNativeVector, agrees with it
+ * for |v| < 2^62 - 256 and wraps beyond (or_fit_wrap below) [PALISADE-1.11]. */
 uint64_t or_mod_signed(int64_t v, uint64_t q) {
   if (v >= 0) return (uint64_t)v % q;
   uint64_t m = (uint64_t)(-(v + 1)) + 1; /* |v| without overflow */
@@ -357,12 +357,37 @@ int64_t or_round_half_away(double x) {
 /* encode  (ckks.cpp:80 MakeCKKSPackedPlaintext -> CKKSPackedEncoding::Encode)*/
 /* ------------------------------------------------------------------------ */
 
-/* x[0..n) (n <= slots) -> signed coefficient vector coeff[N] (COEFFICIENT
- * domain, before the per-tower reduction).  Returns -2 if some scaled value
- * exceeds 2^61 (PALISADE's approxFactor path; not implemented — the product
- * rejects such inputs the same way). */
-int or_encode_coeffs(const double* x, size_t n, uint32_t N, uint32_t slots, double delta,
-                     int64_t* coeff) {
+/* The large-value path of CKKSPackedEncoding::Encode [PALISADE-1.11, restated; no reference
+ * fixture exercises it, so parity with PALISADE is unpinned]:
+ *   v_i = FFTSpecialInv(x)_i * Delta (real and imaginary parts);
+ *   logc = max over nonzero v_i of ceil(log2|v_i|) (glibc log2), at least 0;
+ *   logApprox = max(0, logc - MAX_BITS_IN_WORD), MAX_BITS_IN_WORD = 62;
+ *   r_i = llround(v_i / 2^logApprox)   (|r_i| <= 2^62);
+ *   FitToNativeVector: temp = r < 0 ? B + r : r with B = Max64BitValue() = 2^63 - 513, then
+ *     temp > B >> 1 ? (temp - (B - q)) mod q : temp mod q
+ *   (== r mod q for |r| <= 2^62 - 257, r - B or r + B beyond: or_fit_wrap);
+ *   the residues are then multiplied by 2^logApprox mod q_t (CRTMult steps of <= 2^60 compose
+ *   to exactly that) before the NTT.
+ * For |v| <= 2^61 (logc <= 61) this is the plain llround encode. */
+#define OR_MAX_BITS_IN_WORD 62
+#define OR_MAX64_VALUE 9223372036854775295LL /* 2^63 - 513 */
+
+int64_t or_fit_wrap(int64_t r) {
+  const int64_t hf = OR_MAX64_VALUE >> 1; /* 2^62 - 257 */
+  if (r > hf) return r - OR_MAX64_VALUE;
+  if (r < 0 && OR_MAX64_VALUE + r <= hf) return r + OR_MAX64_VALUE;
+  return r;
+}
+
+/* ceil(log2 |v|) as Encode computes it (glibc log2, then ceil). */
+int or_encode_logc(double v) { return (int)ceil(log2(fabs(v))); }
+
+/* x[0..n) (n <= slots) -> coefficient vector coeff[N] of FitToNativeVector-equivalent signed
+ * values (COEFFICIENT domain, before the per-tower reduction) and the scale-down exponent
+ * *log_approx (the residues are coeff * 2^log_approx mod q_t).  Returns -1 on bad sizes, -3 on a
+ * non-finite scaled value. */
+int or_encode_coeffs_ex(const double* x, size_t n, uint32_t N, uint32_t slots, double delta,
+                        int64_t* coeff, int* log_approx) {
   if (n > slots || 2ull * slots > N) return -1;
   double* re = calloc(slots, sizeof(double));
   double* im = calloc(slots, sizeof(double));
@@ -370,30 +395,52 @@ int or_encode_coeffs(const double* x, size_t n, uint32_t N, uint32_t slots, doub
   or_fft_special_inv(re, im, slots);
   uint32_t gap = N / (2 * slots);
   memset(coeff, 0, sizeof(int64_t) * N);
-  int rc = 0;
-  const double lim = 2305843009213693952.0; /* 2^61 */
+  int logc = 0;
   for (uint32_t i = 0; i < slots; ++i) {
-    double vr = re[i] * delta, vi = im[i] * delta;
-    if (fabs(vr) > lim || fabs(vi) > lim) rc = -2;
-    coeff[i * gap] = or_round_half_away(vr);
-    coeff[N / 2 + i * gap] = or_round_half_away(vi);
+    re[i] *= delta;
+    im[i] *= delta;
+    if (!isfinite(re[i]) || !isfinite(im[i])) {
+      free(re);
+      free(im);
+      return -3;
+    }
+    if (re[i] != 0 && or_encode_logc(re[i]) > logc) logc = or_encode_logc(re[i]);
+    if (im[i] != 0 && or_encode_logc(im[i]) > logc) logc = or_encode_logc(im[i]);
+  }
+  const int a = logc > OR_MAX_BITS_IN_WORD ? logc - OR_MAX_BITS_IN_WORD : 0;
+  const double approx = ldexp(1.0, a);
+  for (uint32_t i = 0; i < slots; ++i) {
+    coeff[i * gap] = or_fit_wrap(or_round_half_away(re[i] / approx));
+    coeff[N / 2 + i * gap] = or_fit_wrap(or_round_half_away(im[i] / approx));
   }
   free(re);
   free(im);
-  return rc;
+  *log_approx = a;
+  return 0;
 }
 
-/* full encode: coeffs -> per-tower residues -> NTT (EVALUATION). out[L][N]. */
+/* The plain signed coefficients; -2 when the vector takes the scale-down path (its
+ * coefficients are coeff * 2^logApprox, not int64 values). */
+int or_encode_coeffs(const double* x, size_t n, uint32_t N, uint32_t slots, double delta,
+                     int64_t* coeff) {
+  int a = 0;
+  int rc = or_encode_coeffs_ex(x, n, N, slots, delta, coeff, &a);
+  return rc ? rc : (a ? -2 : 0);
+}
+
+/* full encode: coeffs -> per-tower residues (x 2^logApprox) -> NTT (EVALUATION). out[L][N]. */
 int or_encode(const double* x, size_t n, uint32_t N, uint32_t slots, double delta, uint32_t L,
               const uint64_t* q, const uint64_t* psi, uint64_t* out) {
   int64_t* c = malloc(sizeof(int64_t) * N);
-  int rc = or_encode_coeffs(x, n, N, slots, delta, c);
+  int a = 0;
+  int rc = or_encode_coeffs_ex(x, n, N, slots, delta, c, &a);
   if (rc) {
     free(c);
     return rc;
   }
   for (uint32_t t = 0; t < L; ++t) {
-    for (uint32_t j = 0; j < N; ++j) out[(size_t)t * N + j] = or_mod_signed(c[j], q[t]);
+    const uint64_t pw = or_powmod(2, (uint64_t)a, q[t]);
+    for (uint32_t j = 0; j < N; ++j) out[(size_t)t * N + j] = mulmod(or_mod_signed(c[j], q[t]), pw, q[t]);
     or_ntt_fwd(out + (size_t)t * N, N, q[t], psi[t]);
   }
   free(c);

@@ -62,6 +62,10 @@ def _load():
         "or_fft_special": (None, [f64p, f64p, C.c_uint32]),
         "or_round_half_away": (C.c_int64, [C.c_double]),
         "or_encode_coeffs": (C.c_int, [f64p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_double, i64p]),
+        "or_encode_coeffs_ex": (C.c_int, [f64p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_double, i64p,
+                                          C.POINTER(C.c_int)]),
+        "or_fit_wrap": (C.c_int64, [C.c_int64]),
+        "or_encode_logc": (C.c_int, [C.c_double]),
         "or_encode": (C.c_int, [f64p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_double, C.c_uint32,
                                 u64p, u64p, u64p]),
         "or_encrypt": (None, [u64p, u64p, i64p, i64p, i64p, C.c_uint32, C.c_uint32, u64p, u64p, u64p]),
@@ -205,6 +209,18 @@ def encode_coeffs(x, N: int, slots: int, delta: float) -> np.ndarray:
     if rc:
         raise ValueError("encode failed rc=%d" % rc)
     return c
+
+
+def encode_coeffs_ex(x, N: int, slots: int, delta: float):
+    """Encode's coefficients with the large-value path: (signed coeffs, logApprox); the
+    residues are coeffs * 2^logApprox mod q_t (PALISADE's approxFactor, ckks_oracle.c)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    c = np.zeros(N, np.int64)
+    a = C.c_int()
+    rc = lib.or_encode_coeffs_ex(_p(x, f64p), len(x), N, slots, float(delta), _p(c, i64p), C.byref(a))
+    if rc:
+        raise ValueError("encode failed rc=%d" % rc)
+    return c, a.value
 
 
 def encode(x, N: int, slots: int, delta: float, q, psi) -> np.ndarray:

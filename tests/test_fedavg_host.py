@@ -7,9 +7,56 @@ from SHELFI_FHE import fedavg as F
 
 
 def test_model_param_counts():
-    assert sum(int(np.prod(s)) for s in F.resnet_shapes(18).values()) == 11_689_512
-    assert sum(int(np.prod(s)) for s in F.resnet_shapes(50).values()) == 25_557_032
+    assert sum(int(np.prod(s)) for s in F.resnet_shapes(18, buffers=False).values()) == 11_689_512
+    assert sum(int(np.prod(s)) for s in F.resnet_shapes(50, buffers=False).values()) == 25_557_032
     assert sum(int(np.prod(s)) for s in F.lenet5_shapes().values()) == 61_706
+
+
+def _bn_channels(depth):
+    """Independent count of BatchNorm channels in torchvision's ResNets: the stem's bn1, every
+    block's BNs (2 of `planes` for BasicBlock; planes, planes, 4 planes for Bottleneck) and the
+    first block's downsample BN of each stage that changes shape."""
+    planes, blocks = [64, 128, 256, 512], {18: [2, 2, 2, 2], 50: [3, 4, 6, 3]}[depth]
+    ch, n_bn = 64, 1
+    for i, (p, nb) in enumerate(zip(planes, blocks)):
+        per_block = [p, p] if depth == 18 else [p, p, 4 * p]
+        ch += nb * sum(per_block)
+        n_bn += nb * len(per_block)
+        if depth == 50 or i > 0:  # stage 1 of ResNet-18 keeps 64 channels at stride 1: no downsample
+            ch += per_block[-1]
+            n_bn += 1
+    return ch, n_bn
+
+
+@pytest.mark.parametrize("depth,params,keys", [(18, 11_689_512, 62), (50, 25_557_032, 161)])
+def test_state_dict_includes_batchnorm_buffers(depth, params, keys):
+    """benchmark.py:457 encrypts model.state_dict(): every BN's running_mean, running_var and
+    num_batches_tracked (one int64 element) ride along with the parameters, each its own key."""
+    sh = F.resnet_shapes(depth)
+    ch, n_bn = _bn_channels(depth)
+    assert n_bn == {18: 20, 50: 53}[depth]
+    assert len(sh) == keys + 3 * n_bn
+    assert sum(int(np.prod(s)) for s in sh.values()) == params + 2 * ch + n_bn
+    nbt = [k for k in sh if k.endswith("num_batches_tracked")]
+    assert len(nbt) == n_bn and all(sh[k] == () for k in nbt)
+    # state_dict order: a BN's buffers follow its bias
+    ks = list(sh)
+    i = ks.index("bn1.bias")
+    assert ks[i + 1:i + 4] == ["bn1.running_mean", "bn1.running_var", "bn1.num_batches_tracked"]
+
+
+def test_per_key_ciphertext_count_resnet18_batch4096():
+    """The reference run (benchmark.py:423 model = model_res18, CKKS batch 4096 :477) encrypts every
+    state_dict key on its own (:489-493): sum_k ceil(n_k / 4096) ciphertexts per client.  The 62
+    parameter keys give 2,893; the 60 BN buffer keys (each <= 512 values) one ciphertext each."""
+    params_only = sum(-(-int(np.prod(s)) // 4096) for s in F.resnet_shapes(18, buffers=False).values())
+    assert params_only == 2893
+    per_key = F.cts_per_key(F.resnet_shapes(18), 4096)
+    assert sum(per_key.values()) == 2953 == params_only + 60
+    assert per_key["layer4.1.bn2.num_batches_tracked"] == 1 and per_key["fc.weight"] == 125
+    st = F.synthetic_states(F.resnet_shapes(18), 1, seed=1)[0]
+    assert st["bn1.num_batches_tracked"].dtype == np.int64 and st["bn1.num_batches_tracked"].shape == (1,)
+    assert (st["layer1.0.bn1.running_var"] >= 0).all()
 
 
 def test_layer_index_rule():

@@ -17,7 +17,8 @@ from SHELFI_FHE import device as D  # noqa: E402
 
 @pytest.fixture(scope="module")
 def ck():
-    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=21, decodeNoise=False)
+    # the library blob: these tests forge its header and residues byte by byte
+    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=21, decodeNoise=False, wireFormat="shelfi")
     c.loadCryptoParams()
     return c
 

@@ -22,16 +22,17 @@ from SHELFI_FHE import dist as X  # noqa: E402
 @pytest.fixture(scope="module")
 def c2(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("u64_c2")) + os.sep
-    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False, wireFormat="shelfi")
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 
 
 def test_auto_layout_by_rows(c2):
     """cfg2's 16 x 4 arena (2,048 rows per learner) takes the uint64 layout; cfg5-sized ones stay packed."""
-    assert D.Arena(c2, 16, 4).layout == "uint64"
-    assert D.Arena(c2, 2, 8).layout == "uint64"   # 4,096 rows: the threshold itself
-    assert D.Arena(c2, 2, 9).layout == "packed"
+    assert D.Arena(c2, 16, 4, layout="auto").layout == "uint64"
+    assert D.Arena(c2, 16, 4).layout == "packed"  # the default; "auto" is opt-in
+    assert D.Arena(c2, 2, 8, layout="auto").layout == "uint64"   # 4,096 rows: the threshold itself
+    assert D.Arena(c2, 2, 9, layout="auto").layout == "packed"
     assert D.Arena(c2, 2, 1, layout="packed").layout == "packed"
     with pytest.raises(ValueError):
         D.Arena(c2, 2, 1, layout="u128")
@@ -85,7 +86,8 @@ def test_u64_layout_refusals(c2, tmp_path):
     ar.put(0, cts[0])
     assert torch.equal(ar.wavg([0.5, 0.5]), good)
     # an upload under another key is refused at its header and marks the slot too
-    other = m.CKKS("ckks", 16384, 52, str(tmp_path) + os.sep, multDepth=3, seed=8, decodeNoise=False)
+    other = m.CKKS("ckks", 16384, 52, str(tmp_path) + os.sep, multDepth=3, seed=8, decodeNoise=False,
+                   wireFormat="shelfi")
     assert other.genCryptoContextAndKeyGen() == 1
     with pytest.raises(m.ShelfiError, match="different key"):
         ar.put(1, other.encrypt(xs[1]))
@@ -93,6 +95,11 @@ def test_u64_layout_refusals(c2, tmp_path):
         ar.wavg([0.5, 0.5])
     ar.put(1, cts[1])
     assert torch.equal(ar.wavg([0.5, 0.5]), good)
+    # slot() is a copy: writing into it cannot place an unvalidated residue in the arena
+    s0 = ar.slot(0)
+    assert torch.equal(s0, cts[0])
+    s0.fill_(-1)
+    assert torch.equal(ar.slot(0), cts[0]) and torch.equal(ar.wavg([0.5, 0.5]), good)
     # the C-ABI combine takes packed arenas only
     comm = X.Comm(c2, rank=0, world=1)
     try:

@@ -29,7 +29,7 @@ K = 3
 @pytest.fixture(scope="module")
 def c2(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("arena_c2")) + os.sep
-    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False)
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=7, decodeNoise=False, wireFormat="shelfi")
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 
@@ -37,14 +37,14 @@ def c2(tmp_path_factory):
 @pytest.fixture(scope="module")
 def c2_other_key(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("arena_c2b")) + os.sep
-    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=8, decodeNoise=False)
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=8, decodeNoise=False, wireFormat="shelfi")
     assert ck.genCryptoContextAndKeyGen() == 1
     return ck
 
 
 @pytest.fixture(scope="module")
 def c1():
-    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42, decodeNoise=False)
+    ck = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=42, decodeNoise=False, wireFormat="shelfi")
     ck.loadCryptoParams()
     return ck
 

@@ -93,7 +93,7 @@ def test_sweep_row_bitexact(tmp_path, batch, sb):
     got = ar.wavg(w)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), ref)
-    au = D.Arena(ck, 3, K)  # a small arena: the uint64 layout
+    au = D.Arena(ck, 3, K, layout="auto")  # a small arena: the uint64 layout
     assert au.layout == "uint64"
     for c, b in enumerate(blobs):
         au.put(c, b)
@@ -111,9 +111,13 @@ def test_sweep_row_cnn_archives(tmp_path, batch, sb):
     """benchmark_crypto.py:163-224 for N = 3 clients holding the same CNN weights: per-key
     encrypt in the reference's wire format, the pickled size of client 0's archives, the
     per-key weighted average and decrypt to each layer's size."""
-    ck, inf, q, psi, kseed, d = _context(tmp_path, batch, sb)
-    ck.set_wire_format("palisade")
-    ck.set_decode_noise(True)
+    # the reference's constructor and nothing else (benchmark_crypto.py:170-173): the reference's
+    # wire format and the flooded decrypt are the defaults, no set_wire_format call
+    d = str(tmp_path) + os.sep
+    ck = m.CKKS("ckks", batch, sb, d)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    assert ck.wire_format() == "palisade"
+    inf = ck.info()
     rng = np.random.default_rng(sb)
     params = collections.OrderedDict((k, rng.uniform(-0.1, 0.1, n).astype(np.float32)) for k, n in CNN_KEYS)
     enc = [collections.OrderedDict() for _ in range(3)]

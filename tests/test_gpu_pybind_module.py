@@ -53,8 +53,8 @@ def test_byte_identical_to_ctypes_package(nm):
     a = nm.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=99, decodeNoise=False)
     a.loadCryptoParams()
     b = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=99, decodeNoise=False)
-    b.loadCryptoParams()
-    b.set_wire_format("palisade")
+    b.loadCryptoParams()  # both front ends default to the reference's wire format: no set_wire_format
+    assert b.wire_format() == "palisade"
     ea, eb = [a.encrypt(x) for x in xs], [b.encrypt(x) for x in xs]
     assert ea == eb
     ra, rb = a.computeWeightedAverage(ea, w), b.computeWeightedAverage(eb, w)
@@ -89,3 +89,19 @@ def test_keygen_then_load(nm, tmp_path):
     user.loadCryptoParams()
     x = np.random.default_rng(2).uniform(-1, 1, 9000)
     assert np.abs(gen.decrypt(user.encrypt(x), 9000) - x).max() < 1e-6
+
+
+def test_default_bytes_identical_after_keygen(nm, tmp_path):
+    """Option A (ctypes) and Option B (pybind) constructed as the reference's scripts do, keys from
+    genCryptoContextAndKeyGen: the same seeded encrypt gives the same PALISADE archive bytes."""
+    d = str(tmp_path) + os.sep
+    gen = m.CKKS("ckks", 4096, 52, d, seed=5)
+    assert gen.genCryptoContextAndKeyGen() == 1
+    a = nm.CKKS("ckks", 4096, 52, d, seed=77)
+    a.loadCryptoParams()
+    b = m.CKKS("ckks", 4096, 52, d, seed=77)
+    b.loadCryptoParams()
+    x = np.random.default_rng(8).uniform(-1, 1, 2 * 4096 + 5)
+    ea, eb = a.encrypt(x), b.encrypt(x)
+    assert ea == eb and m.blob_info(eb)["format"] == "palisade"
+    assert gen.encrypt(x)[:1] == b"\x01"  # the generating context answers in archives too

@@ -103,7 +103,7 @@ def test_blob_info_validation():
     struct.pack_into("<HHIIQIIdQQII", hdr, 4, 1, 64, 13, 2, 1, 1, 0, 2.0 ** 52, 1, 2, 4096, 4)
     blob = bytes(hdr) + bytes(2 * 2 * 8192 * 8)
     info = m.blob_info(blob)
-    assert info == {"num_cts": 1, "depth": 1, "scale": 2.0 ** 52, "key_id": 2}
+    assert info == {"num_cts": 1, "depth": 1, "scale": 2.0 ** 52, "key_id": 2, "format": "shelfi"}
     with pytest.raises(RuntimeError):
         m.blob_info(blob[:-8])
     with pytest.raises(RuntimeError):
@@ -409,3 +409,103 @@ def test_packed_exchange_combine_gloo_world8_rehearsal():
     pytest.importorskip("torch")
     res = _spawn_world(8, _gloo_packed_worker, 3, K=13, C_=11)
     assert res == [(r, True) for r in range(8)]
+
+
+def _c_abi_packed_plan(K, W, pieces):
+    """comm.cpp shelfi_dev_combine_arena_packed's block arithmetic, restated: rank r owns global
+    ciphertexts [r Ks, (r+1) Ks), Ks = ceil(K / W); piece j covers sub-slice [j Kp, j Kp + kn) of
+    EVERY rank's slice, Kp = ceil(Ks / P), P = max(1, min(pieces, Ks)); the send region of piece j
+    starts W * kj0 packed ciphertexts in and holds [W][kn] blocks: block gr = global cts
+    a = gr Ks + kj0 .. a + cnt (cnt = min(kn, K - a), 0 past K), zero-padded to kn."""
+    Ks = -(-K // W)
+    P = max(1, min(pieces or 1, Ks))
+    Kp = -(-Ks // P)
+    plan = []
+    for j in range(P):
+        kj0 = j * Kp
+        if kj0 >= Ks:
+            break
+        kn = min(Kp, Ks - kj0)
+        blocks = []
+        for gr in range(W):
+            a = gr * Ks + kj0
+            blocks.append((a, min(kn, K - a) if a < K else 0))
+        plan.append((kj0, kn, blocks))
+    return Ks, plan
+
+
+def _gloo_c_abi_packed_worker(rank, world, port, pieces, result_q, K=7, C_=5):
+    """The C ABI's packed combine (shelfi_dev_combine_arena_packed) block for block on gloo: the
+    [W][kn] send regions at W * kj0, packed partials of a = gr Ks + kj0 with zero padding past K,
+    the grouped send / recv as one all_to_all_single of equal blocks, the unit-weight sum of the
+    W received blocks into share[kj0 ..].  Rank r's contiguous share must equal the one-process
+    aggregate of [r Ks, min(K, (r+1) Ks))."""
+    import sys
+
+    import torch
+    import torch.distributed as dist_
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import arena_layout as AL
+    import oracle as O_
+    from SHELFI_FHE import dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist_.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, L = 1024, 2
+        q, _ = O_.params_generate(N, L, 40, 50)
+        delta = float(int(q[-1]))
+        qi = [int(x) for x in q]
+        pcw = 2 * N * sum(AL.widths(qi)) // 64  # arena_ct_words(p, 1)
+        rng = np.random.default_rng(11)
+        cts = []
+        for _ in range(C_):
+            a = np.empty((K, 2, L, N), np.uint64)
+            for t in range(L):
+                a[:, :, t, :] = rng.integers(0, qi[t], (K, 2, N), dtype=np.uint64)
+            cts.append(a)
+        w = list(rng.dirichlet(np.ones(C_)))
+        mine = dist.learner_shard(C_, rank, world)
+        Ks, plan = _c_abi_packed_plan(K, world, pieces)
+        send = torch.full((world * Ks * pcw,), -7, dtype=torch.int64)  # garbage: padding must be written
+        recv = torch.full((world * Ks * pcw,), -7, dtype=torch.int64)
+        share = np.full((Ks, 2, L, N), 2 ** 64 - 1, np.uint64)
+        for kj0, kn, blocks in plan:
+            base = world * kj0 * pcw
+            for gr, (a, cnt) in enumerate(blocks):
+                off = base + gr * kn * pcw
+                if cnt:
+                    part = O_.wavg([cts[i][a:a + cnt] for i in mine], [w[i] for i in mine], q, delta)
+                    send[off:off + cnt * pcw] = torch.from_numpy(AL.pack_arena([part], qi, N).view(np.int64).copy())
+                if cnt < kn:
+                    send[off + cnt * pcw:off + kn * pcw] = 0
+            n = world * kn * pcw
+            dist_.all_to_all_single(recv[base:base + n], send[base:base + n])
+            acc = np.zeros((kn, 2, L, N), np.uint64)
+            for h in range(world):
+                blk = recv[base + h * kn * pcw:base + (h + 1) * kn * pcw].numpy().view(np.uint32)
+                (x,) = AL.unpack_arena(blk, 1, kn, L, N, qi)
+                for t in range(L):
+                    acc[:, :, t, :] = (acc[:, :, t, :] + x[:, :, t, :]) % q[t]
+            share[kj0:kj0 + kn] = acc
+        full = O_.wavg(cts, w, q, delta)
+        a, b = min(K, rank * Ks), min(K, (rank + 1) * Ks)
+        ok = np.array_equal(share[:b - a], full[a:b])
+        ok &= bool((share[b - a:] == 0).all())  # the padded tail sums packed zeros
+        ok &= Ks == -(-K // world)
+        result_q.put((rank, bool(ok)))
+    finally:
+        dist_.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,pieces,K,C_", [(2, 1, 7, 5), (2, 3, 7, 5), (8, 3, 13, 11), (8, 8, 5, 9)])
+def test_c_abi_packed_combine_layout_gloo(world, pieces, K, C_):
+    """the C ABI's multi-rank packed combine had run only at one rank on device.  Its
+    offset arithmetic (owned range gr*Ks + kj0, per-piece kn, zero padding past K, equal [W][kn]
+    blocks to every peer) restated on gloo: every rank's share is bit-exact, K = 5 over 8 ranks
+    included (ranks owning nothing)."""
+    pytest.importorskip("torch")
+    res = _spawn_world(world, _gloo_c_abi_packed_worker, pieces, K=K, C_=C_)
+    assert res == [(r, True) for r in range(world)]
