@@ -1008,14 +1008,19 @@ struct StageRun {
   }
 };
 
-// encode + encrypt n doubles (host) -> K ciphertext payloads written to out_payload.
+// The encode range flag of an encrypt call (kernels.hip enc_range_flag): non-finite values are refused;
+// a finite |x Delta| above 2^61 means the call is redone on the large-value path.
+static bool encode_needs_approx(uint32_t flag) {
+  if (flag & 2u) throw Error{SHELFI_ERR_RANGE, "encrypt: non-finite input value"};
+  return (flag & 1u) != 0;
+}
+
+// encode + encrypt n doubles (host) -> K ciphertext payloads written to out_payload (approx: every
+// chunk on the large-value path, launch_encrypt_approx; same key and counters, so the same samples).
 static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, uint64_t K,
-                                   const CtLayout& dst) {
+                                   const CtLayout& dst, const uint32_t key[8], uint64_t g0, bool approx) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
-  uint32_t key[8];
-  uint64_t g0;
-  draw_key(ctx, K, key, &g0);
   uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
   kc = std::min<uint64_t>(kc, K);
   const size_t xin = kc * p.batch * 8, cto = kc * ct_bytes;
@@ -1041,8 +1046,12 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
     SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
     SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
     if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));  // ct buffer drained
-    launch_encrypt(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
-                   g0 + k0, ctx->dev_flag, pp.b);
+    if (approx)
+      launch_encrypt_approx(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
+                            g0 + k0, pp.b);
+    else
+      launch_encrypt(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
+                     g0 + k0, ctx->dev_flag, pp.b);
     if (dst.packed)  // canonical residues: the residue check cannot fire
       launch_blob_pack((const uint64_t*)cb[b], kn, p.L, p.logN, ap, ctx->dt.tc, (uint32_t*)pb[b],
                        ctx->dev_flag + 5, pp.b);
@@ -1056,11 +1065,8 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
   SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, pp.b));  // pinned
   sr.finish();
   pp.sync();
-  std::memset(key, 0, sizeof(key));
-  const uint32_t flag = ctx->host_flag[0];
-  if (flag)
-    throw Error{SHELFI_ERR_RANGE,
-                "encrypt: non-finite input or |value * scale| > 2^61 (PALISADE approxFactor range)"};
+  if (!approx && encode_needs_approx(ctx->host_flag[0]))
+    encrypt_bytes_pipeline(ctx, x, n, K, dst, key, g0, true);
 }
 
 int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out, size_t out_cap,
@@ -1081,7 +1087,18 @@ int shelfi_encrypt_into(shelfi_ctx* ctx, const double* x, size_t n, uint8_t* out
     // residues first (the parallel drains first-touch the fresh pages), framing after
     CtLayout dst = make_output(ctx, ctx->wire, K, 1, 0, p.delta, nullptr, &total);
     dst.base = out;
-    if (K) encrypt_bytes_pipeline(ctx, x, n, K, dst);
+    if (K) {
+      uint32_t key[8];
+      uint64_t g0;
+      draw_key(ctx, K, key, &g0);
+      try {
+        encrypt_bytes_pipeline(ctx, x, n, K, dst, key, g0, false);
+      } catch (...) {
+        std::memset(key, 0, sizeof(key));
+        throw;
+      }
+      std::memset(key, 0, sizeof(key));
+    }
     make_output(ctx, ctx->wire, K, 1, 0, p.delta, out, &total);
   });
 }
@@ -1928,17 +1945,32 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
     SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, s));
     const size_t ct_words = 2ull * p.L * p.N;
-    for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
-      const uint64_t kc = std::min(kc_max, K - k0);
-      const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kc * p.batch);
-      launch_encrypt(p, ctx->dt, ctx->dk, x_dev + xs, xn, kc, ct_dev + k0 * ct_words, scratch,
-                     key, g0 + k0, ctx->dev_flag, s);
+    bool approx = false;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (uint64_t k0 = 0; k0 < K; k0 += kc_max) {
+        const uint64_t kc = std::min(kc_max, K - k0);
+        const uint64_t xs = k0 * p.batch, xn = std::min<uint64_t>(n - xs, kc * p.batch);
+        if (approx)
+          launch_encrypt_approx(p, ctx->dt, ctx->dk, x_dev + xs, xn, kc, ct_dev + k0 * ct_words, scratch, key,
+                                g0 + k0, s);
+        else
+          launch_encrypt(p, ctx->dt, ctx->dk, x_dev + xs, xn, kc, ct_dev + k0 * ct_words, scratch,
+                         key, g0 + k0, ctx->dev_flag, s);
+      }
+      if (approx) break;
+      SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));  // pinned
+      SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
+      bool redo;
+      try {
+        redo = encode_needs_approx(ctx->host_flag[0]);
+      } catch (...) {
+        std::memset(key, 0, sizeof(key));
+        throw;
+      }
+      if (!redo) break;
+      approx = true;  // some |x Delta| > 2^61: redo the call on the large-value path
     }
     std::memset(key, 0, sizeof(key));
-    SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));  // pinned
-    SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
-    if (ctx->host_flag[0])
-      throw Error{SHELFI_ERR_RANGE, "encrypt: |value * scale| exceeds 2^61 (approxFactor range)"};
   });
 }
 

@@ -24,7 +24,11 @@
 // multiplications use Shoup's precomputed quotient (w' = floor(w 2^64 / q)).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "dev_common.h"
 #include "shelfi_internal.h"
@@ -1143,6 +1147,10 @@ __device__ __forceinline__ void load_cdt32(const uint64_t* __restrict__ cdt, int
   }
 }
 
+// Encode's range flag (dev_flag[0]): bit 0 = a finite |x Delta| above 2^61 (the call is redone on the
+// large-value path, launch_encrypt_approx), bit 1 = a non-finite value (refused).
+__device__ __forceinline__ uint32_t enc_range_flag(double val) { return isfinite(val) ? 1u : 2u; }
+
 __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
                                                        uint64_t K, uint32_t logN, uint32_t logS,
                                                        double delta,
@@ -1162,7 +1170,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
   const double dS = (double)S;
-  const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
+  const double lim = 2305843009213693952.0;  // 2^61: beyond, the call is redone by launch_encrypt_approx
   uint32_t w[16];
   chacha20_block32(key, h >> 2, nonce, w);
   uint32_t u[4] = {w[4 * (h & 3)], w[4 * (h & 3) + 1], w[4 * (h & 3) + 2], w[4 * (h & 3) + 3]};
@@ -1178,7 +1186,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
     if ((jj & ((1u << gapLog) - 1)) == 0) {
       const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
       const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
-      if (!(fabs(val) <= lim)) atomicOr(flag, 1u);  // also catches NaN / inf
+      if (!(fabs(val) <= lim)) atomicOr(flag, enc_range_flag(val));
       m = round_half_away(val);
     }
     me0[(k << logN) + j] = m + gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 2 * N16 + h, nonce, i); });
@@ -1309,7 +1317,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   const uint32_t S = 1u << logS, gapLog = logN - 1 - logS;
   const double invS = 1.0 / (double)S;  // a power of two: x * (1/S) == x / S exactly
-  const double lim = 2305843009213693952.0;  // 2^61 (PALISADE approxFactor threshold)
+  const double lim = 2305843009213693952.0;  // 2^61: beyond, the call is redone by launch_encrypt_approx
   const uint64_t LN = (uint64_t)L << logN;
   // columns stages of one polynomial of tower t (values x[r] < q) and its lazy store
   // (towers with q < kNoRedQ run unreduced (NORED, fwd_set_ct): no stage reductions, no
@@ -1450,7 +1458,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
         const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
         const double vr = __dmul_rn(__dmul_rn(cv.x, invS), delta);
         const double vi = __dmul_rn(__dmul_rn(cv.y, invS), delta);
-        if (!(fabs(vr) <= lim) || !(fabs(vi) <= lim)) atomicOr(flag, 1u);  // also NaN / inf
+        if (!(fabs(vr) <= lim) || !(fabs(vi) <= lim)) atomicOr(flag, enc_range_flag(vr) | enc_range_flag(vi));
         mre = round_half_away(vr);
         mim = round_half_away(vi);
       }
@@ -1505,19 +1513,16 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
 constexpr uint64_t kEncTsMaxK = 24;
 
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K) {
-  // FFT buffer | pbuf [K][3][L][N] | me0 [K][N] int64 | ve [K][N] int16
+  // FFT buffer | pbuf [K][3][L][N] | me0 [K][N] int64 | ve [K][N] int16 | the large-value path's
+  // per-ciphertext max, exponent and 2^logApprox mod q_t (launch_encrypt_approx)
   return K * (uint64_t)p.batch * sizeof(double2) + K * 3ull * p.L * p.N * sizeof(uint64_t) +
-         K * (uint64_t)p.N * (sizeof(int64_t) + sizeof(int16_t)) + 64;
+         K * (uint64_t)p.N * (sizeof(int64_t) + sizeof(int16_t)) + K * (8 + 8 + 16ull * p.L) + 64;
 }
 
-void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
-                    uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
-                    uint64_t g0, uint32_t* flag, hipStream_t s) {
-  if (!K) return;
+// encode's FFTSpecialInv of K slot vectors (x: n doubles, zero-padded) into fbuf [K][S] (complex)
+static void launch_encode_fft(const Params& p, const DeviceTables& dt, const double* x, uint64_t n, uint64_t K,
+                              double2* fbuf, hipStream_t s) {
   const uint32_t logS = __builtin_ctz(p.batch);
-  double2* fbuf = reinterpret_cast<double2*>(scratch);
-  uint64_t* pbuf = reinterpret_cast<uint64_t*>(fbuf + K * (uint64_t)p.batch);
-  // 1. FFTSpecialInv of each ciphertext's slot vector
   const uint32_t blkLog = fft_block_log(logS);
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;
@@ -1545,6 +1550,17 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                        blkLog, 1, dt.fft_inv);
   }
   SHELFI_HIP(hipGetLastError());
+}
+
+void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
+                    uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
+                    uint64_t g0, uint32_t* flag, hipStream_t s) {
+  if (!K) return;
+  const uint32_t logS = __builtin_ctz(p.batch);
+  double2* fbuf = reinterpret_cast<double2*>(scratch);
+  uint64_t* pbuf = reinterpret_cast<uint64_t*>(fbuf + K * (uint64_t)p.batch);
+  // 1. FFTSpecialInv of each ciphertext's slot vector
+  launch_encode_fft(p, dt, x, n, K, fbuf, s);
   Key8 k8;
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
   const uint32_t nblkLog = ntt_block_log(p.logN);
@@ -1674,6 +1690,183 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   SHELFI_HIP(hipGetLastError());
 }
 
+// ---------------------------------------------- encode's large-value path ----
+// PALISADE 1.11 CKKSPackedEncoding::Encode (ckks.cpp:80) scales a slot vector down before rounding when
+// its largest coefficient would not fit a 62-bit word [PALISADE-1.11, restated in
+// oracle/ckks_oracle.c or_encode_coeffs_ex; parity with PALISADE unpinned]:
+//   logc = max over nonzero v_i = FFTSpecialInv(x)_i * Delta of ceil(log2 |v_i|);
+//   logApprox = max(0, logc - 62); r_i = llround(v_i / 2^logApprox), wrapped as FitToNativeVector
+//   does with Max64BitValue() = 2^63 - 513 (enc_fit_wrap); residue_t = r_i * 2^logApprox mod q_t.
+// The fast encrypt kernels handle |v| <= 2^61 (logApprox = 0, no wrap) and flag anything larger;
+// the call is then redone here: per-ciphertext max |v| on the device, logApprox from glibc's log2 on
+// the host (the function PALISADE calls; one exponent per ciphertext), then the coefficients,
+// samples and the 2^logApprox factor written as canonical residues [K][3][L][N], the generic NTT,
+// and the public-key combine.  Same ChaCha20 streams as the fast path, so only the message
+// coefficients can differ, and only where the fast path refused.
+__device__ __forceinline__ int64_t enc_fit_wrap(int64_t r) {
+  constexpr int64_t kMax64 = 9223372036854775295LL;  // PALISADE Max64BitValue(): 2^63 - 513
+  constexpr int64_t hf = kMax64 >> 1;
+  if (r > hf) return r - kMax64;
+  if (r < 0 && kMax64 + r <= hf) return r + kMax64;
+  return r;
+}
+
+// per ciphertext: max |Re|, |Im| of its FFTSpecialInv output, as the bits of a positive double
+__global__ __launch_bounds__(256) void enc_maxabs_kernel(const double2* __restrict__ fbuf, uint32_t logS,
+                                                         uint64_t* __restrict__ amax) {
+  const uint32_t S = 1u << logS;
+  const double2* __restrict__ f = fbuf + (uint64_t)blockIdx.x * S;
+  uint64_t m = 0;
+  for (uint32_t i = threadIdx.x; i < S; i += 256) {
+    const double2 v = f[i];
+    const uint64_t a = (uint64_t)__double_as_longlong(fabs(v.x)), b = (uint64_t)__double_as_longlong(fabs(v.y));
+    m = max(m, max(a, b));
+  }
+  __shared__ uint64_t red[256];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t w = 128; w; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) amax[blockIdx.x] = red[0];
+}
+
+// thread = sample group h of ciphertext k (enc_prep_kernel's mapping and streams): v, m + e0, e1 as
+// canonical residues of every tower into pbuf [K][3][L][N] (COEFFICIENT domain)
+__global__ __launch_bounds__(256) void enc_expand_approx_kernel(
+    const double2* __restrict__ fbuf, uint64_t K, uint32_t logN, uint32_t logS, uint32_t L, double delta,
+    const uint64_t* __restrict__ cdt, int T, Key8 key, uint64_t g0, const TowerConst* __restrict__ tcs,
+    const int32_t* __restrict__ log_approx, const uint64_t* __restrict__ pw, uint64_t* __restrict__ pbuf) {
+  const uint32_t N = 1u << logN, S = 1u << logS, N16 = N >> 4, V0 = N >> 6;
+  __shared__ uint32_t thi[64], tlo[64];
+  load_cdt32(cdt, T, thi, tlo);
+  __syncthreads();
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = gid >> (logN - 4);
+  if (k >= K) return;
+  const uint32_t h = (uint32_t)(gid & (N16 - 1));
+  const uint64_t nonce = (1ull << 56) | (g0 + k);
+  const uint32_t half = N >> 1, gapLog = logN - 1 - logS;
+  const double dS = (double)S;
+  const double approx = ldexp(1.0, log_approx[k]);
+  uint32_t w[16];
+  chacha20_block32(key, h >> 2, nonce, w);
+  uint32_t u[4] = {w[4 * (h & 3)], w[4 * (h & 3) + 1], w[4 * (h & 3) + 2], w[4 * (h & 3) + 3]};
+  int32_t vv[16], e0[16], e1[16];
+  int64_t mm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) vv[i] = (int32_t)trit_next(u) - 1;
+  chacha20_block32(key, V0 + h, nonce, w);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t j = h + N16 * i;
+    const uint32_t jj = j < half ? j : j - half;
+    int64_t m = 0;
+    if ((jj & ((1u << gapLog) - 1)) == 0) {
+      const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
+      const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
+      m = enc_fit_wrap(round_half_away(__ddiv_rn(val, approx)));
+    }
+    mm[i] = m;
+    e0[i] = (int32_t)gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 2 * N16 + h, nonce, i); });
+  }
+  chacha20_block32(key, V0 + N16 + h, nonce, w);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    e1[i] = (int32_t)gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 3 * N16 + h, nonce, i); });
+  const uint64_t LN = (uint64_t)L << logN;
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst cst = tcs[t];
+    const uint64_t q = cst.q, P = pw[(k * L + t) * 2], Psh = pw[(k * L + t) * 2 + 1];
+    uint64_t* __restrict__ o = pbuf + k * 3 * LN + ((uint64_t)t << logN) + h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t j = (uint64_t)N16 * i;
+      o[j] = small_mod(vv[i], q);
+      o[LN + j] = addmod(shoup_mul(mod_signed_dev(mm[i], cst), P, Psh, q), small_mod(e0[i], q), q);
+      o[2 * LN + j] = small_mod(e1[i], q);
+    }
+  }
+}
+
+// c0 = NTT(v) b + NTT(m + e0), c1 = NTT(v) a + NTT(e1) from canonical EVALUATION residues
+__global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __restrict__ pbuf, uint64_t K,
+                                                          uint32_t logN, uint32_t L,
+                                                          const TowerConst* __restrict__ tcs,
+                                                          const uint64_t* __restrict__ pk,
+                                                          const uint64_t* __restrict__ pk_sh,
+                                                          uint64_t* __restrict__ ct) {
+  const uint64_t LN = (uint64_t)L << logN;
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= K * LN) return;
+  const uint64_t k = gid / LN, r = gid - k * LN;
+  const uint64_t q = tcs[r >> logN].q;
+  const uint64_t* __restrict__ b = pbuf + k * 3 * LN;
+  const uint64_t V = b[r], M = b[LN + r], E = b[2 * LN + r];
+  ct[k * 2 * LN + r] = addmod(shoup_mul(V, pk[r], pk_sh[r], q), M, q);
+  ct[k * 2 * LN + LN + r] = addmod(shoup_mul(V, pk[LN + r], pk_sh[LN + r], q), E, q);
+}
+
+static uint64_t host_powmod2(uint32_t e, uint64_t q) {
+  unsigned __int128 r = 1 % q, b = 2 % q;
+  for (; e; e >>= 1) {
+    if (e & 1) r = r * b % q;
+    b = b * b % q;
+  }
+  return (uint64_t)r;
+}
+
+void launch_encrypt_approx(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
+                           uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
+                           uint64_t g0, hipStream_t s) {
+  if (!K) return;
+  const uint32_t logS = __builtin_ctz(p.batch);
+  double2* fbuf = reinterpret_cast<double2*>(scratch);
+  uint64_t* pbuf = reinterpret_cast<uint64_t*>(fbuf + K * (uint64_t)p.batch);
+  // aux region after me0 / ve (encrypt_scratch_bytes): amax [K] u64 | log_approx [K] i32 (8-aligned) |
+  // pw [K][L][2] u64
+  uint8_t* aux = reinterpret_cast<uint8_t*>(pbuf + K * 3ull * p.L * p.N) + K * (uint64_t)p.N * 10;
+  uint64_t* amax = reinterpret_cast<uint64_t*>(aux);
+  int32_t* la_dev = reinterpret_cast<int32_t*>(amax + K);
+  uint64_t* pw_dev = amax + K + (K + 1) / 2;
+  launch_encode_fft(p, dt, x, n, K, fbuf, s);
+  hipLaunchKernelGGL(enc_maxabs_kernel, dim3((uint32_t)K), dim3(256), 0, s, fbuf, logS, amax);
+  SHELFI_HIP(hipGetLastError());
+  std::vector<uint64_t> hm(K);
+  SHELFI_HIP(hipMemcpyAsync(hm.data(), amax, K * 8, hipMemcpyDeviceToHost, s));
+  SHELFI_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> la(K);
+  std::vector<uint64_t> pw(K * p.L * 2);
+  for (uint64_t k = 0; k < K; ++k) {
+    double M;
+    std::memcpy(&M, &hm[k], 8);
+    const double v = (M / (double)p.batch) * p.delta;  // the kernels' (c / S) * Delta, monotone in c
+    int logc = 0;
+    if (v != 0) logc = std::max(0, (int)std::ceil(std::log2(v)));  // glibc, as Encode calls it
+    la[k] = logc > 62 ? logc - 62 : 0;
+    for (uint32_t t = 0; t < p.L; ++t) {
+      const uint64_t q = p.q[t], w = host_powmod2((uint32_t)la[k], q);
+      pw[(k * p.L + t) * 2] = w;
+      pw[(k * p.L + t) * 2 + 1] = (uint64_t)(((unsigned __int128)w << 64) / q);
+    }
+  }
+  SHELFI_HIP(hipMemcpyAsync(la_dev, la.data(), K * 4, hipMemcpyHostToDevice, s));
+  SHELFI_HIP(hipMemcpyAsync(pw_dev, pw.data(), pw.size() * 8, hipMemcpyHostToDevice, s));
+  Key8 k8;
+  for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
+  const uint64_t threads = K * (p.N / 16);
+  hipLaunchKernelGGL(enc_expand_approx_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, fbuf, K,
+                     p.logN, logS, p.L, p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, la_dev, pw_dev, pbuf);
+  SHELFI_HIP(hipGetLastError());
+  launch_ntt(pbuf, K * 3ull * p.L, p.L, p.logN, false, dt, s);
+  const uint64_t tot = K * (uint64_t)p.L * p.N;
+  hipLaunchKernelGGL(enc_combine_kernel, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, s, pbuf, K, p.logN, p.L,
+                     dt.tc, dk.pk, dk.pk_sh, ct);
+  SHELFI_HIP(hipGetLastError());
+  SHELFI_HIP(hipStreamSynchronize(s));  // the host tables above are uploaded from pageable memory
+}
+
 // One coefficient of the exact centered CRT: y(t) in [0, q_t) are b_t (Q/q_t)^-1 mod q_t
 // for the L towers; X = sum_t y_t (Q/q_t) - k Q with k = round(sum_t y_t / q_t), read as a
 // signed 128-bit integer, then (double)X * (1/scale) (PALISADE Decode: ConvertToDouble *
@@ -1690,8 +1883,8 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
 // terms (y_t >> s_t) * (2^s_t / q_t) with y_t >> s_t < 2^32 (TowerConst::crt_sh) are each within
 // 2^-31 + 2^-23 of y_t / q_t, and L <= 7 float additions of values below 8 round by <= 2^-21
 // each; round half up.  Correctness therefore needs |X| < 2^127, which every decryptable
-// ciphertext meets by construction (|X| ~ |m| * scale: the encoder refuses |x scale| > 2^61 and
-// a depth-2 aggregate multiplies by weights W < 2^63), not a runtime check;
+// ciphertext meets while |x| * scale^depth < 2^127 (|X| ~ |m| * scale: fresh ciphertexts of |x| < 2^75 and
+// depth-2 aggregates of |sum w x| < 2^23 at scale ~ 2^52; PALISADE's bigint decode reaches Q / 2), not a runtime check;
 // tests/test_gpu_decode_towers.py::test_prefix_decode_near_the_2_127_limit decodes |X| ~ 2^125
 // over a 2^132 prefix.  Over a chain below 2^130 the decode is the plain centred CRT mod Q, and a
 // valid decryption has |X| << Q / 2.  The oracle's CRT is exact (multi-word centring); the two

@@ -286,6 +286,11 @@ void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, boo
 void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const double* x, uint64_t n, uint64_t K, uint64_t* ct, void* scratch,
                     const uint32_t key[8], uint64_t g0, uint32_t* flag, hipStream_t s);
+// encode's large-value path (|x Delta| > 2^61 somewhere in the call; PALISADE's approxFactor): the
+// same ciphertexts' encryption redone with per-ciphertext scale-down exponents (kernels.hip)
+void launch_encrypt_approx(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
+                           uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
+                           uint64_t g0, hipStream_t s);
 size_t encrypt_scratch_bytes(const Params& p, uint64_t K);
 // Decode noise flooding (PALISADE 1.11 Decode); off = exact decode.
 struct DecodeNoise {
