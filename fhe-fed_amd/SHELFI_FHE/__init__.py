@@ -29,7 +29,13 @@ from . import _lib
 from ._lib import ShelfiError, check
 
 __version__ = "0.1.0"
-__all__ = ["Scheme", "CKKS", "ShelfiError", "__version__"]
+__all__ = ["Scheme", "CKKS", "ShelfiError", "__version__", "reload_switches"]
+
+
+def reload_switches() -> None:
+    """Re-read the library's SHELFI_* A/B probe switches from os.environ.  The
+    library reads them when a context is created and here, never on a launch path."""
+    _lib.load().shelfi_reload_switches()
 
 _WIRE_CODES = {"shelfi": 0, "palisade": 1, "packed": 2}  # shelfi_set_wire_format's numbering
 

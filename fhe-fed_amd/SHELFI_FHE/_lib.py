@@ -76,6 +76,7 @@ class PalisadeInfo(C.Structure):
 # name -> (restype, argtypes); every symbol declared in include/shelfi.h
 SIGNATURES = {
     "shelfi_abi_version": (C.c_int, []),
+    "shelfi_reload_switches": (None, []),
     "shelfi_last_error": (C.c_char_p, []),
     "shelfi_free": (None, [C.c_void_p]),
     "shelfi_params_generate": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,

@@ -525,10 +525,53 @@ static int arena_weight_slot(shelfi_ctx* ctx, const float* w, size_t C, hipStrea
   return i;
 }
 
+static Switches g_switches;
+
+static bool env_flag(const char* name, char off_or_on, bool dflt) {
+  const char* e = getenv(name);
+  return e && *e == off_or_on ? !dflt : dflt;
+}
+static int env_choice(const char* name, std::initializer_list<int> allowed, int dflt) {
+  const char* e = getenv(name);
+  if (!e) return dflt;
+  const int v = atoi(e);
+  for (int a : allowed)
+    if (a == v) return v;
+  return dflt;
+}
+
+void reload_switches() {
+  Switches s;
+  s.xcd_order = env_flag("SHELFI_XCD_ORDER", '0', true);
+  s.ntt_wl = env_flag("SHELFI_NTT_WL", '0', true);
+  s.fft_ct = env_flag("SHELFI_FFT_CT", '0', true);
+  s.enc_fused = env_flag("SHELFI_ENC_FUSED_COLS", '0', true);
+  s.enc_pp = env_flag("SHELFI_ENC_PP", '0', true);
+  s.dec_pp = env_flag("SHELFI_DEC_PP", '0', true);
+  s.enc_nored = env_flag("SHELFI_ENC_NORED", '0', true);
+  s.enc_tab = env_flag("SHELFI_ENC_TAB", '0', true);
+  s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
+  s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
+  if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;
+  s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
+  s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);
+  s.wavg_rows = env_choice("SHELFI_WAVG_ROWS", {1, 2}, 0);
+  s.arena_stager = env_choice("SHELFI_ARENA_STAGER", {0, 1}, -1);
+  if (const char* e = getenv("SHELFI_DEV_CHUNK_MIB"))
+    if (atoll(e) > 0) s.dev_chunk_mib = (uint64_t)atoll(e);
+  if (const char* e = getenv("SHELFI_WAVG_CHUNK_MIB"))
+    if (atoll(e) > 0) s.wavg_chunk_mib = (uint64_t)atoll(e);
+  g_switches = s;
+}
+const Switches& switches() { return g_switches; }
+static const bool g_switches_read = (reload_switches(), true);
+
 }  // namespace shelfi
 
 // ============================================================== C ABI ======
 extern "C" {
+
+void shelfi_reload_switches(void) { reload_switches(); }
 
 int shelfi_abi_version(void) { return SHELFI_ABI_VERSION; }
 const char* shelfi_last_error(void) { return g_last_error.c_str(); }
@@ -581,6 +624,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
   *out = nullptr;
   shelfi_ctx* ctx = new (std::nothrow) shelfi_ctx();
   if (!ctx) return SHELFI_ERR_DEVICE;
+  reload_switches();  // the probe switches are read once per context
   int rc = guarded([&] {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -1150,19 +1194,9 @@ static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* c
 
 // Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
 // chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
-// (stream B), with two device buffer sets.  Writes the payload of the result.
-// Zero-copy uploads (SHELFI_H2D_REGISTER=1, A/B probe switch read per call): each learner's
-// upload is page-locked in place for the call (hipHostRegister) and DMA'd straight from it,
-// instead of being copied into the pinned staging ring first.
-struct HostRegistration {
-  std::vector<void*> ptrs;
-  hipStream_t s = nullptr;
-  ~HostRegistration() {
-    if (s) (void)hipStreamSynchronize(s);  // no DMA may still read a buffer being unpinned
-    for (void* p : ptrs) (void)hipHostUnregister(p);
-  }
-};
-
+// (stream B), with two device buffer sets.  Writes the payload of the result.  (Zero-copy uploads
+// registered in place with hipHostRegister measured slower than the staging ring and were removed
+// in round 5: tools/h2d_register_ab.py.)
 static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in,
                                 const float* weights, size_t C, uint64_t K, const CtLayout& dst,
                                 const size_t* lens) {
@@ -1171,9 +1205,8 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   // chunk: ~128 MiB of input per learner-group buffer (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 /
   // 48.2 / 48.7 ms for 16 learners x 64 cts, uint64 blobs; packed wire 54.6 / 46.0 / 42.1 / 42.5 ms,
-  // profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch, read per call)
-  const char* ck_env = getenv("SHELFI_WAVG_CHUNK_MIB");
-  const uint64_t chunk_mib = ck_env && atoll(ck_env) > 0 ? (uint64_t)atoll(ck_env) : 128;
+  // profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
+  const uint64_t chunk_mib = switches().wavg_chunk_mib;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
@@ -1193,20 +1226,6 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
   std::vector<HostPiece> pcs;
-  HostRegistration reg;
-  const char* zc_env = getenv("SHELFI_H2D_REGISTER");
-  bool zc = zc_env && *zc_env == '1';
-  if (zc) {
-    reg.s = pp.a;
-    for (size_t c = 0; c < C && zc; ++c) {
-      if (hipHostRegister(in[c].base, lens[c], hipHostRegisterDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        zc = false;  // not registrable (e.g. already pinned elsewhere): the staging ring
-      } else {
-        reg.ptrs.push_back(in[c].base);
-      }
-    }
-  }
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
   const uint64_t nchunks = (K + kc - 1) / kc;
@@ -1220,15 +1239,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         in[c0 + c].pieces(k0, kn, p, pcs);
         // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked)
         uint8_t* land = pin ? pinb[b] + c * kn * pct : inb[b] + c * kn * ct_bytes;
-        if (zc) {  // DMA straight from the registered upload
-          uint8_t* d = land;
-          for (const HostPiece& pc : pcs) {
-            SHELFI_HIP(hipMemcpyAsync(d, pc.p, pc.n, hipMemcpyHostToDevice, pp.a));
-            d += pc.n;
-          }
-        } else {
-          sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
-        }
+        sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
       }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
@@ -1391,10 +1402,9 @@ int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
 // exact for |X| < 2^127; over a prefix modulus Q' > 2^130 the centred residue of X is X itself
 // and |X| / Q' < 2^-3 keeps k's estimate clear of its rounding boundary, so the towers past the
 // prefix change no output bit.  2^15 / L4 (60 + 3 x 52 bits): 3 of 4 towers.
-// SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe switch, read per call).
+// SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe switch).
 static uint32_t decode_towers(const Params& p, uint32_t towers) {
-  const char* env = getenv("SHELFI_DEC_ALL_TOWERS");
-  if (env && *env == '1') return towers;
+  if (switches().dec_all_towers) return towers;
   uint32_t bits = 0;
   for (uint32_t t = 0; t < towers; ++t) {
     bits += 63 - (uint32_t)__builtin_clzll(p.q[t]);  // q_t >= 2^floor(log2 q_t)
@@ -1651,10 +1661,9 @@ static void arena_place(shelfi_ctx* ctx, size_t K, size_t learner, size_t C, uin
 // hipMemcpyAsync from the caller's pageable memory (54 GB/s for a 1.5 GB upload), the 2 L tower runs
 // of 256 KiB per ciphertext of a PALISADE archive through the bytes API's pinned staging ring (49 vs
 // 18.5 GB/s as separate copies; probes/r03_arena_put.txt).  SHELFI_ARENA_STAGER=0|1 forces one (A/B
-// probe switch, read per call).
+// probe switch).
 static bool arena_use_stager(size_t pieces, size_t bytes) {
-  const char* e = getenv("SHELFI_ARENA_STAGER");
-  if (e && (*e == '0' || *e == '1')) return *e == '1';
+  if (switches().arena_stager >= 0) return switches().arena_stager == 1;
   return pieces > 1 && bytes / pieces < (4u << 20);
 }
 // Host uploads are staged through the scratch in pieces of about 64 MiB.
@@ -1918,10 +1927,9 @@ int shelfi_dev_modq(shelfi_ctx* ctx, uint64_t* buf_dev, size_t K, void* stream) 
 // Ciphertexts per launch chain of the device-resident encrypt/decrypt: as many as a
 // 4 GiB scratch holds (1149 at N = 2^15, L = 4: one chain for a ResNet-18 learner),
 // split into equal chunks, so no launch runs a short tail chunk.
-// SHELFI_DEV_CHUNK_MIB overrides the budget (read per call, for A/B probes).
+// SHELFI_DEV_CHUNK_MIB overrides the budget (A/B probe switch).
 static uint64_t dev_chunk(uint64_t K, size_t scratch_per_ct) {
-  const char* env = getenv("SHELFI_DEV_CHUNK_MIB");
-  const uint64_t mib = env && atoll(env) > 0 ? (uint64_t)atoll(env) : 4096;
+  const uint64_t mib = switches().dev_chunk_mib;
   const uint64_t cap = std::max<uint64_t>(1, (mib << 20) / scratch_per_ct);
   const uint64_t n = (K + cap - 1) / cap;
   return n ? (K + n - 1) / n : 1;

@@ -37,10 +37,9 @@ namespace shelfi {
 
 // Host side of xcd_block: the combo count G when the block passes may deal (tower, block)
 // combos per XCD (G % 8 == 0), else 0.  SHELFI_XCD_ORDER=0 keeps the natural order (A/B
-// probe switch, read per launch).
+// probe switch).
 static uint32_t xcd_combos(uint64_t G) {
-  const char* env = getenv("SHELFI_XCD_ORDER");
-  if (env && *env == '0') return 0;
+  if (!switches().xcd_order) return 0;
   return (G % 8 == 0 && G <= 0xFFFFFFFFull) ? (uint32_t)G : 0;
 }
 
@@ -657,13 +656,10 @@ __global__ __launch_bounds__(256) void ntt_inv_blocks_dec_pp(uint64_t* __restric
   }
 }
 
-// Wave-local exchanges in the persistent block passes (the default since round 4; SHELFI_NTT_WL=0,
-// read per launch, keeps the four-barrier form): bit-identical, decrypt 2-3% and flooded decrypt ~2%
-// faster, encrypt within 1% (profiles/r04r/wl_ab*.txt).
-static bool ntt_wave_local() {
-  const char* env = getenv("SHELFI_NTT_WL");
-  return !(env && *env == '0');
-}
+// Wave-local exchanges in the persistent block passes (the default since round 4; SHELFI_NTT_WL=0
+// keeps the four-barrier form): bit-identical, decrypt 2-3% and flooded decrypt ~2% faster, encrypt
+// within 1% (profiles/r04r/wl_ab*.txt).
+static bool ntt_wave_local() { return switches().ntt_wl; }
 
 // Workgroups of the persistent decrypt / encrypt block passes: LDS-bound residency per CU
 // times the CUs, spread evenly over the (tower, block) combos (at least one each).
@@ -1530,13 +1526,8 @@ static void launch_encode_fft(const Params& p, const DeviceTables& dt, const dou
     const uint64_t nb = K * ((p.batch >> logR) / 256);
     FFT_DISPATCH(logR, fft_inv_cols, dim3((uint32_t)nb), dim3(256), 0, s, x, n, fbuf, logS,
                  dt.fft_inv);
-    const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switches (read per launch)
-    const bool fct = !(fenv && *fenv == '0');
-    const char* zenv = getenv("SHELFI_FFT_SWZ");
-    if (fct && blkLog == 10 && zenv && *zenv == '0')
-      hipLaunchKernelGGL((fft_inv_blocks_ct<10, 3, 3, 2, 2, false>), dim3((uint32_t)(K << logR)), dim3(128), 0, s,
-                         fbuf, logS, dt.fft_inv);
-    else if (fct && blkLog == 10)
+    const bool fct = switches().fft_ct;
+    if (fct && blkLog == 10)
       hipLaunchKernelGGL((fft_inv_blocks_ct<10, 3, 3, 2, 2>), dim3((uint32_t)(K << logR)), dim3(128), 0, s, fbuf,
                          logS, dt.fft_inv);
     else if (fct && blkLog == 11)
@@ -1565,39 +1556,32 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
   const uint32_t nblkLog = ntt_block_log(p.logN);
   const int nlogR = (int)(p.logN - nblkLog);
-  const char* env = getenv("SHELFI_ENC_FUSED_COLS");  // A/B probe switch (read per launch)
-  const bool fused = (nlogR == 3 || nlogR == 4) && dt.enc_tab && !(env && *env == '0');
+  const Switches& sw = switches();
+  const bool fused = (nlogR == 3 || nlogR == 4) && dt.enc_tab && sw.enc_fused;
   int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
   int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
   // NORED towers (fwd_set_ct): q < kNoRedQ, run unreduced through both passes — only with the
   // persistent blocks pass, and only as a suffix of the chain (q_0 the 60-bit tower, the rest
   // near 2^scale_bits); t_split = L turns it off
-  const char* ppenv = getenv("SHELFI_ENC_PP");  // A/B probe switch (read per launch)
-  const bool pp = fused && nblkLog == 11 && dt.red_ok && !(ppenv && *ppenv == '0');
+  const bool pp = fused && nblkLog == 11 && dt.red_ok && sw.enc_pp;
   uint32_t t_split = 0;
   while (t_split < p.L && p.q[t_split] >= kNoRedQ) ++t_split;
   for (uint32_t t = t_split; t < p.L; ++t)
     if (p.q[t] >= kNoRedQ) t_split = p.L;
-  const char* nrenv = getenv("SHELFI_ENC_NORED");  // A/B probe switch (read per launch)
-  if (!pp || (nrenv && *nrenv == '0')) t_split = p.L;
+  if (!pp || !sw.enc_nored) t_split = p.L;
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
     const uint64_t nb = (K << (p.logN - nlogR)) / 256;
-    const char* tabenv = getenv("SHELFI_ENC_TAB");  // A/B probe switch (read per launch)
-    const bool tab = !(tabenv && *tabenv == '0');
-    // LDS column twiddles at 3 waves/SIMD (no SGPR / VGPR spills): enc_cols_fused 578 -> 534 us per
-    // 714 cts (probes/r03_enc_cols_twl.txt); SHELFI_ENC_TWL=0 keeps the scalar-loaded twiddles
-    const char* twlenv = getenv("SHELFI_ENC_TWL");  // A/B probe switch (read per launch)
-    const bool twl = !(twlenv && *twlenv == '0');
+    const bool tab = sw.enc_tab;
+    // LDS column twiddles at 3 waves/SIMD with the tables (no SGPR / VGPR spills): enc_cols_fused 578 ->
+    // 534 us per 714 cts (probes/r03_enc_cols_twl.txt; the scalar-loaded form was removed in round 5)
 #define ENC_COLS(LR, TB, ...)                                                                                   \
   hipLaunchKernelGGL((enc_cols_fused<LR, TB, ##__VA_ARGS__>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, K, p.logN, logS, p.L, \
                      p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh, pbuf, flag, t_split,  \
                      dt.enc_tab)
     // small calls (K <= kEncTsMaxK at 4 towers): one wave per tower (TS), so a call of a few
     // ciphertexts spreads over 4x the waves; SHELFI_ENC_TS=0 / 1 forces either (A/B switch)
-    const char* tsenv = getenv("SHELFI_ENC_TS");
-    const bool ts = nlogR == 4 && tab && twl && p.L == 4 &&
-                    (tsenv ? *tsenv == '1' : K <= kEncTsMaxK);
+    const bool ts = nlogR == 4 && tab && p.L == 4 && (sw.enc_ts >= 0 ? sw.enc_ts == 1 : K <= kEncTsMaxK);
     if (ts)
       hipLaunchKernelGGL((enc_cols_fused<4, true, 3, true, true>), dim3((uint32_t)(nb * 4)), dim3(256), 0, s, fbuf, K,
                          p.logN, logS, p.L, p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh,
@@ -1606,10 +1590,8 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       ENC_COLS(3, true);
     else if (nlogR == 3)
       ENC_COLS(3, false);
-    else if (tab && twl)  // 164 VGPRs without spills at 3 waves (4 would spill 36)
+    else if (tab)  // 164 VGPRs without spills at 3 waves (4 would spill 36)
       ENC_COLS(4, true, 3, true);
-    else if (tab)
-      ENC_COLS(4, true);
     else
       ENC_COLS(4, false);
 #undef ENC_COLS
@@ -2434,8 +2416,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
     const uint32_t xg = xcd_combos(p.L << (logR > 0 ? logR : 0));
-    const char* ppenv = getenv("SHELFI_DEC_PP");  // A/B probe switch (read per launch)
-    const bool pp = logR > 0 && blkLog == 11 && dt.red_ok && !(ppenv && *ppenv == '0');
+    const bool pp = logR > 0 && blkLog == 11 && dt.red_ok && switches().dec_pp;
     if (pp) {
       const uint32_t ncombo = p.L << logR;
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
@@ -2493,8 +2474,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     fa.g0 = dn->g0;
     fa.flags = dn->flags;
     fa.logN = p.logN;
-    const char* env = getenv("SHELFI_FLOOD_OLD");  // A/B probe switch (read per launch)
-    fused_flood = p.batch >= 64 && !(env && *env == '1');
+    fused_flood = p.batch >= 64;  // decode_flood_kernel below 2^6 slots
     if (fused_flood) {
       fa.G = flood_groups(p.batch);
       double2* part = fbuf + K * (uint64_t)p.batch;
@@ -2508,18 +2488,9 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     }
     SHELFI_HIP(hipGetLastError());
   }
-  const char* fenv = getenv("SHELFI_FFT_CT");  // A/B probe switch (read per launch)
-  const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && !(fenv && *fenv == '0');
+  const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && switches().fft_ct;
   const dim3 fg((uint32_t)(K << flogR));
-  const char* zenv = getenv("SHELFI_FFT_SWZ");
-  const bool noswz = zenv && *zenv == '0';
-  if (fct && fblkLog == 10 && noswz && fused_flood)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd,
-                       fa);
-  else if (fct && fblkLog == 10 && noswz)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false, false>), fg, dim3(128), 0, s, fbuf, logS,
-                       dt.fft_fwd, fa);
-  else if (fct && fblkLog == 10 && fused_flood)
+  if (fct && fblkLog == 10 && fused_flood)
     hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
   else if (fct && fblkLog == 10)
     hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);

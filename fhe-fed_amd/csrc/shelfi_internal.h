@@ -55,6 +55,30 @@ inline uint32_t ntt_block_log(uint32_t logN) {
   return logN < b ? logN : b;
 }
 
+// A/B probe switches (none changes an output bit), read from the environment
+// when a context is created and by shelfi_reload_switches() -- never on a launch path.
+struct Switches {
+  bool xcd_order = true;       // SHELFI_XCD_ORDER=0: natural block order in the NTT block passes
+  bool ntt_wl = true;          // SHELFI_NTT_WL=0: a workgroup barrier at every block-pass exchange
+  bool fft_ct = true;          // SHELFI_FFT_CT=0: LDS-loop FFT block passes
+  bool enc_fused = true;       // SHELFI_ENC_FUSED_COLS=0: enc_prep_kernel + three column passes
+  bool enc_pp = true;          // SHELFI_ENC_PP=0: one-shot encrypt block pass
+  bool dec_pp = true;          // SHELFI_DEC_PP=0: one-shot decrypt block pass
+  bool enc_nored = true;       // SHELFI_ENC_NORED=0: reductions in every tower
+  bool enc_tab = true;         // SHELFI_ENC_TAB=0: butterflies for v's / e1's first column stages
+  int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
+  bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
+  int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
+  int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
+  int pack_waves = 0;          // SHELFI_PACK_WAVES=2|8 (0: 4 rows per block)
+  int wavg_rows = 0;           // SHELFI_WAVG_ROWS=1|2 (0: by shape)
+  int arena_stager = -1;       // SHELFI_ARENA_STAGER=0|1 (-1: by upload shape)
+  uint64_t dev_chunk_mib = 4096;  // SHELFI_DEV_CHUNK_MIB: device encrypt / decrypt scratch per chain
+  uint64_t wavg_chunk_mib = 128;  // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
+};
+const Switches& switches();
+void reload_switches();
+
 struct Params {
   uint32_t N = 0, logN = 0, L = 0, batch = 0, gap = 0, scale_bits = 0, first_mod_bits = 0;
   uint64_t q[kMaxTowers] = {0};

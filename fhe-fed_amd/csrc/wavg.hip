@@ -46,7 +46,7 @@ __device__ __forceinline__ uint64_t wavg_fold(uint64_t s00, uint64_t s01, uint64
 // R rows per block (R = 2 for C <= 8 learners): with few learners one 512-residue row gives
 // a thread only C 16-byte loads in flight; two adjacent rows (same tower: N / 512 is even)
 // double that.
-// UNR learners' loads in flight per thread (8 / R by default; SHELFI_WAVG_UNROLL=16 for an A/B).
+// UNR learners' loads in flight per thread (8 / R; all 16 in flight measured no faster, round 4).
 template <bool CHECK = false, int R = 1, int UNR = 8 / R>
 __global__ __launch_bounds__(kWavgThreads) void wavg_kernel(WavgArgs a,
                                                             const TowerConst* __restrict__ tcs) {
@@ -317,67 +317,42 @@ constexpr int kPackedWaves = 4;  // waves per block, one row each
 
 // crow: the learner count of the input's row layout (C for an arena, 1 for stacked C = 1 batches
 // lstride dwords apart); out (uint64) or, with PO, pout (packed, C = 1 layout) receives the result.
-// SP = 2 (small launches): two waves per row, each summing half of the learners; the second hands its
-// 8 residues per lane to the first through LDS, which adds them and stores -- twice the waves (and
-// bytes in flight) for a grid too small to fill the chip, one extra fold per row.
-template <int UR, int WV = kPackedWaves, bool PO = false, bool STK = false, int SP = 1>
+// (Round 4 also measured two waves per row for small launches and an XCD-contiguous block order:
+// within +-1% and 8% slower; both were removed in round 5.)
+template <int UR, int WV = kPackedWaves, bool PO = false, bool STK = false>
 __global__ __launch_bounds__(64 * WV) void wavg_packed(const uint32_t* __restrict__ arena,
                                                       const uint32_t* __restrict__ wl, uint32_t C, uint32_t crow,
                                                       uint64_t lstride, uint64_t rows, uint32_t L, uint32_t logN,
                                                       ArenaPack ap, const TowerConst* __restrict__ tcs,
-                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pout,
-                                                      uint32_t xcd) {
-  static_assert(SP == 1 || (SP == 2 && !PO && WV % 2 == 0), "row split");
+                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pout) {
   // the running sum of the rows' residues across learner groups (C > 16): 8 x 64 per wave
   __shared__ uint64_t run_lds[WV][8 * 64];
-  __shared__ uint64_t xch_lds[SP == 2 ? WV / 2 : 1][SP == 2 ? 8 * 64 : 1];
-  // xcd: consecutive blocks land on the 8 XCDs in turn; remap so each XCD walks one contiguous
-  // eighth of the rows (probe switch SHELFI_PACK_XCD; needs gridDim.x % 8 == 0)
-  const uint32_t b = xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t part = SP == 2 ? (wave & 1u) : 0u, slot = wave / SP;
-  const uint64_t r = (uint64_t)b * (WV / SP) + slot;
-  const bool valid = r < rows;
-  if (SP == 1 && !valid) return;  // (SP == 2: every wave reaches the exchange barrier)
+  const uint64_t r = (uint64_t)blockIdx.x * WV + wave;
+  if (r >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   uint64_t x[8];
-  uint64_t q = 0;
-  if (valid) {
-    const PackedRow pr = packed_row(r, crow, L, logN, ap);
-    const TowerConst c = tcs[pr.t];
-    q = c.q;
-    const uint32_t* __restrict__ sl = arena + pr.base;
-    const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
-    const uint32_t half = (C + 1) / 2;
-    const uint32_t kbeg = SP == 2 ? part * half : 0u, kend = SP == 2 ? min(C, (part + 1) * half) : C;
-    uint32_t* __restrict__ po = PO ? pout + packed_row(r, 1, L, logN, ap).base : nullptr;
-    switch (pr.U) {
-#define WPR(UU)                                                                                     \
-  case UU:                                                                                          \
-    wavg_packed_row<UU, UR, STK>(sl, kbeg, kend, lstride, wlt, 2 * L, c, lane, run_lds[wave], x);   \
-    if (PO) {                                                                                       \
-      uint32_t pw[PackShape<UU>::D], pf;                                                            \
-      pk_pack<UU>(x, pw, pf);                                                                       \
-      pk_store<UU>(po, lane, pw, pf);                                                               \
-    }                                                                                               \
+  const PackedRow pr = packed_row(r, crow, L, logN, ap);
+  const TowerConst c = tcs[pr.t];
+  const uint32_t* __restrict__ sl = arena + pr.base;
+  const uint32_t* __restrict__ wlt = wl + 2 * pr.t;
+  uint32_t* __restrict__ po = PO ? pout + packed_row(r, 1, L, logN, ap).base : nullptr;
+  switch (pr.U) {
+#define WPR(UU)                                                                               \
+  case UU:                                                                                    \
+    wavg_packed_row<UU, UR, STK>(sl, 0u, C, lstride, wlt, 2 * L, c, lane, run_lds[wave], x);  \
+    if (PO) {                                                                                 \
+      uint32_t pw[PackShape<UU>::D], pf;                                                      \
+      pk_pack<UU>(x, pw, pf);                                                                 \
+      pk_store<UU>(po, lane, pw, pf);                                                         \
+    }                                                                                         \
     break;
-      SHELFI_PACK_WIDTHS(WPR)
+    SHELFI_PACK_WIDTHS(WPR)
 #undef WPR
-      default:
+    default:
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = 0;
-        break;
-    }
-    if (SP == 2 && part == 1) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xch_lds[slot][64 * j + lane] = x[j];
-    }
-  }
-  if (SP == 2) {
-    __syncthreads();  // every wave of the block, valid or not: the one barrier of the kernel
-    if (!valid || part == 1) return;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = addmod(x[j], xch_lds[slot][64 * j + lane], q);
+      for (int j = 0; j < 8; ++j) x[j] = 0;
+      break;
   }
   if (!PO) store_row_u64(out + r * kArenaChunk, lane, x);
 }
@@ -429,11 +404,8 @@ __global__ __launch_bounds__(64 * WV) void wavg_packed_r3(const uint32_t* __rest
                                                       const uint32_t* __restrict__ wl, uint32_t C,
                                                       uint64_t rows, uint32_t L, uint32_t logN, ArenaPack ap,
                                                       const TowerConst* __restrict__ tcs,
-                                                      uint64_t* __restrict__ out, uint32_t xcd) {
-  // xcd: consecutive blocks land on the 8 XCDs in turn; remap so each XCD walks one contiguous
-  // eighth of the rows (probe switch SHELFI_PACK_XCD; needs gridDim.x % 8 == 0)
-  const uint32_t b = xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const uint64_t r = (uint64_t)b * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+                                                      uint64_t* __restrict__ out) {
+  const uint64_t r = (uint64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (r >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   const PackedRow pr = packed_row(r, C, L, logN, ap);
@@ -514,33 +486,27 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   if (!nrows) return;
   if (nrows > 0xFFFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
   const bool po = pout != nullptr, stk = lstride != 0;
-  // A/B probe switches, read per launch (profiles/probes/r03_wavg_packed_ab.txt,
-  // profiles/r04a/probes/): learners unrolled per iteration SHELFI_PACK_UNROLL=1|2|4(|8), waves (rows)
-  // per block SHELFI_PACK_WAVES=2|4|8, XCD-contiguous block order SHELFI_PACK_XCD=1, the round-4
-  // three-accumulator kernel SHELFI_PACK_KERNEL=v4 (the packed-output and stacked forms always use
-  // it) and its two-waves-per-row form SHELFI_PACK_SPLIT=2.  Without switches the launch picks by
-  // shape from the same-process A/Bs (profiles/r04a/probes/wavg_kernel_ab.txt, r04d/): see auto_v4.
-  const char* kenv = getenv("SHELFI_PACK_KERNEL");
-  const char* env = getenv("SHELFI_PACK_UNROLL");
-  const char* wenv = getenv("SHELFI_PACK_WAVES");
-  const int wv = wenv ? atoi(wenv) : kPackedWaves;
-  const char* xenv = getenv("SHELFI_PACK_XCD");
-  const char* senv = getenv("SHELFI_PACK_SPLIT");
-  const int u = env ? atoi(env) : (!kenv && !wenv && C == 16 && nrows >= 16384 ? 8 : 2);
-  const bool split = senv && *senv == '2' && !po && !stk;
+  // A/B probe switches (Switches; profiles/probes/r03_wavg_packed_ab.txt, profiles/r04a/probes/):
+  // learners unrolled per iteration SHELFI_PACK_UNROLL=1|2|4|8, waves (rows) per block
+  // SHELFI_PACK_WAVES=2|8, the kernel SHELFI_PACK_KERNEL=r3|v4 (the packed-output and stacked forms
+  // always use v4).  Without switches the launch picks by shape from the same-process A/Bs
+  // (profiles/r04a/probes/wavg_kernel_ab.txt, r04d/): see auto_v4.
+  const Switches& sw = switches();
+  const bool forced = sw.pack_kernel || sw.pack_unroll || sw.pack_waves;
+  const int wv = sw.pack_waves ? sw.pack_waves : kPackedWaves;
+  const int u = sw.pack_unroll ? sw.pack_unroll : (!forced && C == 16 && nrows >= 16384 ? 8 : 2);
   // default: v4 with 8 learners in flight for 16-learner arenas of >= 16384 rows (cfg3's per-GPU
   // shard, cfg4: +0.6-1.4% over r3 in the same-process A/B), round 3's kernel otherwise (cfg5's 8,
   // the cts-sharded 128 learners, and small grids, where it leads by 1-4%)
-  const bool auto_v4 = !kenv && !env && !wenv && C == 16 && nrows >= 16384;
-  const bool v4 = po || stk || split || auto_v4 || (kenv && kenv[0] == 'v' && kenv[1] == '4');
+  const bool auto_v4 = !forced && C == 16 && nrows >= 16384;
+  const bool v4 = po || stk || auto_v4 || sw.pack_kernel == 4;
   const int wvs = (wv == 2 || wv == 8) && u == 2 && !po && !stk ? wv : kPackedWaves;
   if (!v4) {
     const uint64_t blocks = (nrows + wvs - 1) / wvs;
     if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-    const uint32_t xcd = xenv && *xenv == '1' && blocks % 8 == 0 ? 1u : 0u;
 #define WPK3(UU, WW)                                                                                         \
   hipLaunchKernelGGL((wavg_packed_r3<UU, WW>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s, in, wl_dev, C, nrows, \
-                     L, logN, ap, tc, out, xcd)
+                     L, logN, ap, tc, out)
     if (wvs == 2)
       WPK3(2, 2);
     else if (wvs == 8)
@@ -555,18 +521,12 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
     SHELFI_HIP(hipGetLastError());
     return;
   }
-  const uint64_t rows_per_block = split ? kPackedWaves / 2 : wvs;
-  const uint64_t blocks = (nrows + rows_per_block - 1) / rows_per_block;
+  const uint64_t blocks = (nrows + wvs - 1) / wvs;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
-  const uint32_t xcd = xenv && *xenv == '1' && blocks % 8 == 0 ? 1u : 0u;
 #define WPK(UU, WW, PO, STK)                                                                                 \
   hipLaunchKernelGGL((wavg_packed<UU, WW, PO, STK>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s, in, wl_dev,  \
-                     C, crow, lstride, nrows, L, logN, ap, tc, out, pout, xcd)
-  if (split)
-    hipLaunchKernelGGL((wavg_packed<2, kPackedWaves, false, false, 2>), dim3((uint32_t)blocks),
-                       dim3(64 * kPackedWaves), 0, s, in, wl_dev, C, crow, lstride, nrows, L, logN, ap, tc, out,
-                       pout, xcd);
-  else if (stk && po)
+                     C, crow, lstride, nrows, L, logN, ap, tc, out, pout)
+  if (stk && po)
     throw Error{SHELFI_ERR_ARG, "stacked inputs with a packed output"};
   else if (stk)
     WPK(2, 4, false, true);
@@ -675,18 +635,11 @@ void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t lo
 
 // Rows per wavg block: with C <= 8 learners a one-row thread has only C 16-byte loads in
 // flight; the kernel then takes 2 rows.  Measured in one process per shape (tools/wavg_rows_ab.py,
-// profiles/probes/r03_wavg_rows_ab.txt).  SHELFI_WAVG_ROWS=1|2 forces one (A/B probe switch, read
-// per launch).
+// profiles/probes/r03_wavg_rows_ab.txt).  SHELFI_WAVG_ROWS=1|2 forces one (A/B probe switch).
 static int wavg_rows(uint32_t C, uint64_t rows) {
-  const char* env = getenv("SHELFI_WAVG_ROWS");
-  if (env && (*env == '1' || *env == '2')) return *env - '0';
+  if (switches().wavg_rows) return switches().wavg_rows;
   if (C <= 8) return 2;
   return C >= 16 && rows >= 16384 ? 2 : 1;
-}
-
-static int wavg_unroll() {
-  const char* env = getenv("SHELFI_WAVG_UNROLL");
-  return env && atoi(env) == 16 ? 16 : 8;
 }
 
 void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
@@ -704,8 +657,6 @@ void launch_wavg(const WavgArgs& a, const TowerConst* tc, hipStream_t s) {
     hipLaunchKernelGGL((wavg_kernel<true, 1>), g, b, 0, s, a, tc);
   else if (R == 2)
     hipLaunchKernelGGL((wavg_kernel<false, 2>), g, b, 0, s, a, tc);
-  else if (wavg_unroll() == 16)
-    hipLaunchKernelGGL((wavg_kernel<false, 1, 16>), g, b, 0, s, a, tc);
   else
     hipLaunchKernelGGL((wavg_kernel<false, 1>), g, b, 0, s, a, tc);
   SHELFI_HIP(hipGetLastError());

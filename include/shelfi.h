@@ -55,6 +55,9 @@ typedef struct shelfi_info {
 
 /* ---- library ------------------------------------------------------------ */
 int shelfi_abi_version(void);
+/* Re-read the SHELFI_* A/B probe switches from the environment.  They are read
+ * when a context is created and here, never by a launch; call between calls, not during one. */
+void shelfi_reload_switches(void);
 const char* shelfi_last_error(void);
 void shelfi_free(void* p);
 

@@ -24,6 +24,30 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: large-size property tests")
 
 
+def set_switch(monkeypatch, var, val):
+    """An A/B probe switch for the rest of the test: the environment variable, then the library's
+    re-read (switches are never read on a launch path).  val None removes it."""
+    if val is None:
+        monkeypatch.delenv(var, raising=False)
+    else:
+        monkeypatch.setenv(var, val)
+    import SHELFI_FHE
+
+    SHELFI_FHE.reload_switches()
+
+
+@pytest.fixture(autouse=True)
+def _switches_restored():
+    """After each test (and after monkeypatch has restored the environment): the library's switches
+    re-read, so a test's probe switch never leaks into the next one."""
+    yield
+    if "SHELFI_FHE" in sys.modules:
+        try:
+            sys.modules["SHELFI_FHE"].reload_switches()
+        except (OSError, AttributeError):
+            pass
+
+
 @pytest.fixture(scope="session")
 def palisade_keys():
     import palisade_fixture as P

@@ -1,5 +1,5 @@
 """§8(f3) on the HIP path: decode noise flooding (decode_stats_kernel + the noise fused into
-the first FFT pass; decode_flood_kernel for tiny batches and SHELFI_FLOOD_OLD=1) against the
+the first FFT pass; decode_flood_kernel for batches below 2^6 slots) against the
 oracle's restatement with the same seeded noise stream.  Tolerance 1e-14 absolute:
 the noise (~1e-13) is generated with GPU vs glibc log/sincos (ulp-level differences)
 and sigma is a tree vs sequential sum; everything else is the exact decode."""
@@ -39,6 +39,15 @@ def ck2(tmp_path_factory):
 
 
 @pytest.fixture(scope="module")
+def ck_tiny(tmp_path_factory):
+    """2^11 ring, 32 slots: below 2^6 slots the per-ciphertext decode_flood_kernel floods."""
+    d = str(tmp_path_factory.mktemp("keys_noise_tiny")) + os.sep
+    ck = m.CKKS("ckks", 32, 52, d, ringDim=2048, seed=6, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    return ck
+
+
+@pytest.fixture(scope="module")
 def ck_small(tmp_path_factory):
     """2^11 ring, 128 slots (gap 8): one stats workgroup per ciphertext, single FFT pass."""
     d = str(tmp_path_factory.mktemp("keys_noise_small")) + os.sep
@@ -47,13 +56,11 @@ def ck_small(tmp_path_factory):
     return ck
 
 
-@pytest.mark.parametrize("kernel", ["fused", "old"])
-@pytest.mark.parametrize("which", ["ck1", "ck2", "ck_small"])
-def test_flooded_decrypt_matches_oracle(which, kernel, request, monkeypatch):
-    """decode_stats_kernel + fft_fwd_blocks<true> (noise fused into the FFT load, the default)
-    and decode_flood_kernel
-    (SHELFI_FLOOD_OLD=1) against the oracle."""
-    monkeypatch.setenv("SHELFI_FLOOD_OLD", "1" if kernel == "old" else "0")
+@pytest.mark.parametrize("which", ["ck1", "ck2", "ck_small", "ck_tiny"])
+def test_flooded_decrypt_matches_oracle(which, request):
+    """decode_stats_kernel + fft_fwd_blocks<true> (noise fused into the FFT load) against the
+    oracle; ck_tiny (32 slots) takes decode_flood_kernel, the per-ciphertext form that serves rings
+    below 2^6 slots (no longer selectable elsewhere since round 5)."""
     ck = request.getfixturevalue(which)
     q, psi, N, S, delta = _arrays(ck)
     n = 2 * S + 33

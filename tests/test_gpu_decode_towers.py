@@ -29,10 +29,12 @@ def _both(fn):
     """fn() with the trimmed decode, then with every tower."""
     a = fn()
     os.environ["SHELFI_DEC_ALL_TOWERS"] = "1"
+    m.reload_switches()
     try:
         b = fn()
     finally:
         del os.environ["SHELFI_DEC_ALL_TOWERS"]
+        m.reload_switches()
     return a, b
 
 

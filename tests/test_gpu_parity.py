@@ -13,7 +13,7 @@ import pytest
 import oracle as O
 import arena_layout as AL
 import palisade_fixture as P
-from conftest import PALISADE_DIR
+from conftest import PALISADE_DIR, set_switch
 
 pytestmark = pytest.mark.gpu
 
@@ -206,27 +206,26 @@ def test_wavg_arena_packed_widths(tmp_path, monkeypatch, scale, first, depth, C,
     w = list(rng.uniform(-1, 1, C))
     ref = O.wavg(cts, w, q, delta)
     for unroll in ("1", "2", "4", "8"):
-        monkeypatch.setenv("SHELFI_PACK_UNROLL", unroll)
+        set_switch(monkeypatch, "SHELFI_PACK_UNROLL", unroll)
         got = ar.wavg(w)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), unroll
-    monkeypatch.setenv("SHELFI_PACK_KERNEL", "v4")
+    set_switch(monkeypatch, "SHELFI_PACK_KERNEL", "v4")
     for unroll in ("1", "2", "4", "8"):
-        monkeypatch.setenv("SHELFI_PACK_UNROLL", unroll)
+        set_switch(monkeypatch, "SHELFI_PACK_UNROLL", unroll)
         got = ar.wavg(w)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), ("v4", unroll)
-    monkeypatch.delenv("SHELFI_PACK_KERNEL")
-    monkeypatch.delenv("SHELFI_PACK_UNROLL")
-    # the probe switches: rows per block, XCD-contiguous block order, two waves per row (learners
-    # split), the round-4 three-accumulator kernel (also under every unroll depth)
-    for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_XCD", "1"),
-                     ("SHELFI_PACK_SPLIT", "2"), ("SHELFI_PACK_KERNEL", "v4")):
-        monkeypatch.setenv(env, val)
+    set_switch(monkeypatch, "SHELFI_PACK_KERNEL", None)
+    set_switch(monkeypatch, "SHELFI_PACK_UNROLL", None)
+    # the probe switches: rows per block, round 3's and round 4's kernels
+    for env, val in (("SHELFI_PACK_WAVES", "2"), ("SHELFI_PACK_WAVES", "8"), ("SHELFI_PACK_KERNEL", "r3"),
+                     ("SHELFI_PACK_KERNEL", "v4")):
+        set_switch(monkeypatch, env, val)
         got = ar.wavg(w)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), (env, val)
-        monkeypatch.delenv(env)
+        set_switch(monkeypatch, env, None)
     if K > 1:
         got = ar.wavg(w, k0=1, k1=K)
         torch.cuda.synchronize()

@@ -1,7 +1,8 @@
 """Every A/B switch on the device encrypt / decrypt / aggregation paths selects between two
 implementations of the same arithmetic ("None changes an output bit"): under
 each switch the seeded encryptions, the exact decode and the aggregate are bit-identical to the
-default path's.  The switches are read per launch or per call, so one process flips them.
+default path's.  The switches are read when a context is created or on shelfi_reload_switches() (never
+on a launch path); conftest.set_switch sets one and re-reads them, so one process flips them.
 
 Encrypt-side switches are checked at both ring shapes the kernels dispatch on (2^15 / L4: NORED
 towers and fused columns; 2^16 / L6: 60-bit towers, the generic columns) with an odd K so the
@@ -11,6 +12,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import set_switch
+
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
@@ -19,20 +22,18 @@ from SHELFI_FHE import device as D  # noqa: E402
 
 ENC_DEC_SWITCHES = [
     ("SHELFI_NTT_WL", "0"),          # workgroup barrier at every block-pass exchange
-    ("SHELFI_FFT_SWZ", "0"),         # plain LDS index in the FFT block passes
     ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
     ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
     ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
     ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
     ("SHELFI_ENC_TAB", "0"),         # butterflies instead of the small-polynomial tables
-    ("SHELFI_ENC_TWL", "0"),         # scalar-loaded column twiddles
     ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
     ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
     ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
     ("SHELFI_ENC_TS", "0"),          # one column per thread over every tower (K = 7 defaults to one wave per tower)
 ]
-WAVG_SWITCHES = [("SHELFI_WAVG_ROWS", "1"), ("SHELFI_WAVG_ROWS", "2"), ("SHELFI_WAVG_UNROLL", "16")]
+WAVG_SWITCHES = [("SHELFI_WAVG_ROWS", "1"), ("SHELFI_WAVG_ROWS", "2")]
 SEED = 2024
 
 
@@ -57,7 +58,7 @@ def ctx(request, tmp_path_factory):
 @pytest.mark.parametrize("var,val", ENC_DEC_SWITCHES, ids=lambda v: str(v))
 def test_encrypt_decrypt_switch_bitexact(ctx, monkeypatch, var, val):
     ck, x, ct_ref, dec_ref = ctx
-    monkeypatch.setenv(var, val)
+    set_switch(monkeypatch, var, val)
     ck.set_seed(SEED)
     ct = D.encrypt(ck, x)
     dec = D.decrypt(ck, ct_ref, x.numel(), ck.info()["delta"])
@@ -81,7 +82,7 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
         cts.append(a)
     w = list(np.random.default_rng(C).dirichlet(np.ones(C)))
     ref = D.wavg(ck, cts, w)
-    monkeypatch.setenv(var, val)
+    set_switch(monkeypatch, var, val)
     got = D.wavg(ck, cts, w)
     torch.cuda.synchronize()
     assert torch.equal(got, ref), var
@@ -99,8 +100,9 @@ def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire):
         blobs = [ck.encrypt(xs * (i + 1) / 4) for i in range(3)]
         w = [0.5, 0.25, 0.25]
         ref = ck.computeWeightedAverage(blobs, w)
-        monkeypatch.setenv("SHELFI_WAVG_CHUNK_MIB", "1")
+        set_switch(monkeypatch, "SHELFI_WAVG_CHUNK_MIB", "1")
         got = ck.computeWeightedAverage(blobs, w)
     finally:
-        ck.set_wire_format("shelfi")
+        ck.set_wire_format("palisade")
     assert got == ref
+

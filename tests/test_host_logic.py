@@ -509,3 +509,30 @@ def test_c_abi_packed_combine_layout_gloo(world, pieces, K, C_):
     pytest.importorskip("torch")
     res = _spawn_world(world, _gloo_c_abi_packed_worker, pieces, K=K, C_=C_)
     assert res == [(r, True) for r in range(world)]
+
+
+def test_no_getenv_on_a_launch_path():
+    """VERDICT r4 item 9: the A/B probe switches are read into shelfi::Switches when a context is
+    created or on shelfi_reload_switches(), never by a launch.  The only getenv calls left are that
+    reader, the staging pool's construction (host_stage.cpp, per context), the RCCL library path at
+    dlopen (comm.cpp) and the process-wide NTT block size (shelfi_internal.h, read once)."""
+    import re
+
+    csrc = os.path.join(ROOT, "fhe-fed_amd", "csrc")
+    allowed = {"api.cpp": {"env_flag", "env_choice", "reload_switches"}, "host_stage.cpp": None,
+               "comm.cpp": None, "shelfi_internal.h": None}
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".cpp", ".hip", ".h")):
+            continue
+        src = open(os.path.join(csrc, name)).read()
+        hits = [m_.start() for m_ in re.finditer(r"\bgetenv\s*\(", src)]
+        if not hits:
+            continue
+        assert name in allowed, "%s calls getenv" % name
+        if allowed[name] is None:
+            continue
+        for h in hits:  # the enclosing function: the last definition header before the call
+            head = re.findall(r"\n(?:static |const )?[\w:<>&* ]+?\b(\w+)\([^;{]*\)\s*\{", src[:h])
+            assert head and head[-1] in allowed[name], (name, head[-1:] if head else None)
+    for name in ("kernels.hip", "wavg.hip", "keyswitch.hip", "eval.cpp"):
+        assert "getenv" not in open(os.path.join(csrc, name)).read(), name
