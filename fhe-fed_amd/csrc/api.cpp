@@ -163,6 +163,7 @@ static void free_tables(shelfi_ctx* ctx) {
   dfree_t(ctx->dt.fft_fwd);
   dfree_t(ctx->dt.cdt);
   dfree_t(ctx->dt.enc_tab);
+  dfree_t(ctx->dt.enc_vtab);
 }
 
 static void free_keys(shelfi_ctx* ctx) {
@@ -336,6 +337,51 @@ static void build_tables(shelfi_ctx* ctx) {
       }
     }
     ctx->dt.enc_tab = upload(et.data(), et.size());
+  }
+  // NTT(v)'s 4 column stages as table sums (DeviceTables::enc_vtab): the stages' 16 x 16 matrix M_t
+  // (row r' of the output from input row r, the columns pass's twiddles psi_rev[m + i] at stage
+  // s = log2 m) applied to the ternary rows of each group g = {g, g + 4, g + 8, g + 12}
+  if (p.logN >= 15 && p.logN - ntt_block_log(p.logN) == 4) {
+    constexpr int R = 16;
+    std::vector<uint64_t> vt((size_t)p.L * R * 4 * 81);
+    for (uint32_t t = 0; t < p.L; ++t) {
+      const uint64_t q = p.q[t];
+      const auto mul = [q](uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % q); };
+      const auto add = [q](uint64_t a, uint64_t b) { return (uint64_t)(((u128)a + b) % q); };
+      const auto sub = [q](uint64_t a, uint64_t b) { return a >= b ? a - b : a + q - b; };
+      // psi_rev[m + i] = psi^bitrev_logN(m + i)
+      const auto tw = [&](uint32_t idx) { return powmod(p.psi[t], bitrev_host(idx, p.logN), q); };
+      uint64_t M[R][R];  // M[r'][r]
+      for (int r = 0; r < R; ++r) {
+        uint64_t x[R] = {0};
+        x[r] = 1;
+        for (int s = 0; s < 4; ++s) {
+          const int m = 1 << s, tr = R >> (s + 1);
+          for (int i = 0; i < m; ++i) {
+            const uint64_t W = tw((uint32_t)(m + i));
+            for (int jj = 0; jj < tr; ++jj) {
+              const int r0 = 2 * i * tr + jj, r1 = r0 + tr;
+              const uint64_t a = x[r0], b = mul(W, x[r1]);
+              x[r0] = add(a, b);
+              x[r1] = sub(a, b);
+            }
+          }
+        }
+        for (int rp = 0; rp < R; ++rp) M[rp][r] = x[rp];
+      }
+      for (int rp = 0; rp < R; ++rp)
+        for (int g = 0; g < 4; ++g)
+          for (int idx = 0; idx < 81; ++idx) {
+            uint64_t acc = 0;
+            for (int kk = 0, d = idx; kk < 4; ++kk, d /= 3) {
+              const int trit = d % 3 - 1;
+              const uint64_t e = M[rp][g + 4 * kk];
+              acc = trit > 0 ? add(acc, e) : trit < 0 ? sub(acc, e) : acc;
+            }
+            vt[(((size_t)t * R + rp) * 4 + g) * 81 + idx] = acc;
+          }
+    }
+    ctx->dt.enc_vtab = upload(vt.data(), vt.size());
   }
   ctx->params_id = compute_params_id(p);
 }
@@ -550,6 +596,7 @@ void reload_switches() {
   s.dec_pp = env_flag("SHELFI_DEC_PP", '0', true);
   s.enc_nored = env_flag("SHELFI_ENC_NORED", '0', true);
   s.enc_tab = env_flag("SHELFI_ENC_TAB", '0', true);
+  s.enc_vt = env_flag("SHELFI_ENC_VT", '0', true);
   s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
   s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
   if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;

@@ -326,18 +326,24 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_ct(
 // so that they do too (set g = 2 * 64 w + 64 r + lane), so the exchanges between the middle chunks
 // and into the last one need only the wave's own LDS ordering (wave_lds_sync), not a workgroup
 // barrier: 2 barriers per polynomial instead of 4.
-template <int BL, int K1, int K2, int K3, int K4, bool NR, bool WL = false>
+// VT (round 5): v's columns pass never ran (enc_cols_fused<..., VT>): the first chunk's v words are
+// the column's packed group patterns, and each row value is the sum of its block's 4 enc_vtab entries
+// (< 4q), looked up in a 2.6 KiB LDS slice copied once per workgroup (the combo's block b is the row).
+template <int BL, int K1, int K2, int K3, int K4, bool NR, bool WL = false, bool VT = false>
 __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
     const uint64_t* __restrict__ pbuf, uint32_t L, uint32_t logN, const ulonglong2* __restrict__ twb,
     const TowerConst* __restrict__ tcs, const uint64_t* __restrict__ pk, const uint64_t* __restrict__ pksh,
-    uint64_t* __restrict__ ct, uint32_t K, uint32_t per_combo, uint32_t t0, uint32_t nt) {
+    uint64_t* __restrict__ ct, uint32_t K, uint32_t per_combo, uint32_t t0, uint32_t nt,
+    const uint64_t* __restrict__ vtab) {
   static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan must cover the block");
+  static_assert(!VT || (BL == 11 && K1 == 3), "v tables: a 16-row columns pass, 8 columns per thread");
   constexpr int M1 = 1 << K1, NS1 = (1 << (BL - K1)) / 256, D1 = BL - K1;
   constexpr int ML = 1 << K4, NSL = (1 << (BL - K4)) / 256;
   // WL needs every middle-chunk set of a wave inside its 64 * 2^(BL-8) contiguous elements
   static_assert(!WL || (BL == 11 && K1 == 3 && K2 == 3 && K3 == 3 && K4 == 2), "wave-local plan");
   __shared__ __attribute__((aligned(16))) ulonglong2 tws[1 << BL];
   __shared__ __attribute__((aligned(16))) uint64_t sm[lpad_size(BL)];
+  __shared__ uint64_t vts[VT ? 4 * 81 : 1];
   // the last chunk's set r of this thread
   const auto last_g = [&](int r) -> uint32_t {
     return WL ? ((threadIdx.x >> 6) * (64u * NSL) + 64u * r + (threadIdx.x & 63u)) : threadIdx.x + 256u * r;
@@ -353,11 +359,19 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
   {
     const ulonglong2* __restrict__ src = twb + off;
     for (uint32_t i = threadIdx.x; i < (1u << BL); i += 256) tws[i] = src[i];
+    if (VT)  // rows = blocks: this combo's row b of tower t
+      for (uint32_t i = threadIdx.x; i < 4 * 81; i += 256) vts[i] = vtab[((uint64_t)t * 16 + b) * (4 * 81) + i];
   }
   uint64_t pf[NS1][M1];              // the next polynomial's first-chunk words
   ulonglong2 P[NSL][ML / 2], Ps[NSL][ML / 2];  // the next combine's key words (b or a)
   uint64_t V[NSL][ML];                // NTT(v) at this thread's last-chunk positions
   const auto fetch = [&](uint32_t kk, int poly) {
+    if (VT && poly == 0) {  // the packed patterns of columns tid + 256 m (this block's row of each)
+      const uint32_t* __restrict__ vp = reinterpret_cast<const uint32_t*>(pbuf + (uint64_t)kk * 3 * LN);
+#pragma unroll
+      for (int m = 0; m < M1; ++m) pf[0][m] = vp[threadIdx.x + (m << D1)];
+      return;
+    }
     const uint64_t* __restrict__ src = pbuf + ((uint64_t)kk * 3 + poly) * LN + off;
 #pragma unroll
     for (int r = 0; r < NS1; ++r)
@@ -390,10 +404,18 @@ __global__ __launch_bounds__(256) void ntt_fwd_blocks_enc_pp(
 #pragma unroll 1
     for (int poly = 0; poly < 3; ++poly) {
       uint64_t x[NS1][M1];
+      if (VT && poly == 0) {  // NTT(v)'s columns pass as table sums: row b of each column, < 4q
 #pragma unroll
-      for (int r = 0; r < NS1; ++r)
+        for (int m = 0; m < M1; ++m) {
+          const uint32_t w = (uint32_t)pf[0][m];
+          x[0][m] = vts[w & 127u] + vts[81 + ((w >> 7) & 127u)] + vts[162 + ((w >> 14) & 127u)] + vts[243 + (w >> 21)];
+        }
+      } else {
 #pragma unroll
-        for (int m = 0; m < M1; ++m) x[r][m] = pf[r][m];
+        for (int r = 0; r < NS1; ++r)
+#pragma unroll
+          for (int m = 0; m < M1; ++m) x[r][m] = pf[r][m];
+      }
       // the next polynomial's words (or the next ciphertext's v) and this one's key words
       if (poly < 2)
         fetch(k, poly + 1);
@@ -1080,42 +1102,6 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __re
 // fft_fwd_blocks (the first FFTSpecial pass) is defined with the decode-noise flooding
 // below, which it can fuse into its load.
 
-template <int LOGR>
-__global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ buf, uint32_t logS,
-                                                    const double2* __restrict__ tw,
-                                                    double* __restrict__ out, uint64_t n) {
-  constexpr int R = 1 << LOGR;
-  const uint32_t S = 1u << logS;
-  const uint32_t BLK = S >> LOGR;
-  const uint32_t bpp = BLK / 256;
-  const uint64_t k = blockIdx.x / bpp;
-  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
-  double2 v[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) v[r] = buf[k * S + col + (uint64_t)r * BLK];
-#pragma unroll
-  for (int s = 0; s < LOGR; ++s) {
-    const uint32_t lenh = BLK << s;
-    const int tr = 1 << s;
-#pragma unroll
-    for (int r0 = 0; r0 < R; ++r0) {
-      if ((r0 >> s) & 1) continue;
-      const int r1 = r0 + tr;
-      const uint32_t j = col + (uint32_t)(r0 & ((2 << s) - 1)) * BLK;  // (col + r0 BLK) mod len
-      const double2 W = tw[lenh + j];
-      const double2 u = v[r0];
-      const double2 w = cmul(v[r1], W);
-      v[r0] = cadd(u, w);
-      v[r1] = csub(u, w);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint64_t gi = k * S + col + (uint64_t)r * BLK;
-    if (gi < n) out[gi] = v[r].x;
-  }
-}
-
 #define FFT_DISPATCH(LOGRV, KERNEL, ...)                                                   \
   switch (LOGRV) {                                                                       \
     case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                           \
@@ -1274,7 +1260,11 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 // sampling its columns itself (4x the sampler work, no cross-wave traffic): a K = 4 call's 8192
 // columns become 512 waves instead of 128, for calls too small to fill the chip one column per thread
 // (register budget for 2 waves per SIMD: a small call has no more to give it).
-template <int LOGR, bool TAB, int WV = 4, bool TWL = false, bool TS = false>
+// VT (round 5; LOGR = 4, TAB, not TS): v's columns pass is left to the blocks pass, which sums
+// DeviceTables::enc_vtab entries for each row; this kernel writes only the column's 4 radix-4 group
+// patterns, packed 7 bits each into one uint32 at word c of the ciphertext's pbuf v region (8 KiB per
+// ciphertext instead of v's 4 towers x 256 KiB).
+template <int LOGR, bool TAB, int WV = 4, bool TWL = false, bool TS = false, bool VT = false>
 __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
                                                       double delta, const uint64_t* __restrict__ cdt,
@@ -1288,6 +1278,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
   constexpr int R = 1 << LOGR, IS = 16 / R, G = R / 4;
   constexpr int NTW = TS ? 4 : 1;  // towers with their own LDS tables in one workgroup
   static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
+  static_assert(!VT || (LOGR == 4 && TAB && !TS), "v tables: 16-row columns, one column per thread");
   __shared__ uint32_t thi[64], tlo[64];
   __shared__ uint64_t tabs_all[NTW][kEncTab];  // the tower's DeviceTables::enc_tab slice
   __shared__ ulonglong2 twl_all[NTW][1 << LOGR];  // TWL: the tower's {w, w'} for column stages (index m + i)
@@ -1393,6 +1384,8 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
       const auto tr = [&](int r) { return (uint32_t)((int32_t)(int8_t)(sv[r] & 0xFF) + 1); };
       vidx[g] = tr(g) + 3 * tr(g + G) + 9 * tr(g + 2 * G) + 27 * tr(g + 3 * G);
     }
+    if constexpr (VT)
+      reinterpret_cast<uint32_t*>(out + k * 3 * LN)[c] = vidx[0] | (vidx[1] << 7) | (vidx[2] << 14) | (vidx[3] << 21);
     // towers [0, t_split) reduced, [t_split, L) unreduced (q < kNoRedQ; the blocks pass knows)
     const auto small_polys = [&](uint32_t ta, uint32_t tb, auto nored) __attribute__((always_inline)) {
 #pragma unroll 1
@@ -1417,7 +1410,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
             twl[tid] = make_ulonglong2(tw[((uint64_t)t << logN) + tid], twp[((uint64_t)t << logN) + tid]);
         }
         tower_sync();
-        {
+        if constexpr (!VT) {
           uint64_t x[R];
 #pragma unroll
           for (int g = 0; g < G; ++g)
@@ -1569,6 +1562,7 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   for (uint32_t t = t_split; t < p.L; ++t)
     if (p.q[t] >= kNoRedQ) t_split = p.L;
   if (!pp || !sw.enc_nored) t_split = p.L;
+  bool vt = false;  // NTT(v)'s columns pass as enc_vtab sums in the blocks pass (round 5)
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
     const uint64_t nb = (K << (p.logN - nlogR)) / 256;
@@ -1582,7 +1576,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     // small calls (K <= kEncTsMaxK at 4 towers): one wave per tower (TS), so a call of a few
     // ciphertexts spreads over 4x the waves; SHELFI_ENC_TS=0 / 1 forces either (A/B switch)
     const bool ts = nlogR == 4 && tab && p.L == 4 && (sw.enc_ts >= 0 ? sw.enc_ts == 1 : K <= kEncTsMaxK);
-    if (ts)
+    vt = pp && tab && !ts && nlogR == 4 && dt.enc_vtab && sw.enc_vt && ntt_wave_local();
+    if (vt)  // v's columns pass left to the blocks pass (enc_vtab sums)
+      ENC_COLS(4, true, 3, true, false, true);
+    else if (ts)
       hipLaunchKernelGGL((enc_cols_fused<4, true, 3, true, true>), dim3((uint32_t)(nb * 4)), dim3(256), 0, s, fbuf, K,
                          p.logN, logS, p.L, p.delta, dt.cdt, dt.cdt_len, k8, g0, dt.tc, dt.psi_rev, dt.psi_rev_sh,
                          pbuf, flag, t_split, dt.enc_tab);
@@ -1631,28 +1628,22 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint32_t xg = xcd_combos(p.L << nlogR);
   if (pp) {  // one launch per tower class, each spread over all CUs
     const bool wl = ntt_wave_local();
-    if (t_split > 0) {
-      const uint32_t ncombo = t_split << nlogR;
+    const auto launch_pp = [&](uint32_t ta, uint32_t nt, bool nr) {
+      const uint32_t ncombo = nt << nlogR;
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
-      if (wl)
-        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false, true>), dim3(ncombo * pc), dim3(256), 0, s,
-                           pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
-      else
-        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, false>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
-                           p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, 0u, t_split);
-    }
-    if (t_split < p.L) {
-      const uint32_t ncombo = (p.L - t_split) << nlogR;
-      const uint32_t pc = pp_per_combo(ncombo, K, 3);
-      if (wl)
-        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true, true>), dim3(ncombo * pc), dim3(256), 0, s,
-                           pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
-                           p.L - t_split);
-      else
-        hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, true>), dim3(ncombo * pc), dim3(256), 0, s, pbuf,
-                           p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, t_split,
-                           p.L - t_split);
-    }
+#define ENC_PP(NR, WL, VT)                                                                                       \
+  hipLaunchKernelGGL((ntt_fwd_blocks_enc_pp<11, 3, 3, 3, 2, NR, WL, VT>), dim3(ncombo * pc), dim3(256), 0, s, pbuf, \
+                     p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, (uint32_t)K, pc, ta, nt, dt.enc_vtab)
+      if (nr && wl && vt) ENC_PP(true, true, true);
+      else if (nr && wl) ENC_PP(true, true, false);
+      else if (nr) ENC_PP(true, false, false);
+      else if (wl && vt) ENC_PP(false, true, true);
+      else if (wl) ENC_PP(false, true, false);
+      else ENC_PP(false, false, false);
+#undef ENC_PP
+    };
+    if (t_split > 0) launch_pp(0u, t_split, false);
+    if (t_split < p.L) launch_pp(t_split, p.L - t_split, true);
   } else if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
                        pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
@@ -2267,10 +2258,6 @@ struct FloodArgs {
 };
 
 // FFTSpecial first pass (decode): input already bit-reversed by the CRT's scatter; DIT
-// stages len = 2..blk with twiddle ffwd[len/2 + (x mod len)] in LDS blocks; the top LOGR
-// stages follow on register columns (fft_fwd_cols).  A single pass writes the real parts
-// of the first `n` slots straight into the caller's output vector.  FLOOD: the decode
-// noise is added while loading (see decode_stats_kernel).
 // Ciphertext k's flooding scale from decode_stats_kernel's partial sums: the noise's standard
 // deviation in slot units (the first block of each ciphertext records the precision failure and
 // logError).
@@ -2294,6 +2281,11 @@ __device__ __forceinline__ double flood_nsd(const FloodArgs& fa, uint64_t k, uin
   return stddev_p / fa.two_p;
 }
 
+// FFTSpecial first pass (decode): input already bit-reversed by the CRT's scatter; DIT
+// stages len = 2..blk with twiddle ffwd[len/2 + (x mod len)] in LDS blocks; the top LOGR
+// stages follow on register columns (fft_fwd_cols).  A single pass writes the real parts
+// of the first `n` slots straight into the caller's output vector; FLOOD adds the decode
+// noise there, in the output domain (as fft_fwd_cols).
 template <bool FLOOD>
 __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf, uint32_t logS,
                                                       uint32_t blkLog, const double2* __restrict__ tw,
@@ -2305,26 +2297,7 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
   const uint64_t k = blockIdx.x >> sh;
   const uint32_t b = blockIdx.x & ((1u << sh) - 1);
   const uint64_t off = k * S + ((uint64_t)b << blkLog);
-  if (FLOOD) {
-    const double nsd = flood_nsd(fa, k, b, S);
-    const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
-    const double4* src = reinterpret_cast<const double4*>(buf + off);
-    for (uint32_t m = threadIdx.x; m < blk / 8; m += 256) {  // positions 8m .. 8m + 7
-      uint64_t w[8];
-      chacha20_block(fa.key, (((uint64_t)b << blkLog) >> 3) + m, nonce, w);
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        double z0, z1, z2, z3;
-        flood_pair(w[2 * h], z0, z1);
-        flood_pair(w[2 * h + 1], z2, z3);
-        const double4 v = src[4 * m + h];
-        smc[8 * m + 2 * h] = make_double2(v.x + nsd * z0, v.y + nsd * z1);
-        smc[8 * m + 2 * h + 1] = make_double2(v.z + nsd * z2, v.w + nsd * z3);
-      }
-    }
-  } else {
-    for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];
-  }
+  for (uint32_t i = threadIdx.x; i < blk; i += 256) smc[i] = buf[off + i];
   __syncthreads();
   for (uint32_t len = 2; len <= blk; len <<= 1) {
     const uint32_t lenh = len >> 1;
@@ -2339,10 +2312,25 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
     }
     __syncthreads();
   }
-  if (final_pass) {
+  if (final_pass) {  // (one block per ciphertext: b == 0, blk == S)
+    double nso = 0.0;
+    uint64_t nonce = 0;
+    if (FLOOD) {
+      nso = flood_nsd(fa, k, b, S) * sqrt((double)S);
+      nonce = (3ull << 56) | (fa.g0 + k);
+    }
     for (uint32_t i = threadIdx.x; i < blk; i += 256) {
       const uint64_t gi = off + i;
-      if (gi < n) out[gi] = smc[i].x;
+      double v = smc[i].x;
+      if (FLOOD) {  // fft_fwd_cols's output-domain stream: normal (i div S/16) of block (i mod S/16)
+        const uint32_t S16 = S >> 4, nidx = i / S16;
+        uint64_t w[8];
+        chacha20_block(fa.key, i & (S16 - 1), nonce, w);
+        double z0, z1;
+        flood_pair(w[nidx >> 1], z0, z1);
+        v = __dadd_rn(v, __dmul_rn(nso, (nidx & 1) ? z1 : z0));
+      }
+      if (gi < n) out[gi] = v;
     }
   } else {
     for (uint32_t i = threadIdx.x; i < blk; i += 256) buf[off + i] = smc[i];
@@ -2350,12 +2338,12 @@ __global__ __launch_bounds__(256) void fft_fwd_blocks(double2* __restrict__ buf,
 }
 
 // FFTSpecial's first pass (decode, not the final pass): block b of ciphertext k, DIT half-sizes
-// 1 .. 2^(BL-1); K1 = 3, so the first chunk's set is 8 consecutive positions = one ChaCha block
-// of the flooding stream.
-template <int BL, int K1, int K2, int K3, int K4, bool FLOOD, bool SWZ = true>
+// 1 .. 2^(BL-1).  (Until round 4 the flooding noise was added here, on load; it now lands on the
+// output in fft_fwd_cols.)
+template <int BL, int K1, int K2, int K3, int K4, bool SWZ = true>
 __global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __restrict__ buf, uint32_t logS,
-                                                                  const double2* __restrict__ tw, FloodArgs fa) {
-  static_assert(K1 == 3 && K1 + K2 + K3 + K4 == BL, "chunk plan");
+                                                                  const double2* __restrict__ tw) {
+  static_assert(K1 + K2 + K3 + K4 == BL, "chunk plan");
   __shared__ __attribute__((aligned(16))) double2 sm[1 << BL];
   const uint32_t S = 1u << logS, sh = logS - BL;
   const uint64_t k = blockIdx.x >> sh;
@@ -2363,21 +2351,7 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __re
   double2* __restrict__ g = buf + k * S + ((uint64_t)b << BL);
   const auto lds_ld = [&](uint32_t j) { return sm[fft_swz<SWZ>(j)]; };
   const auto lds_st = [&](uint32_t j, double2 v) { sm[fft_swz<SWZ>(j)] = v; };
-  if (FLOOD) {
-    const double nsd = flood_nsd(fa, k, b, S);
-    const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
-    // set s = positions 8s .. 8s + 7 = ChaCha block (b 2^BL) / 8 + s; position 8s + i takes word i
-    uint64_t w[8];
-    chacha20_block(fa.key, (((uint64_t)b << BL) >> 3) + threadIdx.x, nonce, w);
-    fft_chunk<BL, K1, 0, true>(tw, [&](uint32_t j) {
-      double z0, z1;
-      flood_pair(w[j & 7], z0, z1);
-      const double2 v = g[j];
-      return make_double2(v.x + nsd * z0, v.y + nsd * z1);
-    }, lds_st);
-  } else {
-    fft_chunk<BL, K1, 0, true>(tw, [&](uint32_t j) { return g[j]; }, lds_st);
-  }
+  fft_chunk<BL, K1, 0, true>(tw, [&](uint32_t j) { return g[j]; }, lds_st);
   __syncthreads();
   fft_chunk<BL, K2, K1, true>(tw, lds_ld, lds_st);
   __syncthreads();
@@ -2385,6 +2359,84 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_fwd_blocks_ct(double2* __re
   __syncthreads();
   fft_chunk<BL, K4, K1 + K2 + K3, true>(tw, lds_ld, [&](uint32_t j, double2 v) { g[j] = v; });
 }
+
+// FFTSpecial's last pass (decode): the top LOGR stages on register columns; writes the real parts
+// of the first `n` slots straight into the caller's output vector.  FLOOD (round 5): PALISADE's
+// decode noise in the output domain -- N(0, sd sqrt(S)) added to each decoded real part, the same
+// distribution as N(0, sd) on every FFT input (FFTSpecial's F F^H = S I; oracle or_decrypt_flood):
+// slot i takes normal (i div S/16) of ChaCha20 block (i mod S/16), so a thread's 2^LOGR rows share
+// 2^max(0, LOGR-4) blocks.
+template <int LOGR, bool FLOOD = false>
+__global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ buf, uint32_t logS,
+                                                    const double2* __restrict__ tw,
+                                                    double* __restrict__ out, uint64_t n, FloodArgs fa) {
+  constexpr int R = 1 << LOGR;
+  const uint32_t S = 1u << logS;
+  const uint32_t BLK = S >> LOGR;
+  const uint32_t bpp = BLK / 256;
+  const uint64_t k = blockIdx.x / bpp;
+  const uint32_t col = (blockIdx.x % bpp) * 256 + threadIdx.x;
+  double2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = buf[k * S + col + (uint64_t)r * BLK];
+#pragma unroll
+  for (int s = 0; s < LOGR; ++s) {
+    const uint32_t lenh = BLK << s;
+    const int tr = 1 << s;
+#pragma unroll
+    for (int r0 = 0; r0 < R; ++r0) {
+      if ((r0 >> s) & 1) continue;
+      const int r1 = r0 + tr;
+      const uint32_t j = col + (uint32_t)(r0 & ((2 << s) - 1)) * BLK;  // (col + r0 BLK) mod len
+      const double2 W = tw[lenh + j];
+      const double2 u = v[r0];
+      const double2 w = cmul(v[r1], W);
+      v[r0] = cadd(u, w);
+      v[r1] = csub(u, w);
+    }
+  }
+  if (FLOOD) {
+    const double nso = flood_nsd(fa, k, blockIdx.x % bpp, S) * sqrt((double)S);
+    const uint64_t nonce = (3ull << 56) | (fa.g0 + k);
+    const uint32_t S16 = S >> 4;
+    constexpr int LO = LOGR > 4 ? LOGR - 4 : 0;  // ChaCha blocks per thread: 2^LO
+#pragma unroll
+    for (int rl = 0; rl < (1 << LO); ++rl) {
+      uint64_t w[8];
+      chacha20_block(fa.key, (col + BLK * (uint32_t)rl) & (S16 - 1), nonce, w);
+      if (LOGR >= 4) {  // the thread's rows use all 16 normals of the block
+        double z[16];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) flood_pair(w[m], z[2 * m], z[2 * m + 1]);
+#pragma unroll
+        for (int r = rl; r < R; r += (1 << LO)) {
+          const uint32_t nidx = (col + BLK * (uint32_t)r) / S16;  // < 16
+          double zr = 0.0;
+#pragma unroll
+          for (int m = 0; m < 16; ++m) zr = (uint32_t)m == nidx ? z[m] : zr;  // no dynamic register index
+          v[r].x = __dadd_rn(v[r].x, __dmul_rn(nso, zr));
+        }
+      } else {  // rows 2^(4-LOGR) normals apart: one Box-Muller pair per row, half of it used
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t nidx = (col + BLK * (uint32_t)r) / S16;
+          uint64_t wr = 0;
+#pragma unroll
+          for (int m = 0; m < 8; ++m) wr = (uint32_t)m == (nidx >> 1) ? w[m] : wr;
+          double z0, z1;
+          flood_pair(wr, z0, z1);
+          v[r].x = __dadd_rn(v[r].x, __dmul_rn(nso, (nidx & 1) ? z1 : z0));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t gi = k * S + col + (uint64_t)r * BLK;
+    if (gi < n) out[gi] = v[r].x;
+  }
+}
+
 static uint32_t flood_groups(uint32_t S) {
   const uint32_t half = S / 2;
   return half >= kFloodPairsPerWg ? half / kFloodPairsPerWg : 1;
@@ -2490,25 +2542,36 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   }
   const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && switches().fft_ct;
   const dim3 fg((uint32_t)(K << flogR));
-  if (fct && fblkLog == 10 && fused_flood)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, true>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
-  else if (fct && fblkLog == 10)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2, false>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd, fa);
-  else if (fct && fused_flood)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<11, 3, 3, 3, 2, true>), fg, dim3(256), 0, s, fbuf, logS, dt.fft_fwd, fa);
+  // the flooding noise lands on the pass that writes the output (fft_fwd_cols, or the single pass)
+  if (fct && fblkLog == 10)
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<10, 3, 3, 2, 2>), fg, dim3(128), 0, s, fbuf, logS, dt.fft_fwd);
   else if (fct)
-    hipLaunchKernelGGL((fft_fwd_blocks_ct<11, 3, 3, 3, 2, false>), fg, dim3(256), 0, s, fbuf, logS, dt.fft_fwd, fa);
-  else if (fused_flood)
-    hipLaunchKernelGGL(fft_fwd_blocks<true>, fg, dim3(256), lds, s, fbuf, logS,
-                       fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
+    hipLaunchKernelGGL((fft_fwd_blocks_ct<11, 3, 3, 3, 2>), fg, dim3(256), 0, s, fbuf, logS, dt.fft_fwd);
+  else if (fused_flood && flogR == 0)
+    hipLaunchKernelGGL(fft_fwd_blocks<true>, fg, dim3(256), lds, s, fbuf, logS, fblkLog, dt.fft_fwd, out, n, 1, fa);
   else
     hipLaunchKernelGGL(fft_fwd_blocks<false>, fg, dim3(256), lds, s, fbuf, logS,
                        fblkLog, dt.fft_fwd, out, n, flogR == 0 ? 1 : 0, fa);
   SHELFI_HIP(hipGetLastError());
   if (flogR > 0) {
     const uint64_t nb = K * ((p.batch >> flogR) / 256);
-    FFT_DISPATCH(flogR, fft_fwd_cols, dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd,
-                 out, n);
+#define COLS_FWD(LR)                                                                                          \
+  if (fused_flood)                                                                                            \
+    hipLaunchKernelGGL((fft_fwd_cols<LR, true>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd, out, \
+                       n, fa);                                                                                 \
+  else                                                                                                        \
+    hipLaunchKernelGGL((fft_fwd_cols<LR, false>), dim3((uint32_t)nb), dim3(256), 0, s, fbuf, logS, dt.fft_fwd,     \
+                       out, n, fa);
+    switch (flogR) {
+      case 1: COLS_FWD(1) break;
+      case 2: COLS_FWD(2) break;
+      case 3: COLS_FWD(3) break;
+      case 4: COLS_FWD(4) break;
+      case 5: COLS_FWD(5) break;
+      case 6: COLS_FWD(6) break;
+      default: throw Error{SHELFI_ERR_ARG, "unsupported batch size"};
+    }
+#undef COLS_FWD
     SHELFI_HIP(hipGetLastError());
   }
 }

@@ -66,6 +66,7 @@ struct Switches {
   bool dec_pp = true;          // SHELFI_DEC_PP=0: one-shot decrypt block pass
   bool enc_nored = true;       // SHELFI_ENC_NORED=0: reductions in every tower
   bool enc_tab = true;         // SHELFI_ENC_TAB=0: butterflies for v's / e1's first column stages
+  bool enc_vt = true;          // SHELFI_ENC_VT=0: v's columns pass in enc_cols_fused, not enc_vtab sums
   int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
   bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
   int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
@@ -153,6 +154,11 @@ struct DeviceTables {
   // [L][kEncTab]: the radix-4 outputs of 4 ternary inputs (stages 0-1, 4 x 81) and W0 e for e1's
   // stage 0 (e + 64, |e| <= 63), all canonical
   uint64_t* enc_tab = nullptr;
+  // encrypt's NTT(v) without the columns pass (round 5, kernels.hip ntt_fwd_blocks_enc_pp<VT>): for a
+  // 16-row columns pass (logN - BL = 4), [L][16 rows][4 groups][81]: output row r of the 4 column
+  // stages applied to v restricted to rows g, g + 4, g + 8, g + 12 with ternary pattern p (base 3),
+  // canonical; the row's value is the sum over the 4 groups.  nullptr for other shapes.
+  uint64_t* enc_vtab = nullptr;
   int cdt_len = 0;
   uint64_t qmod128_lo = 0, qmod128_hi = 0;  // Q mod 2^128
 };

@@ -994,7 +994,35 @@ void or_flood_normals(uint64_t seed, uint64_t g, uint32_t S, double* z) {
   }
 }
 
-/* decrypt + flooded decode of one ciphertext (seeded stream, ciphertext index g). */
+/* Decode-flooding normals in the output domain (round 5, the product's stream for 2^6 slots and
+ * more): slot i's normal is normal (i div S/16) of ChaCha20 block (i mod S/16) (nonce (3 << 56) | g);
+ * the block's words 2m, 2m + 1 are one Box-Muller pair (as or_flood_normals), giving normals 2m
+ * (r cos) and 2m + 1 (r sin).  zo[i] for i < S. */
+void or_flood_out_normals(uint64_t seed, uint64_t g, uint32_t S, double* zo) {
+  uint32_t key[8], blk[16];
+  or_seed_to_key(seed, key);
+  const uint32_t S16 = S / 16;
+  for (uint32_t b = 0; b < S16; ++b) {
+    or_chacha20_block(key, b, (3ull << 56) | g, blk);
+    for (uint32_t m = 0; m < 8; ++m) {
+      double u1 = ((double)blk[2 * m] + 1.0) * 0x1.0p-32;
+      double u2 = (double)blk[2 * m + 1] * 0x1.0p-32;
+      double r = sqrt(-2.0 * log(u1));
+      zo[b + S16 * (2 * m)] = r * cos(2.0 * M_PI * u2);
+      zo[b + S16 * (2 * m + 1)] = r * sin(2.0 * M_PI * u2);
+    }
+  }
+}
+
+/* decrypt + flooded decode of one ciphertext (seeded stream, ciphertext index g).
+ * PALISADE adds N(0, sd) to every coefficient of the symmetrized decryption, then decodes: the
+ * decoded slots' real parts carry Re(F z) sd for an i.i.d. standard complex Gaussian vector z of
+ * the S FFT inputs.  FFTSpecial is F with F F^H = S I (rows: evaluations at the S powers zeta^(5^k)
+ * of a primitive 4S-th root; distinct 5^k are congruent mod 4, so every off-diagonal geometric sum
+ * vanishes), hence Re(F z) is i.i.d. N(0, S) over the slots: the same distribution as adding
+ * N(0, sd sqrt(S)) to each decoded real part.  From 2^6 slots on that is how the noise is drawn
+ * (or_flood_out_normals, round 5): the exact decode plus output-domain noise, so the product adds it
+ * in the FFT's last pass.  Below 2^6 slots the input-domain form (round 2) stays. */
 int or_decrypt_flood(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
                      const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale,
                      uint32_t p_bits, double m_factor, uint64_t seed, uint64_t g, size_t n,
@@ -1007,10 +1035,18 @@ int or_decrypt_flood(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_
   if (!rc) {
     double sd;
     or_decode_stats(re, im, slots, N, p_bits, m_factor, &sd, log_error, fail);
-    or_flood_normals(seed, g, slots, z);
-    or_decode_symmetrize(re, im, slots, z, sd / ldexp(1.0, (int)p_bits));
-    or_fft_special(re, im, slots);
-    for (size_t i = 0; i < n; ++i) out[i] = re[i];
+    const double nsd = sd / ldexp(1.0, (int)p_bits);
+    if (slots >= 64) {
+      or_flood_out_normals(seed, g, slots, z);
+      or_fft_special(re, im, slots);
+      const double nso = nsd * sqrt((double)slots);
+      for (size_t i = 0; i < n; ++i) out[i] = re[i] + nso * z[i];
+    } else {
+      or_flood_normals(seed, g, slots, z);
+      or_decode_symmetrize(re, im, slots, z, nsd);
+      or_fft_special(re, im, slots);
+      for (size_t i = 0; i < n; ++i) out[i] = re[i];
+    }
   }
   free(z);
   free(re);

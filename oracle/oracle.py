@@ -53,6 +53,7 @@ def _load():
         "or_decode_stats": (None, [f64p, f64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, f64p,
                                    C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "or_flood_normals": (None, [C.c_uint64, C.c_uint64, C.c_uint32, f64p]),
+        "or_flood_out_normals": (None, [C.c_uint64, C.c_uint64, C.c_uint32, f64p]),
         "or_decrypt_flood": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
                                        C.c_double, C.c_uint32, C.c_double, C.c_uint64, C.c_uint64,
                                        C.c_size_t, f64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -327,6 +328,19 @@ def decrypt(ct, sk, q, psi, slots: int, scale: float, n: int) -> np.ndarray:
 
 
 # ------------------------------------------------------------ randomness ----
+def seed_to_key(seed: int) -> np.ndarray:
+    key = np.zeros(8, np.uint32)
+    lib.or_seed_to_key(seed, _p(key, u32p))
+    return key
+
+
+def flood_out_normals(seed: int, g: int, S: int) -> np.ndarray:
+    """Output-domain decode-flooding normals of ciphertext g (round 5): one per slot."""
+    z = np.zeros(S, np.float64)
+    lib.or_flood_out_normals(seed, g, S, _p(z, f64p))
+    return z
+
+
 def chacha20_block(key_words, counter: int, nonce: int) -> np.ndarray:
     key = np.ascontiguousarray(key_words, dtype=np.uint32)
     out = np.zeros(16, np.uint32)

@@ -75,3 +75,44 @@ def test_flooded_decrypt_of_a_real_ciphertext(palisade_keys):
     # the seeded stream is reproducible, another ciphertext index draws other noise
     assert np.array_equal(O.decrypt_flood(ct, sk, q, psi, S, delta, S, seed=11, g=5)[0], fl)
     assert not np.array_equal(O.decrypt_flood(ct, sk, q, psi, S, delta, S, seed=11, g=6)[0], fl)
+
+
+def test_fft_special_is_sqrt_s_times_unitary():
+    """Round 5 moved the decode noise to the output domain (or_flood_out_normals).  That is
+    distribution-preserving because FFTSpecial's matrix F satisfies F F^H = S I: PALISADE's i.i.d.
+    circular complex input noise z (unit variance per component) maps to F z, whose real parts have
+    covariance (Re(F E[z z^H] F^H) + Re(F E[z z^T] F^T)) / 2 = S I: i.i.d. N(0, S)."""
+    for S in (64, 256):
+        F = np.stack([O.fft_special(np.eye(S)[j] + 0j) for j in range(S)], axis=1)  # column j = F e_j
+        assert np.abs(F @ F.conj().T - S * np.eye(S)).max() < 1e-9 * S
+        # z circular (E z z^T = 0): Cov(Re F z) = Re(F F^H) / 2 per unit component variance x 2 = S I
+
+
+def test_output_domain_noise_matches_input_domain_distribution():
+    """The input-domain form (PALISADE's order: symmetrize, add N(0, nsd) to every FFT input, decode)
+    and the output-domain form (exact decode + N(0, nsd sqrt(S)) per slot) have the same
+    per-slot standard deviation and no cross-slot correlation (Monte Carlo at S = 256)."""
+    S, nsd, trials = 256, 1.0, 400
+    rng = np.random.default_rng(7)
+    samples = []
+    for _ in range(trials):
+        z = rng.standard_normal(S) + 1j * rng.standard_normal(S)
+        samples.append(O.fft_special(nsd * z).real)
+    a = np.array(samples)
+    assert np.std(a) == pytest.approx(nsd * np.sqrt(S), rel=0.05)
+    c = np.corrcoef(a[:, :8].T)
+    assert np.abs(c - np.eye(8)).max() < 0.2
+
+
+def test_output_domain_normals_stream():
+    """or_flood_out_normals: slot i takes normal (i div S/16) of block (i mod S/16); standard normal."""
+    S = 4096
+    z = O.flood_out_normals(11, 5, S)
+    assert z.shape == (S,) and abs(np.mean(z)) < 0.1 and np.std(z) == pytest.approx(1.0, rel=0.05)
+    key = O.seed_to_key(11)
+    blk = O.chacha20_block(key, 7, (3 << 56) | 5)
+    u1 = (float(blk[2]) + 1.0) * 2.0 ** -32
+    u2 = float(blk[3]) * 2.0 ** -32
+    r = np.sqrt(-2 * np.log(u1))
+    assert z[7 + (S // 16) * 2] == pytest.approx(r * np.cos(2 * np.pi * u2), abs=1e-15)
+    assert z[7 + (S // 16) * 3] == pytest.approx(r * np.sin(2 * np.pi * u2), abs=1e-15)

@@ -1,5 +1,5 @@
-"""§8(f3) on the HIP path: decode noise flooding (decode_stats_kernel + the noise fused into
-the first FFT pass; decode_flood_kernel for batches below 2^6 slots) against the
+"""§8(f3) on the HIP path: decode noise flooding (decode_stats_kernel + the noise added to the
+FFT's output in its last pass; decode_flood_kernel for batches below 2^6 slots) against the
 oracle's restatement with the same seeded noise stream.  Tolerance 1e-14 absolute:
 the noise (~1e-13) is generated with GPU vs glibc log/sincos (ulp-level differences)
 and sigma is a tree vs sequential sum; everything else is the exact decode."""
@@ -58,7 +58,8 @@ def ck_small(tmp_path_factory):
 
 @pytest.mark.parametrize("which", ["ck1", "ck2", "ck_small", "ck_tiny"])
 def test_flooded_decrypt_matches_oracle(which, request):
-    """decode_stats_kernel + fft_fwd_blocks<true> (noise fused into the FFT load) against the
+    """decode_stats_kernel + fft_fwd_cols<.., true> / fft_fwd_blocks<true> (output-domain noise,
+    fused into the FFT's last pass) against the
     oracle; ck_tiny (32 slots) takes decode_flood_kernel, the per-ciphertext form that serves rings
     below 2^6 slots (no longer selectable elsewhere since round 5)."""
     ck = request.getfixturevalue(which)

@@ -27,6 +27,7 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
     ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
     ("SHELFI_ENC_TAB", "0"),         # butterflies instead of the small-polynomial tables
+    ("SHELFI_ENC_VT", "0"),          # v's columns pass in enc_cols_fused, not table sums in the blocks pass
     ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
     ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
