@@ -91,10 +91,10 @@ def parse():
                     help="--layout arena: Arena's layout (auto = uint64 learner batches for arenas of at most "
                          "Arena.AUTO_U64_ROWS rows per learner, e.g. cfg2; packed otherwise)")
     ap.add_argument("--place-output", type=int, default=16,
-                    help="arena layout, no collective: time this many candidate output buffers before "
-                         "the timed region and keep the fastest placement (Arena.place_output; the "
-                         "plain torch.empty buffer's launch is reported as roofline.untuned_output); "
-                         "0 = one plain buffer")
+                    help="arena layout, no collective: the aggregate goes to the arena's own placed buffer "
+                         "(Arena.output, which times this many fresh candidates plus a plain torch.empty "
+                         "buffer once and keeps the fastest; the plain buffer's launch is reported as "
+                         "roofline.untuned_output); 0 = one plain buffer")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the N>1 path (NCCL group, pipelined reduce_scatter, modq) even at N=1")
@@ -411,15 +411,13 @@ def main():
         comb = None
         placement = None
         if args.layout == "arena" and arena.layout == "packed" and shard != "learners" and args.place_output > 0:
-            # where the aggregate lands in HBM relative to the arena moves the launch time by
-            # up to 12%: keep the fastest of a few candidate buffers; the penalty
-            # follows ~3 GiB address ranges (probes/r03_placement_alloc.txt), so 16 candidates
-            # (24 GiB of address space, freed after the pick) find a fast range more often than 8
-            # candidate 0 is a plain torch.empty buffer allocated first (on some boxes every
-            # buffer allocated next to the others ran slower than it)
+            # the launch runs up to ~14% slower for some (arena, output) pairs of physical HBM regions
+            # (a property of the pair: tools/placement_probe2.py); the arena's own
+            # output buffer (Arena.output) is the fastest of a plain torch.empty buffer (candidate 0,
+            # reported as roofline.untuned_output) and 16 fresh candidates, timed once
             plain0 = torch.empty((K_loc, 2, L, N), dtype=torch.int64, device=dev)
-            out, cand_ms = arena.place_output(weights, candidates=args.place_output, launches=4,
-                                              include=[plain0])
+            out = arena.output(candidates=args.place_output, include=[plain0])
+            cand_ms = arena.output_placement
             del plain0
             placement = {"candidates": len(cand_ms), "candidate_launch_ms": cand_ms,
                          "chosen": cand_ms.index(min(cand_ms))}

@@ -599,6 +599,7 @@ void reload_switches() {
   s.enc_vt = env_flag("SHELFI_ENC_VT", '0', true);
   s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
   s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
+  s.crt_swz = env_flag("SHELFI_CRT_SWZ", '0', true);
   if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;
   s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
   s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);
@@ -608,6 +609,7 @@ void reload_switches() {
     if (atoll(e) > 0) s.dev_chunk_mib = (uint64_t)atoll(e);
   if (const char* e = getenv("SHELFI_WAVG_CHUNK_MIB"))
     if (atoll(e) > 0) s.wavg_chunk_mib = (uint64_t)atoll(e);
+  s.h2d_direct = env_flag("SHELFI_H2D_DIRECT", '0', true);
   g_switches = s;
 }
 const Switches& switches() { return g_switches; }
@@ -727,6 +729,8 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     dfree_t(ctx->unit_wl);
     dfree(ctx->scratch);
     dfree(ctx->io);
+    if (ctx->gather_host) (void)hipHostFree(ctx->gather_host);
+    ctx->gather_host = nullptr;
     dfree_t(ctx->dev_flag);
     if (ctx->host_flag) (void)hipHostFree(ctx->host_flag);
     ctx->host_flag = nullptr;
@@ -1241,19 +1245,26 @@ static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* c
 
 // Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
 // chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
-// (stream B), with two device buffer sets.  Writes the payload of the result.  (Zero-copy uploads
-// registered in place with hipHostRegister measured slower than the staging ring and were removed
-// in round 5: tools/h2d_register_ab.py.)
+// (stream B), with two device buffer sets.  Writes the payload of the result.
+// Uploads (round 5, SHELFI_H2D_DIRECT): each learner's chunk is one contiguous byte range of its
+// blob, copied straight from the caller's pageable memory (the runtime's own pinned path: 55.6 GB/s
+// in 32 MiB copies vs 42.5 GB/s through the staging ring, tools/h2d_pageable_probe.py); a PALISADE
+// archive's range lands raw and its tower runs are gathered into [K][2][L][N] on the device.  The
+// staging ring (SHELFI_H2D_DIRECT=0) copies each residue run through pinned slots.  (Zero-copy
+// uploads registered in place with hipHostRegister measured slower than the ring and were removed in
+// round 5: tools/h2d_register_ab.py.)  The sum's D2H goes through the ring either way.
 static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in,
                                 const float* weights, size_t C, uint64_t K, const CtLayout& dst,
                                 const size_t* lens) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
-  // chunk: ~128 MiB of input per learner-group buffer (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 /
-  // 48.2 / 48.7 ms for 16 learners x 64 cts, uint64 blobs; packed wire 54.6 / 46.0 / 42.1 / 42.5 ms,
+  const bool direct = switches().h2d_direct;
+  // chunk of input per learner-group buffer: direct uploads want >= 32 MiB per copy (8 MiB copies
+  // ran 51.6 GB/s, 2 MiB 41.3), so 512 MiB per 16 learners; through the ring ~128 MiB (round 4:
+  // 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x 64 cts,
   // profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
-  const uint64_t chunk_mib = switches().wavg_chunk_mib;
+  const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 512 : 128;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
@@ -1261,35 +1272,76 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   // output is packed before its D2H
   const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
   const bool pin = in.front().packed, pout = dst.packed;
+  const bool raw = direct && in.front().pal;  // archives: raw ranges, gathered on the device
   const size_t pin_chunk = pin ? group * kc * pct : 0, pout_chunk = pout ? kc * pct : 0;
-  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (in_chunk + out_chunk + pin_chunk + pout_chunk));
+  const uint64_t nchunks = (K + kc - 1) / kc;
+  std::vector<HostPiece> pcs;
+  // raw ranges: the largest byte range any learner's chunk spans (tower headers included)
+  size_t raw_cap = 0, runs_cap = 0;
+  if (raw) {
+    for (uint64_t ci = 0; ci < nchunks; ++ci) {
+      const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+      for (size_t c = 0; c < C; ++c) {
+        in[c].pieces(k0, kn, p, pcs);
+        raw_cap = std::max<size_t>(raw_cap, (size_t)(pcs.back().p + pcs.back().n - pcs.front().p));
+      }
+    }
+    raw_cap = (raw_cap + 64 + 255) & ~(size_t)255;  // + the gather's read-ahead of one dword
+    runs_cap = group * kc * 2 * p.L;
+    if (ctx->gather_cap < runs_cap) {
+      if (ctx->gather_host) SHELFI_HIP(hipHostFree(ctx->gather_host));
+      ctx->gather_host = nullptr;
+      ctx->gather_cap = 0;
+      SHELFI_HIP(hipHostMalloc((void**)&ctx->gather_host, 2 * runs_cap * 8, hipHostMallocDefault));
+      ctx->gather_cap = runs_cap;
+    }
+  }
+  const size_t raw_chunk = raw ? group * raw_cap : 0, tab_chunk = raw ? runs_cap * 8 : 0;
+  uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes,
+                                 2 * (in_chunk + out_chunk + pin_chunk + pout_chunk + raw_chunk + tab_chunk));
   uint8_t* inb[2] = {io, io + in_chunk};
   uint8_t* outb[2] = {io + 2 * in_chunk, io + 2 * in_chunk + out_chunk};
   uint8_t* const pbase = io + 2 * (in_chunk + out_chunk);
   uint8_t* pinb[2] = {pbase, pbase + pin_chunk};
   uint8_t* poutb[2] = {pbase + 2 * pin_chunk, pbase + 2 * pin_chunk + pout_chunk};
+  uint8_t* const rbase = pbase + 2 * (pin_chunk + pout_chunk);
+  uint8_t* rawb[2] = {rbase, rbase + raw_chunk};
+  uint64_t* tabd[2] = {(uint64_t*)(rbase + 2 * raw_chunk), (uint64_t*)(rbase + 2 * raw_chunk + tab_chunk)};
   const ArenaPack ap = arena_pack(p);
-  // A: staged H2D of the learners' slices; B: wavg; C: staged D2H of the sum
+  // A: H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
-  std::vector<HostPiece> pcs;
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
-  const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
     for (size_t c0 = 0; c0 < C; c0 += group) {
       const size_t gc = std::min(group, C - c0);
       if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
+      uint64_t* tabh = raw ? ctx->gather_host + b * runs_cap : nullptr;
+      if (raw && (ci >= 2 || c0 > 0)) SHELFI_HIP(hipEventSynchronize(pp.in_ready[b]));  // tabh's last copy done
+      uint64_t runs = 0;
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
-        // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked)
-        uint8_t* land = pin ? pinb[b] + c * kn * pct : inb[b] + c * kn * ct_bytes;
-        sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
+        // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked), or
+        // (archives) its raw range, gathered below
+        uint8_t* land = raw ? rawb[b] + c * raw_cap : pin ? pinb[b] + c * kn * pct : inb[b] + c * kn * ct_bytes;
+        if (direct) {
+          const uint8_t* lo = pcs.front().p;
+          const size_t span = (size_t)(pcs.back().p + pcs.back().n - lo);
+          if (raw)
+            for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
+          SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
+          sr.s.poll();  // drain finished sums while the uploads run
+        } else {
+          sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
+        }
       }
+      if (raw) SHELFI_HIP(hipMemcpyAsync(tabd[b], tabh, runs * 8, hipMemcpyHostToDevice, pp.a));
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+      if (raw) launch_gather_runs(rawb[b], tabd[b], runs, (uint32_t)(p.N * 8), inb[b], pp.b);
       if (pin)  // unpacked on the compute stream, so the upload stream moves on to the next chunk
         for (size_t c = 0; c < gc; ++c)
           launch_blob_unpack((const uint32_t*)(pinb[b] + c * kn * pct), kn, p.L, p.logN, ap,

@@ -69,13 +69,16 @@ struct Switches {
   bool enc_vt = true;          // SHELFI_ENC_VT=0: v's columns pass in enc_cols_fused, not enc_vtab sums
   int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
   bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
+  bool crt_swz = true;         // SHELFI_CRT_SWZ=0: ntt_inv_cols_crt's padded LDS rows (68 u64, 4 WGs/CU)
   int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
   int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
   int pack_waves = 0;          // SHELFI_PACK_WAVES=2|8 (0: 4 rows per block)
   int wavg_rows = 0;           // SHELFI_WAVG_ROWS=1|2 (0: by shape)
   int arena_stager = -1;       // SHELFI_ARENA_STAGER=0|1 (-1: by upload shape)
   uint64_t dev_chunk_mib = 4096;  // SHELFI_DEV_CHUNK_MIB: device encrypt / decrypt scratch per chain
-  uint64_t wavg_chunk_mib = 128;  // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
+  uint64_t wavg_chunk_mib = 0;    // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
+                                  // (0: 512 MiB with direct uploads, 128 through the staging ring)
+  bool h2d_direct = true;         // SHELFI_H2D_DIRECT=0: bytes-API aggregation uploads through the pinned ring
 };
 const Switches& switches();
 void reload_switches();
@@ -248,6 +251,8 @@ struct shelfi_ctx {
   size_t scratch_bytes = 0;
   void* io = nullptr;            // bytes-API staging arena (inputs/outputs)
   size_t io_bytes = 0;
+  uint64_t* gather_host = nullptr;  // pinned run-offset tables of the direct uploads (2 x gather_cap words)
+  size_t gather_cap = 0;
   shelfi::EvalState* ev = nullptr;  // EvalMult / ModReduce state (eval.cpp), lazily created
   // RCCL communicator of the multi-GPU combine (comm.cpp; ncclComm_t, opaque here)
   void* comm = nullptr;
@@ -304,6 +309,10 @@ void launch_blob_pack(const uint64_t* src, uint64_t K, uint32_t L, uint32_t logN
                       const TowerConst* tc, uint32_t* dst, uint32_t* bad, hipStream_t s);
 void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t logN, const ArenaPack& ap,
                         uint64_t* dst, hipStream_t s);
+// Residue runs of an upload landed raw (a PALISADE archive's byte range with its tower headers): run j is
+// run_bytes bytes at raw + src_off[j] (any alignment) -> dst + j * run_bytes (16-B aligned)
+void launch_gather_runs(const uint8_t* raw, const uint64_t* src_off, uint64_t runs, uint32_t run_bytes, uint8_t* dst,
+                        hipStream_t s);
 void launch_modq(uint64_t* buf, uint64_t rows, uint32_t L, uint32_t logN, const TowerConst* tc,
                  hipStream_t s);
 // *bad |= 1 when a residue of the [rows / (2 L)][2][L][N] batch is >= its tower's q

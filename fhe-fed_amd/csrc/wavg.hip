@@ -633,6 +633,40 @@ void launch_blob_unpack(const uint32_t* src, uint64_t K, uint32_t L, uint32_t lo
   SHELFI_HIP(hipGetLastError());
 }
 
+// The direct uploads' gather (round 5): 16 output bytes per thread from 5 aligned dwords of the raw
+// upload and v_alignbyte (the archive's tower runs sit at arbitrary byte offsets); blockIdx.y = run.
+__global__ __launch_bounds__(256) void gather_runs_kernel(const uint8_t* __restrict__ raw,
+                                                          const uint64_t* __restrict__ src_off, uint32_t run_bytes,
+                                                          uint8_t* __restrict__ dst) {
+  const uint64_t j = blockIdx.y;
+  const uint8_t* s = raw + src_off[j];
+  u32x4* d = reinterpret_cast<u32x4*>(dst + j * run_bytes);
+  const uint32_t sh = (uint32_t)((uintptr_t)s & 3u);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)s & ~(uintptr_t)3);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < run_bytes / 16; i += gridDim.x * 256) {
+    const uint32_t* p = w + 4 * i;
+    const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = sh ? p[4] : 0u;
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
+    v.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
+    v.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
+    v.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+    d[i] = v;
+  }
+}
+
+void launch_gather_runs(const uint8_t* raw, const uint64_t* src_off, uint64_t runs, uint32_t run_bytes, uint8_t* dst,
+                        hipStream_t s) {
+  if (run_bytes % 16) throw Error{SHELFI_ERR_ARG, "gather: run size not a multiple of 16 bytes"};
+  const uint32_t per = std::max(1u, std::min(16u, run_bytes / (256u * 16u * 4u)));
+  for (uint64_t j0 = 0; j0 < runs; j0 += 65535) {  // grid.y <= 65535
+    const uint32_t nj = (uint32_t)std::min<uint64_t>(65535, runs - j0);
+    hipLaunchKernelGGL(gather_runs_kernel, dim3(per, nj), dim3(256), 0, s, raw, src_off + j0, run_bytes,
+                       dst + j0 * run_bytes);
+    SHELFI_HIP(hipGetLastError());
+  }
+}
+
 // Rows per wavg block: with C <= 8 learners a one-row thread has only C 16-byte loads in
 // flight; the kernel then takes 2 rows.  Measured in one process per shape (tools/wavg_rows_ab.py,
 // profiles/probes/r03_wavg_rows_ab.txt).  SHELFI_WAVG_ROWS=1|2 forces one (A/B probe switch).

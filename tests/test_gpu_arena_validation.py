@@ -96,6 +96,35 @@ def test_valid_blobs_aggregate_like_the_bytes_api(c2):
     assert np.array_equal(got, ref)
 
 
+def test_arena_output_is_placed_once_and_reused(c2):
+    """Arena.output(): the arena's own aggregate buffer, picked once among timed candidates (round 5,
+    VERDICT r4 item 8) and returned again on later calls; wavg into it gives the same bytes as into a
+    fresh buffer, for every candidate count (0 = a plain buffer) and with a caller's buffer included."""
+    B = c2.info()["batch"]
+    blobs = [c2.encrypt(x) for x in _xs(3, K * B - 5, seed=50)]
+    w = [0.2, 0.3, 0.5]
+    ar = D.Arena(c2, 3, K, layout="packed")
+    for i, b in enumerate(blobs):
+        ar.put(i, b)
+    ref = ar.wavg(w)
+    o = ar.output(candidates=3)
+    assert o.shape == ref.shape and o.dtype == torch.int64 and o.is_contiguous()
+    assert ar.output() is o and len(ar.output_placement) == 3
+    assert torch.equal(ar.wavg(w, out=o), ref)
+    ar2 = D.Arena(c2, 3, K, layout="packed")
+    for i, b in enumerate(blobs):
+        ar2.put(i, b)
+    mine = torch.empty_like(ref)
+    assert ar2.output(candidates=0, include=[mine]) is mine
+    assert torch.equal(ar2.wavg(w, out=ar2.output()), ref)
+    ar3 = D.Arena(c2, 3, K, layout="packed")
+    ar3.put(0, blobs[0])  # the other slots never put: candidates are still timed (garbage sums)
+    assert ar3.output(candidates=2).shape == ref.shape
+    ar.release()
+    with pytest.raises(ValueError, match="released"):
+        ar.output()
+
+
 def test_same_k_blob_of_smaller_parameters_is_refused_before_any_copy(c2, c1):
     """A 2^13/L2 blob of K ciphertexts is 8x smaller than a 2^15/L4 slot of K: refused by
     its header (SHELFI_ERR_FORMAT) with the blob ending at a guard page, so any read past

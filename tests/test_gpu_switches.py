@@ -30,6 +30,7 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_ENC_VT", "0"),          # v's columns pass in enc_cols_fused, not table sums in the blocks pass
     ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
     ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
+    ("SHELFI_CRT_SWZ", "0"),         # ntt_inv_cols_crt's padded LDS rows
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
     ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
     ("SHELFI_ENC_TS", "0"),          # one column per thread over every tower (K = 7 defaults to one wave per tower)
@@ -89,11 +90,13 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
     assert torch.equal(got, ref), var
 
 
-@pytest.mark.parametrize("wire", ["shelfi", "packed"])
-def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire):
-    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default chunk (128 MiB of
-    input per learner group: one chunk here) and forced to one ciphertext per chunk (9 chunks through
-    the two device buffer sets): the same aggregate, byte for byte."""
+@pytest.mark.parametrize("wire", ["palisade", "shelfi", "packed"])
+@pytest.mark.parametrize("mode", ["chunk1", "ring", "ring_chunk1"])
+def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
+    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (direct uploads, 512 MiB of
+    input per learner group: one chunk here) against one ciphertext per chunk (7 chunks through the two
+    device buffer sets), the pinned staging ring (SHELFI_H2D_DIRECT=0), and both: the same aggregate, byte
+    for byte, in every wire format (archives take the raw-range + device gather path)."""
     ck, x, _, _ = ctx
     xs = x.cpu().numpy()
     ck.set_wire_format(wire)
@@ -101,9 +104,11 @@ def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire):
         blobs = [ck.encrypt(xs * (i + 1) / 4) for i in range(3)]
         w = [0.5, 0.25, 0.25]
         ref = ck.computeWeightedAverage(blobs, w)
-        set_switch(monkeypatch, "SHELFI_WAVG_CHUNK_MIB", "1")
+        if mode in ("chunk1", "ring_chunk1"):
+            set_switch(monkeypatch, "SHELFI_WAVG_CHUNK_MIB", "1")
+        if mode in ("ring", "ring_chunk1"):
+            set_switch(monkeypatch, "SHELFI_H2D_DIRECT", "0")
         got = ck.computeWeightedAverage(blobs, w)
     finally:
         ck.set_wire_format("palisade")
     assert got == ref
-

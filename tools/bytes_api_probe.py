@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Bytes-API aggregation (computeWeightedAverage of 16 learners x 64 cts at 2^15 / L4: what
-benchmark.py:506-518 times) per wire format and staging-pool setting, plus the raw H2D rates on this
-box (pinned and pageable, torch) and its NUMA layout.  Each setting gets a fresh context (the
-staging pool reads SHELFI_COPY_THREADS / SHELFI_H2D_COPY_THREADS when it is built); SHELFI_STAGE_TRACE=1
-makes the library print fill / wait / drain times to stderr.  Prints JSON lines.
+benchmark.py:506-518 times) per wire format and upload setting (round 5: direct pageable uploads by
+default, SHELFI_H2D_DIRECT=0 the pinned staging ring; SHELFI_WAVG_CHUNK_MIB), plus the raw H2D rates on
+this box (pinned and pageable, torch) and its NUMA layout.  Each setting gets a fresh context (switches
+are read when it is created); SHELFI_STAGE_TRACE=1 makes the library print fill / wait / drain times to
+stderr.  Prints JSON lines.
     python tools/bytes_api_probe.py"""
 import glob
 import json
@@ -69,17 +70,16 @@ def main():
         base.set_wire_format(fmt)
         inputs[fmt] = [base.encrypt(x) for _ in range(Cl)]
     w = [1.0 / Cl] * Cl
-    settings = [("default", {}), ("copy16", {"SHELFI_COPY_THREADS": "16"}),
-                ("h2d8", {"SHELFI_H2D_COPY_THREADS": "8"}), ("copy16_h2d8", {"SHELFI_COPY_THREADS": "16",
-                                                                         "SHELFI_H2D_COPY_THREADS": "8"}),
-                ("h2d2", {"SHELFI_H2D_COPY_THREADS": "2"})]
+    settings = [("default", {}), ("ring", {"SHELFI_H2D_DIRECT": "0"}),
+                ("direct_chunk256", {"SHELFI_WAVG_CHUNK_MIB": "256"}),
+                ("direct_chunk1024", {"SHELFI_WAVG_CHUNK_MIB": "1024"})]
     for name, env in settings:
-        for k in ("SHELFI_COPY_THREADS", "SHELFI_H2D_COPY_THREADS"):
+        for k in ("SHELFI_COPY_THREADS", "SHELFI_H2D_COPY_THREADS", "SHELFI_H2D_DIRECT", "SHELFI_WAVG_CHUNK_MIB"):
             os.environ.pop(k, None)
         os.environ.update(env)
         ck = m.CKKS("ckks", B, 52, d, multDepth=3)
         ck.loadCryptoParams()
-        for fmt in ("palisade", "shelfi", "packed") if name == "default" else ("palisade",):
+        for fmt in ("palisade", "shelfi", "packed") if name in ("default", "ring") else ("palisade",):
             blobs = inputs[fmt]
             nb = sum(len(b) for b in blobs)
             ck.computeWeightedAverage(blobs, w)

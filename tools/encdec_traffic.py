@@ -14,34 +14,39 @@ import statistics
 
 ENCRYPT = ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
            "ntt_fwd_blocks_enc")
-_DEC_COMMON = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel",
-               "fft_fwd_cols")
-# the decode FFT's first pass is a template over FLOOD: fft_fwd_blocks<FLOOD> (LDS loops) or
-# fft_fwd_blocks_ct<BL, K1..K4, FLOOD, SWZ> (register chunks, the default since round 3; SWZ since
-# round 4).  The exact decrypt counts the FLOOD = false instantiations, the flooded one the true ones
-# plus the sigma pass.
-DECRYPT = _DEC_COMMON + ("fft_fwd_blocks@false",)
-DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks@true", "decode_stats_kernel", "decode_flood_kernel")
+_DEC_COMMON = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel")
+# the decode FFT's passes as templates over FLOOD.  Since round 5 the noise is added in the last pass:
+# fft_fwd_cols<LOGR, FLOOD> (or fft_fwd_blocks<FLOOD> when one pass is the whole FFT), and the register-
+# chunk first pass fft_fwd_blocks_ct<BL, K1..K4, SWZ> serves both chains.  Rounds 3-4 profiles carry
+# fft_fwd_blocks_ct<BL, K1..K4, FLOOD, SWZ> and a flag-less fft_fwd_cols<LOGR> shared by both.
+DECRYPT = _DEC_COMMON + ("fft_fwd_blocks@false", "fft_fwd_cols@false")
+DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks@true", "fft_fwd_cols@true", "decode_stats_kernel",
+                                 "decode_flood_kernel")
 
 
 def flood_arg(full):
-    """The FLOOD template argument of a decode-FFT first pass ('true' / 'false'), else None:
-    the first argument of fft_fwd_blocks<...>, the sixth of fft_fwd_blocks_ct<...>."""
+    """The FLOOD template argument of a decode-FFT pass ('true' / 'false'), 'any' for a pass both
+    chains run, else None."""
     head = full.split("(")[0].strip()
     if "<" not in head:
         return None
     name, args = head[:head.index("<")], [a.strip() for a in head[head.index("<") + 1:head.rindex(">")].split(",")]
     if name == "fft_fwd_blocks" and args:
         return args[0]
-    if name == "fft_fwd_blocks_ct" and len(args) >= 6:
-        return args[5]
+    if name == "fft_fwd_blocks_ct":
+        return args[5] if len(args) >= 7 else "any"
+    if name == "fft_fwd_cols":
+        return args[1] if len(args) >= 2 else "any"
     return None
 
 
 def _matches(full, n):
-    """`fft_fwd_blocks@flag`: a decode-FFT first pass whose FLOOD argument is flag; else a prefix."""
+    """`fft_fwd_blocks@flag`: a decode-FFT pass (fft_fwd_blocks, fft_fwd_blocks_ct, fft_fwd_cols) whose
+    FLOOD argument is flag or that both chains run; else a prefix."""
     if "@" in n:
-        return flood_arg(full) == n.split("@")[1]
+        f = flood_arg(full)
+        return f is not None and (f == n.split("@")[1] or f == "any") and \
+            full.startswith(n.split("@")[0][:len("fft_fwd_")])
     return full.startswith(n) or n in full
 
 

@@ -87,16 +87,41 @@ tail[:aw].copy_(arena.buf)
 for p in pads:
     places.append(("tail+%d" % p, tail.data_ptr(), tail.data_ptr() + aw * 8 + p))
 torch.cuda.synchronize()
+def fill_ms(out_ptr):
+    """write-only rate of the placement: torch fill_ of a [K][2][L][N] view at out_ptr"""
+    views = {plain.data_ptr(): plain}
+    if pool.data_ptr() <= out_ptr < pool.data_ptr() + pool_words * 8:
+        o = (out_ptr - pool.data_ptr()) // 8
+        v = pool[o:o + out_words]
+    elif tail.data_ptr() <= out_ptr < tail.data_ptr() + tail.numel() * 8:
+        o = (out_ptr - tail.data_ptr()) // 8
+        v = tail[o:o + out_words]
+    else:
+        v = views[out_ptr]
+    v.fill_(0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.launches):
+        v.fill_(0)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / a.launches
+
+
 res = {lbl: [] for lbl, _, _ in places}
+fills = {lbl: [] for lbl, _, _ in places}
 for r in range(a.rounds):
     for lbl, bp, op in (places if r % 2 == 0 else places[::-1]):
         res[lbl].append(time_ms(bp, op))
+        fills[lbl].append(fill_ms(op))
 med = {lbl: sorted(v)[len(v) // 2] for lbl, v in res.items()}
 best = min(med.values())
 ptrs = {lbl: (bp, op) for lbl, bp, op in places}
 for lbl, v in med.items():
     bp, op = ptrs[lbl]
-    print(json.dumps({"place": lbl, "ms": round(v, 4), "vs_best": round(v / best, 4), "arena_va": hex(bp),
+    fm = sorted(fills[lbl])[len(fills[lbl]) // 2]
+    print(json.dumps({"place": lbl, "ms": round(v, 4), "vs_best": round(v / best, 4),
+                      "fill_ms": round(fm, 4), "fill_TBps": round(out_words * 8 / fm / 1e9, 2), "arena_va": hex(bp),
                       "out_va": hex(op), "out_minus_arena_gib": round((op - bp) / (1 << 30), 4)}))
 print(json.dumps({"summary": True, "best_ms": round(best, 4), "plain_ms": round(med["plain"], 4),
                   "tail0_ms": round(med["tail+0"], 4), "arena_bytes": aw * 8, "out_bytes": out_words * 8,
