@@ -591,6 +591,7 @@ void reload_switches() {
   s.xcd_order = env_flag("SHELFI_XCD_ORDER", '0', true);
   s.ntt_wl = env_flag("SHELFI_NTT_WL", '0', true);
   s.fft_ct = env_flag("SHELFI_FFT_CT", '0', true);
+  s.fft_whole = env_flag("SHELFI_FFT_WHOLE", '0', true);
   s.enc_fused = env_flag("SHELFI_ENC_FUSED_COLS", '0', true);
   s.enc_pp = env_flag("SHELFI_ENC_PP", '0', true);
   s.dec_pp = env_flag("SHELFI_DEC_PP", '0', true);

@@ -1095,6 +1095,127 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __re
   fft_chunk<BL, K4, 0, false>(tw, lds_ld, [&](uint32_t j, double2 v) { g[j] = v; });
 }
 
+// Whole-vector FFT passes (round 5): one 1024-thread workgroup per ciphertext at 2^14 slots holds the
+// vector in registers (16 complex values per thread), so the columns and blocks passes share one
+// launch and the [K][S] intermediate never goes through HBM (encode: 1.18 -> 0.39 MB per ciphertext;
+// decode: 0.92 -> 0.39).  The same butterflies on the same operands as fft_inv_cols<4> +
+// fft_inv_blocks_ct<10, ...> (fft_fwd_blocks_ct<10, ...> + fft_fwd_cols<4>): bit-identical outputs.
+// Rows <-> blocks go through LDS one component at a time (16 x 1024 doubles = 128 KiB, one workgroup
+// per CU); inside a block, a wave exchanges its own 1024 elements (8 KiB) with no workgroup barrier.
+// LDS rows padded by one double per 32 (fft_wpad): at most 2-way conflicts for the three set shapes used
+// (elements 4 s + m, 64 (s >> 2) + (s & 3) + 4 m, s + 64 m; none for the last, which the row <-> block
+// transposes use), counted with the ds_read_b64 / ds_write_b64 lane groups of MI355X_MICROARCH.md §LDS.
+// Unlike an XOR swizzle the padding keeps each thread's 16 addresses at compile-time offsets from one
+// base (an XOR swizzle's 32 live addresses spilled under the 128-VGPR cap of 1024-thread workgroups).
+constexpr uint32_t kFftWholeLogS = 14;
+constexpr uint32_t kFftWholeRow = 1056;  // padded doubles per 1024-element block
+__device__ __forceinline__ uint32_t fft_wpad(uint32_t e) { return e + (e >> 5); }
+
+// A wave's exchange inside its block's 1024 elements: a[m] (at padded block position P(m)) -> a[m] (at
+// Q(m)), real parts first, then imaginary parts, through the wave's LDS slice.  P and Q return padded
+// positions as one per-lane base plus a compile-time offset per m (ds_* immediate offsets): the three
+// set shapes, padded (fft_wpad), are
+//   4 s + m, s = l + 64 q:          (4 l + (l >> 3)) + 264 q + m            (fft_wx1)
+//   64 (l >> 2) + (l & 3) + 4 m:    (66 (l >> 2) + (l & 3)) + 4 m + (m >> 3)  (fft_wx2)
+//   l + 64 m:                       (l + (l >> 5)) + 66 m                     (fft_wx3)
+__device__ __forceinline__ uint32_t fft_wx1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
+__device__ __forceinline__ uint32_t fft_wx2(uint32_t l, int m) { return 66 * (l >> 2) + (l & 3) + 4u * m + (m >> 3); }
+__device__ __forceinline__ uint32_t fft_wx3(uint32_t l, int m) { return l + (l >> 5) + 66u * m; }
+template <class PF, class QF>
+__device__ __forceinline__ void fft_wave_xch(double2 (&a)[16], double* __restrict__ Ls, PF P, QF Q) {
+#pragma unroll
+  for (int m = 0; m < 16; ++m) Ls[P(m)] = a[m].x;
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) a[m].x = Ls[Q(m)];
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) Ls[P(m)] = a[m].y;
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) a[m].y = Ls[Q(m)];
+  wave_lds_sync();
+}
+
+// Rows (thread T holds row r's column T in a[r]) <-> blocks (wave w holds block w's element l + 64 m in
+// a[m]) through the workgroup's 16 x 1024-double LDS, one component at a time.  TO_BLOCKS: rows -> blocks.
+template <bool TO_BLOCKS>
+__device__ __forceinline__ void fft_whole_transpose(double2 (&a)[16], double* __restrict__ lds) {
+  const uint32_t T = threadIdx.x, w = T >> 6, l = T & 63;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const double v = part ? a[i].y : a[i].x;
+      if (TO_BLOCKS)
+        lds[i * kFftWholeRow + fft_wpad(T)] = v;
+      else
+        lds[w * kFftWholeRow + fft_wx3(l, i)] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const double v = TO_BLOCKS ? lds[w * kFftWholeRow + fft_wx3(l, i)] : lds[i * kFftWholeRow + fft_wpad(T)];
+      if (part)
+        a[i].y = v;
+      else
+        a[i].x = v;
+    }
+    __syncthreads();
+  }
+}
+
+// FFTSpecialInv (encode) of one 2^14-slot vector per workgroup: x (n doubles, zero-padded) -> buf [K][S].
+__global__ __launch_bounds__(1024) void fft_inv_whole(const double* __restrict__ x, uint64_t n,
+                                                      double2* __restrict__ buf, const double2* __restrict__ tw) {
+  constexpr uint32_t S = 1u << kFftWholeLogS, BLK = 1024;
+  constexpr int R = 16;
+  __shared__ double lds[16 * kFftWholeRow];
+  const uint64_t k = blockIdx.x;
+  const uint32_t T = threadIdx.x, w = T >> 6, l = T & 63;
+  double2 a[R];
+  // columns: DIF stages len S .. S/8 on column T (fft_inv_cols<4>)
+  const double* __restrict__ xk = x + k * S;
+  const uint32_t rem = n > k * S ? (uint32_t)std::min<uint64_t>(n - k * S, S) : 0u;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = T + (uint32_t)r * BLK;
+    a[r] = make_double2(i < rem ? xk[i] : 0.0, 0.0);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    asm volatile("" ::: "memory");  // each stage's twiddle loads stay in the stage (fft_fwd_whole)
+    const uint32_t lenh = (S >> s) >> 1;
+    const int trr = R >> (s + 1);
+#pragma unroll
+    for (int r0 = 0; r0 < R; ++r0) {
+      if ((r0 / trr) % 2) continue;
+      const int r1 = r0 + trr;
+      const double2 W = tw[lenh + T + (uint32_t)(r0 & ((R >> s) - 1)) * BLK];
+      const double2 u = cadd(a[r0], a[r1]);
+      const double2 d = csub(a[r0], a[r1]);
+      a[r0] = u;
+      a[r1] = cmul(d, W);
+    }
+  }
+  fft_whole_transpose<true>(a, lds);
+  // block w: DIF half-sizes 512 .. 64 on set l (elements l + 64 m), 32 .. 4 on set l (elements
+  // 64 (l >> 2) + (l & 3) + 4 m), 2 .. 1 on sets l + 64 q (elements 4 (l + 64 q) + m)
+  double* Ls = lds + w * kFftWholeRow;
+  fft_dif_set<4, 6>(a, l, tw);
+  fft_wave_xch(a, Ls, [&](int m) { return fft_wx3(l, m); }, [&](int m) { return fft_wx2(l, m); });
+  fft_dif_set<4, 2>(a, l & 3, tw);
+  fft_wave_xch(a, Ls, [&](int m) { return fft_wx2(l, m); }, [&](int m) { return fft_wx1(l, m); });
+  double2* __restrict__ g = buf + k * S + (uint64_t)w * BLK;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double2 c[4] = {a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+    fft_dif_set<2, 0>(c, 0u, tw);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) g[4 * (l + 64 * q) + m] = c[m];
+  }
+}
+
 // FFTSpecial (decode): input already bit-reversed by crt_decode's scatter; DIT
 // stages len = 2..S with twiddle ffwd[len/2 + (x mod len)].  Small len in LDS
 // blocks, the top LOGR stages on register columns; the last pass writes the real
@@ -1515,7 +1636,9 @@ static void launch_encode_fft(const Params& p, const DeviceTables& dt, const dou
   const uint32_t blkLog = fft_block_log(logS);
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;
-  if (logR > 0) {
+  if (logS == kFftWholeLogS && switches().fft_whole) {  // one workgroup per vector, no HBM intermediate
+    hipLaunchKernelGGL(fft_inv_whole, dim3((uint32_t)K), dim3(1024), 0, s, x, n, fbuf, dt.fft_inv);
+  } else if (logR > 0) {
     const uint64_t nb = K * ((p.batch >> logR) / 256);
     FFT_DISPATCH(logR, fft_inv_cols, dim3((uint32_t)nb), dim3(256), 0, s, x, n, fbuf, logS,
                  dt.fft_inv);
@@ -2262,7 +2385,6 @@ struct FloodArgs {
   uint32_t* flags;  // [1] |= precision failure, [2] = max logError
 };
 
-// FFTSpecial first pass (decode): input already bit-reversed by the CRT's scatter; DIT
 // Ciphertext k's flooding scale from decode_stats_kernel's partial sums: the noise's standard
 // deviation in slot units (the first block of each ciphertext records the precision failure and
 // logError).
@@ -2442,6 +2564,88 @@ __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ 
   }
 }
 
+// FFTSpecial (decode) of one 2^14-slot vector per workgroup (see fft_inv_whole): buf [K][S] (bit-reversed
+// by the CRT's scatter) -> the real parts of the first n slots in out; FLOOD adds the decode noise as
+// fft_fwd_cols<4, true> does (thread T's 16 rows share ChaCha block T).
+template <bool FLOOD>
+__global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict__ buf, const double2* __restrict__ tw,
+                                                      double* __restrict__ out, uint64_t n, FloodArgs fa) {
+  constexpr uint32_t S = 1u << kFftWholeLogS, BLK = 1024;
+  constexpr int R = 16;
+  __shared__ double lds[16 * kFftWholeRow];
+  const uint64_t k = blockIdx.x;
+  const uint32_t T = threadIdx.x, w = T >> 6, l = T & 63;
+  double2 a[R];
+  // block w: DIT half-sizes 1 .. 2 on sets l + 64 q (elements 4 (l + 64 q) + m), loaded from HBM
+  const double2* __restrict__ g = buf + k * S + (uint64_t)w * BLK;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double2 c[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c[m] = g[4 * (l + 64 * q) + m];
+    fft_dit_set<2, 0>(c, 0u, tw);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a[4 * q + m] = c[m];
+  }
+  double* Ls = lds + w * kFftWholeRow;
+  // (the empty asm statements keep each phase's twiddle loads in that phase: hoisted to the kernel
+  // entry, 33 twiddles would not fit beside the data under the 128-VGPR cap)
+  fft_wave_xch(a, Ls, [&](int m) { return fft_wx1(l, m); }, [&](int m) { return fft_wx2(l, m); });
+  asm volatile("" ::: "memory");
+  fft_dit_set<4, 2>(a, l & 3, tw);  // half-sizes 4 .. 32
+  fft_wave_xch(a, Ls, [&](int m) { return fft_wx2(l, m); }, [&](int m) { return fft_wx3(l, m); });
+  asm volatile("" ::: "memory");
+  fft_dit_set<4, 6>(a, l, tw);  // half-sizes 64 .. 512
+  asm volatile("" ::: "memory");
+  fft_whole_transpose<false>(a, lds);
+  // columns: DIT half-sizes 1024 .. 4096 on column T (fft_fwd_cols<4>); the last stage (8192) computes
+  // only the real parts decrypt returns and stores each pair as it is done (with every output held to the
+  // end, the column pass spilled under the 128-VGPR cap)
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    asm volatile("" ::: "memory");
+    const uint32_t lenh = BLK << s;
+    const int tr = 1 << s;
+#pragma unroll
+    for (int r0 = 0; r0 < R; ++r0) {
+      if ((r0 >> s) & 1) continue;
+      const int r1 = r0 + tr;
+      const double2 W = tw[lenh + T + (uint32_t)(r0 & ((2 << s) - 1)) * BLK];
+      const double2 u = a[r0];
+      const double2 v = cmul(a[r1], W);
+      a[r0] = cadd(u, v);
+      a[r1] = csub(u, v);
+    }
+  }
+  double nso = 0.0;
+  uint64_t wd[8];
+  if (FLOOD) {  // row r of column T: normal r of ChaCha block T (fft_fwd_cols<4, true>)
+    nso = flood_nsd(fa, k, 0u, S) * sqrt((double)S);
+    chacha20_block(fa.key, T, (3ull << 56) | (fa.g0 + k), wd);
+  }
+  // uniform base + 32-bit offsets (16 precomputed 64-bit addresses would not fit)
+  double* __restrict__ ok = out + k * S;
+  const uint32_t rem = n > k * S ? (uint32_t)std::min<uint64_t>(n - k * S, S) : 0u;
+#pragma unroll
+  for (int r0 = 0; r0 < R / 2; ++r0) {
+    asm volatile("" ::: "memory");
+    const int r1 = r0 + R / 2;
+    const double2 W = tw[(BLK << 3) + T + (uint32_t)r0 * BLK];
+    const double vx = __dsub_rn(__dmul_rn(a[r1].x, W.x), __dmul_rn(a[r1].y, W.y));  // cmul(a[r1], W).x
+    double o0 = __dadd_rn(a[r0].x, vx), o1 = __dsub_rn(a[r0].x, vx);
+    if (FLOOD) {  // rows r0 (normal r0 of the block: word r0 / 2) and r0 + 8 (word 4 + r0 / 2)
+      double z0, z1, z2, z3;
+      flood_pair(wd[r0 >> 1], z0, z1);
+      flood_pair(wd[4 + (r0 >> 1)], z2, z3);
+      o0 = __dadd_rn(o0, __dmul_rn(nso, (r0 & 1) ? z1 : z0));
+      o1 = __dadd_rn(o1, __dmul_rn(nso, (r0 & 1) ? z3 : z2));
+    }
+    const uint32_t i0 = T + (uint32_t)r0 * BLK, i1 = T + (uint32_t)r1 * BLK;
+    if (i0 < rem) ok[i0] = o0;
+    if (i1 < rem) ok[i1] = o1;
+  }
+}
+
 static uint32_t flood_groups(uint32_t S) {
   const uint32_t half = S / 2;
   return half >= kFloodPairsPerWg ? half / kFloodPairsPerWg : 1;
@@ -2554,6 +2758,14 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                          fa.two_p, fa.p_bits, fa.m_factor, fa.key, fa.g0, fa.flags);
     }
     SHELFI_HIP(hipGetLastError());
+  }
+  if (logS == kFftWholeLogS && switches().fft_whole) {  // one workgroup per vector, no HBM intermediate
+    if (fused_flood)
+      hipLaunchKernelGGL(fft_fwd_whole<true>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n, fa);
+    else
+      hipLaunchKernelGGL(fft_fwd_whole<false>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n, fa);
+    SHELFI_HIP(hipGetLastError());
+    return;
   }
   const bool fct = flogR > 0 && (fblkLog == 10 || fblkLog == 11) && switches().fft_ct;
   const dim3 fg((uint32_t)(K << flogR));

@@ -61,6 +61,7 @@ struct Switches {
   bool xcd_order = true;       // SHELFI_XCD_ORDER=0: natural block order in the NTT block passes
   bool ntt_wl = true;          // SHELFI_NTT_WL=0: a workgroup barrier at every block-pass exchange
   bool fft_ct = true;          // SHELFI_FFT_CT=0: LDS-loop FFT block passes
+  bool fft_whole = true;       // SHELFI_FFT_WHOLE=0: separate columns / blocks FFT passes at 2^14 slots
   bool enc_fused = true;       // SHELFI_ENC_FUSED_COLS=0: enc_prep_kernel + three column passes
   bool enc_pp = true;          // SHELFI_ENC_PP=0: one-shot encrypt block pass
   bool dec_pp = true;          // SHELFI_DEC_PP=0: one-shot decrypt block pass

@@ -23,6 +23,7 @@ from SHELFI_FHE import device as D  # noqa: E402
 ENC_DEC_SWITCHES = [
     ("SHELFI_NTT_WL", "0"),          # workgroup barrier at every block-pass exchange
     ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
+    ("SHELFI_FFT_WHOLE", "0"),       # separate columns / blocks FFT passes at 2^14 slots
     ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
     ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
     ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
