@@ -767,10 +767,15 @@ def main():
 
         def api_sample(blobs):
             ck.computeWeightedAverage(blobs, weights)  # warm (allocates staging)
+            # every result is kept until the clock stops, as benchmark.py:506-514 keeps each key's
+            # aggregate in eval_data (freeing a 134 MB bytes object inside the loop cost ~8 ms a call)
+            kept = []
             t0 = time.perf_counter()
             for _ in range(reps):
-                res_b = ck.computeWeightedAverage(blobs, weights)
+                kept.append(ck.computeWeightedAverage(blobs, weights))
             dt = (time.perf_counter() - t0) / reps
+            res_b = kept[-1]
+            del kept
             ck.decrypt(res_b, Ka * batch)  # warm
             t0 = time.perf_counter()
             for _ in range(reps):

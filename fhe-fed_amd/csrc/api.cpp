@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -722,6 +723,8 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     free_tables(ctx);
     delete ctx->stage;
     ctx->stage = nullptr;
+    delete ctx->drain;
+    ctx->drain = nullptr;
     for (int i = 0; i < shelfi_ctx::kWeightRing; ++i) {
       if (ctx->wl_done[i]) (void)hipEventSynchronize(ctx->wl_done[i]);
       if (ctx->wl_done[i]) (void)hipEventDestroy(ctx->wl_done[i]);
@@ -1312,8 +1315,23 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   // A: H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
+  if (direct && !ctx->drain) ctx->drain = new AsyncDrain(default_copy_threads());
+  struct DrainGuard {  // on an error: the worker finishes what was posted before the streams go away
+    AsyncDrain* d;
+    bool armed;
+    ~DrainGuard() {
+      if (armed && d) try {
+          d->finish();
+        } catch (...) {
+        }
+    }
+  } dg{ctx->drain, direct};
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
+  using clk = std::chrono::steady_clock;
+  const bool trace = sr.s.trace();
+  const auto t_start = clk::now();
+  double t_up = 0.0, t_wait = 0.0;  // SHELFI_STAGE_TRACE: host seconds in the direct uploads / tab waits
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
@@ -1321,7 +1339,11 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       const size_t gc = std::min(group, C - c0);
       if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
       uint64_t* tabh = raw ? ctx->gather_host + b * runs_cap : nullptr;
-      if (raw && (ci >= 2 || c0 > 0)) SHELFI_HIP(hipEventSynchronize(pp.in_ready[b]));  // tabh's last copy done
+      if (raw && (ci >= 2 || c0 > 0)) {  // tabh's last copy done
+        const auto t0 = clk::now();
+        SHELFI_HIP(hipEventSynchronize(pp.in_ready[b]));
+        if (trace) t_wait += std::chrono::duration<double>(clk::now() - t0).count();
+      }
       uint64_t runs = 0;
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
@@ -1333,8 +1355,9 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
           const size_t span = (size_t)(pcs.back().p + pcs.back().n - lo);
           if (raw)
             for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
+          const auto t0 = clk::now();
           SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
-          sr.s.poll();  // drain finished sums while the uploads run
+          if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
         } else {
           sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
         }
@@ -1369,14 +1392,31 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         }
         SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
         dst.pieces(k0, kn, p, pcs);
-        sr.s.d2hv(pcs.data(), pcs.size(), pout ? poutb[b] : outb[b], pp.c);
-        SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+        const uint8_t* sum = pout ? poutb[b] : outb[b];
+        if (direct) {  // one DMA into the drain's pinned buffer; its worker scatters it to the pieces
+          size_t nbytes = 0;
+          for (const HostPiece& h : pcs) nbytes += h.n;
+          uint8_t* hb = ctx->drain->buffer(b, nbytes);  // waits until chunk ci - 2 is drained
+          SHELFI_HIP(hipMemcpyAsync(hb, sum, nbytes, hipMemcpyDeviceToHost, pp.c));
+          SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+          ctx->drain->post(b, pp.out_free[b], pcs);
+        } else {
+          sr.s.d2hv(pcs.data(), pcs.size(), sum, pp.c);
+          SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+        }
       }
-      sr.s.poll();
+      if (!direct) sr.s.poll();
     }
   }
+  const auto t_issued = clk::now();
+  if (direct) ctx->drain->finish();
   sr.finish();
   pp.sync();
+  if (trace)
+    std::fprintf(stderr, "[wavg-bytes] %s chunks %llu x %llu cts: issue %.2f ms (uploads %.2f, tab waits %.2f), "
+                 "tail %.2f ms\n", direct ? (raw ? "direct+gather" : "direct") : "ring", (unsigned long long)nchunks,
+                 (unsigned long long)kc, std::chrono::duration<double>(t_issued - t_start).count() * 1e3, t_up * 1e3,
+                 t_wait * 1e3, std::chrono::duration<double>(clk::now() - t_issued).count() * 1e3);
   uint32_t flag = 0;
   SHELFI_HIP(hipMemcpy(&flag, bad, 4, hipMemcpyDeviceToHost));
   if (flag) throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed learner data)"};

@@ -327,4 +327,84 @@ void Stager::abort() noexcept {
   pending_.clear();
 }
 
+// ------------------------------------------------------------ AsyncDrain ----
+AsyncDrain::AsyncDrain(int threads) : pool_(threads) { worker_ = std::thread([this] { run(); }); }
+
+AsyncDrain::~AsyncDrain() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+  for (int i = 0; i < 2; ++i)
+    if (buf_[i]) (void)hipHostFree(buf_[i]);
+}
+
+uint8_t* AsyncDrain::buffer(int slot, size_t bytes) {
+  wait_slot(slot);
+  if (cap_[slot] < bytes) {
+    if (buf_[slot]) SHELFI_HIP(hipHostFree(buf_[slot]));
+    buf_[slot] = nullptr;
+    cap_[slot] = 0;
+    SHELFI_HIP(hipHostMalloc((void**)&buf_[slot], bytes, hipHostMallocDefault));
+    cap_[slot] = bytes;
+  }
+  return buf_[slot];
+}
+
+void AsyncDrain::wait_slot(int slot) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return busy_[slot] == 0; });
+}
+
+void AsyncDrain::post(int slot, hipEvent_t ev, std::vector<HostPiece> pieces) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++busy_[slot];
+    q_.push_back(Job{slot, ev, std::move(pieces)});
+  }
+  cv_.notify_all();
+}
+
+void AsyncDrain::finish() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return busy_[0] == 0 && busy_[1] == 0; });
+  if (!err_.empty()) {
+    const std::string e = err_;
+    err_.clear();
+    throw Error{SHELFI_ERR_DEVICE, e};
+  }
+}
+
+void AsyncDrain::run() {
+  std::vector<CopyJob> jobs;
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stop_ with nothing left
+      j = std::move(q_.front());
+      q_.pop_front();
+    }
+    const hipError_t e = hipEventSynchronize(j.ev);
+    if (e == hipSuccess) {
+      jobs.clear();
+      size_t off = 0;
+      for (const HostPiece& h : j.pieces) {
+        jobs.push_back(CopyJob{h.p, buf_[j.slot] + off, h.n});
+        off += h.n;
+      }
+      pool_.copy_many(jobs.data(), jobs.size());
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (e != hipSuccess && err_.empty()) err_ = std::string("staged copy: ") + hipGetErrorString(e);
+      --busy_[j.slot];
+    }
+    cv_.notify_all();
+  }
+}
+
 }  // namespace shelfi

@@ -1,13 +1,15 @@
 // Host <-> HBM staging for the bytes API.
 //
-// The bytes API hands over pageable Python buffers.  A DMA from pageable memory makes
-// the HIP runtime copy through its own staging buffer on the calling thread, so
-// hipMemcpyAsync blocks the host and the H2D / compute / D2H pipeline serializes;
-// and a freshly allocated output (a new bytes object) first-touch faults on the copy
-// thread at ~16 GB/s.  The Stager instead owns rings of pinned slots: pageable data
-// is memcpy'd into a slot by a pool of threads (faults spread over the cores) and the
-// slot is DMA'd asynchronously; outputs are DMA'd into pinned slots and drained into
-// the destination by the same pool while later DMAs run.
+// The bytes API hands over pageable Python buffers.  A hipMemcpyAsync from pageable memory
+// returns only once the runtime has moved the data (the calling thread waits), and a freshly
+// allocated output (a new bytes object) first-touch faults on the copy thread at ~16 GB/s.
+// The Stager owns rings of pinned slots: pageable data is memcpy'd into a slot by a pool of
+// threads (faults spread over the cores) and the slot is DMA'd asynchronously; outputs are
+// DMA'd into pinned slots and drained into the destination by the same pool while later DMAs
+// run.  Round 5: for large contiguous uploads the runtime's own pageable path is faster (55.6
+// GB/s in 32 MiB copies vs ~44 through the ring, tools/h2d_pageable_probe.py), so the
+// aggregation uploads directly and drains its outputs on an AsyncDrain worker instead, which
+// keeps the uploading thread free.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -18,6 +20,7 @@
 #include <cstdint>
 #include <deque>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -99,6 +102,7 @@ class Stager {
 
   size_t slot_bytes() const { return slot_bytes_; }
   int threads() const { return pool_.threads(); }
+  bool trace() const { return trace_; }  // SHELFI_STAGE_TRACE=1
 
  private:
   struct Slot {
@@ -135,5 +139,40 @@ void advise_huge(void* p, size_t n);
 // Worker threads for a Stager: SHELFI_COPY_THREADS, else min(8, CPUs this process may use).
 int default_copy_threads();
 int default_h2d_copy_threads();  // SHELFI_H2D_COPY_THREADS, default 4
+
+// Background scatter of device -> host chunks (round 5, the direct-upload aggregation): the caller
+// DMAs a chunk into one of two pinned buffers (buffer(slot)), records an event after it and posts
+// the pieces the chunk goes to; a worker thread waits for the event and copies the buffer into the
+// pieces with its own CopyPool while the caller goes on uploading.  wait_slot() before a buffer is
+// reused; finish() waits for every posted job and rethrows the worker's first error.
+class AsyncDrain {
+ public:
+  explicit AsyncDrain(int threads);
+  ~AsyncDrain();
+  AsyncDrain(const AsyncDrain&) = delete;
+  AsyncDrain& operator=(const AsyncDrain&) = delete;
+  uint8_t* buffer(int slot, size_t bytes);  // pinned; grown (the slot must be idle)
+  void wait_slot(int slot);
+  void post(int slot, hipEvent_t ev, std::vector<HostPiece> pieces);
+  void finish();
+
+ private:
+  void run();
+  struct Job {
+    int slot;
+    hipEvent_t ev;
+    std::vector<HostPiece> pieces;
+  };
+  CopyPool pool_;
+  std::thread worker_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  bool stop_ = false;
+  int busy_[2] = {0, 0};  // posted, not yet drained, per slot
+  uint8_t* buf_[2] = {nullptr, nullptr};
+  size_t cap_[2] = {0, 0};
+  std::string err_;
+};
 
 }  // namespace shelfi

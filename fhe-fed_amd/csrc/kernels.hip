@@ -2388,13 +2388,7 @@ struct FloodArgs {
 // Ciphertext k's flooding scale from decode_stats_kernel's partial sums: the noise's standard
 // deviation in slot units (the first block of each ciphertext records the precision failure and
 // logError).
-__device__ __forceinline__ double flood_nsd(const FloodArgs& fa, uint64_t k, uint32_t b, uint32_t S) {
-  double s1 = 0.0, s2 = 0.0;
-  for (uint32_t g = 0; g < fa.G; ++g) {
-    const double2 v = fa.part[k * fa.G + g];
-    s1 += v.x;
-    s2 += v.y;
-  }
+__device__ __forceinline__ double flood_nsd_sums(const FloodArgs& fa, double s1, double s2, uint32_t b, uint32_t S) {
   const double var = (s2 - s1 * (s1 / (double)S)) / (double)(S - 1);
   double sigma_p = 0.5 * sqrt(var > 0.0 ? var : 0.0) * fa.two_p;
   const bool fail = !(log2(sigma_p) <= fa.p_bits - 5.0);
@@ -2406,6 +2400,15 @@ __device__ __forceinline__ double flood_nsd(const FloodArgs& fa, uint64_t k, uin
     atomicMax((int*)&fa.flags[2], (int)rint(log2(stddev_p * sqrt(2.0 * (double)S))));
   }
   return stddev_p / fa.two_p;
+}
+__device__ __forceinline__ double flood_nsd(const FloodArgs& fa, uint64_t k, uint32_t b, uint32_t S) {
+  double s1 = 0.0, s2 = 0.0;
+  for (uint32_t g = 0; g < fa.G; ++g) {
+    const double2 v = fa.part[k * fa.G + g];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  return flood_nsd_sums(fa, s1, s2, b, S);
 }
 
 // FFTSpecial first pass (decode): input already bit-reversed by the CRT's scatter; DIT
@@ -2564,12 +2567,67 @@ __global__ __launch_bounds__(256) void fft_fwd_cols(const double2* __restrict__ 
   }
 }
 
+// decode_stats_kernel's sums inside the whole-vector decode (round 5): a[i] holds FFT-input position
+// P = 1024 w + 4 (l + 64 (i >> 2)) + (i & 3); pair (P, P ^ (2^h - 1)) (h = P's leading bit, P in the
+// lower half of its octave) contributes a = x.re + y.im and b = x.im + y.re, positions 0 and 1 their
+// own terms.  The partners' components come through LDS (real parts, then imaginary), the sums by a
+// wave shuffle and LDS reduction; every thread returns (sum, sum of squares).
+__device__ __forceinline__ double2 fft_whole_flood_stats(const double2 (&a)[16], double* __restrict__ lds) {
+  const uint32_t T = threadIdx.x, w = T >> 6, l = T & 63;
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lds[w * kFftWholeRow + fft_wx1(l, i)] = part ? a[i].y : a[i].x;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t P = 1024 * w + 4 * (l + 64 * (i >> 2)) + (i & 3);
+      if (P < 2) continue;
+      const uint32_t h = 31 - __clz(P);
+      if ((P >> (h - 1)) & 1) continue;  // upper half of the octave: counted by its partner
+      const uint32_t Q = P ^ ((1u << h) - 1);
+      const double y = lds[(Q >> 10) * kFftWholeRow + fft_wpad(Q & 1023)];
+      const double v = part ? a[i].x + y : a[i].y + y;  // part 0: b = x.im + y.re; part 1: a = x.re + y.im
+      s1 += v;
+      s2 += v * v;
+    }
+    __syncthreads();
+  }
+  if (T == 0) {  // slot 0: 2 im; slot S/2: re + im (positions 0 and 1)
+    const double a0 = 2.0 * a[0].y, c = a[1].x + a[1].y;
+    s1 += a0 + c;
+    s2 += a0 * a0 + c * c;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_down(s1, o, 64);
+    s2 += __shfl_down(s2, o, 64);
+  }
+  if (l == 0) {
+    lds[2 * w] = s1;
+    lds[2 * w + 1] = s2;
+  }
+  __syncthreads();
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    t1 += lds[2 * v];
+    t2 += lds[2 * v + 1];
+  }
+  __syncthreads();  // the LDS is the block exchanges' next
+  return make_double2(t1, t2);
+}
+
 // FFTSpecial (decode) of one 2^14-slot vector per workgroup (see fft_inv_whole): buf [K][S] (bit-reversed
-// by the CRT's scatter) -> the real parts of the first n slots in out; FLOOD adds the decode noise as
-// fft_fwd_cols<4, true> does (thread T's 16 rows share ChaCha block T).
-template <bool FLOOD>
+// by the CRT's scatter) -> the real parts of the first n slots in out.  STATS (flooded decrypts): the
+// workgroup also sums decode_stats_kernel's statistics of its vector (fft_whole_flood_stats) into
+// part[k]; flood_add_kernel then adds the noise to out (adding it here, beside the 16 values per thread,
+// spilled under the 128-VGPR cap and ran slower than the extra pass).
+template <bool STATS>
 __global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict__ buf, const double2* __restrict__ tw,
-                                                      double* __restrict__ out, uint64_t n, FloodArgs fa) {
+                                                      double* __restrict__ out, uint64_t n,
+                                                      double2* __restrict__ part) {
   constexpr uint32_t S = 1u << kFftWholeLogS, BLK = 1024;
   constexpr int R = 16;
   __shared__ double lds[16 * kFftWholeRow];
@@ -2579,10 +2637,14 @@ __global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict_
   // block w: DIT half-sizes 1 .. 2 on sets l + 64 q (elements 4 (l + 64 q) + m), loaded from HBM
   const double2* __restrict__ g = buf + k * S + (uint64_t)w * BLK;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    double2 c[4];
+  for (int i = 0; i < R; ++i) a[i] = g[4 * (l + 64 * (i >> 2)) + (i & 3)];
+  if (STATS) {
+    const double2 st = fft_whole_flood_stats(a, lds);
+    if (T == 0) part[k] = st;
+  }
 #pragma unroll
-    for (int m = 0; m < 4; ++m) c[m] = g[4 * (l + 64 * q) + m];
+  for (int q = 0; q < 4; ++q) {
+    double2 c[4] = {a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
     fft_dit_set<2, 0>(c, 0u, tw);
 #pragma unroll
     for (int m = 0; m < 4; ++m) a[4 * q + m] = c[m];
@@ -2617,12 +2679,6 @@ __global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict_
       a[r1] = csub(u, v);
     }
   }
-  double nso = 0.0;
-  uint64_t wd[8];
-  if (FLOOD) {  // row r of column T: normal r of ChaCha block T (fft_fwd_cols<4, true>)
-    nso = flood_nsd(fa, k, 0u, S) * sqrt((double)S);
-    chacha20_block(fa.key, T, (3ull << 56) | (fa.g0 + k), wd);
-  }
   // uniform base + 32-bit offsets (16 precomputed 64-bit addresses would not fit)
   double* __restrict__ ok = out + k * S;
   const uint32_t rem = n > k * S ? (uint32_t)std::min<uint64_t>(n - k * S, S) : 0u;
@@ -2632,17 +2688,34 @@ __global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict_
     const int r1 = r0 + R / 2;
     const double2 W = tw[(BLK << 3) + T + (uint32_t)r0 * BLK];
     const double vx = __dsub_rn(__dmul_rn(a[r1].x, W.x), __dmul_rn(a[r1].y, W.y));  // cmul(a[r1], W).x
-    double o0 = __dadd_rn(a[r0].x, vx), o1 = __dsub_rn(a[r0].x, vx);
-    if (FLOOD) {  // rows r0 (normal r0 of the block: word r0 / 2) and r0 + 8 (word 4 + r0 / 2)
-      double z0, z1, z2, z3;
-      flood_pair(wd[r0 >> 1], z0, z1);
-      flood_pair(wd[4 + (r0 >> 1)], z2, z3);
-      o0 = __dadd_rn(o0, __dmul_rn(nso, (r0 & 1) ? z1 : z0));
-      o1 = __dadd_rn(o1, __dmul_rn(nso, (r0 & 1) ? z3 : z2));
-    }
     const uint32_t i0 = T + (uint32_t)r0 * BLK, i1 = T + (uint32_t)r1 * BLK;
-    if (i0 < rem) ok[i0] = o0;
-    if (i1 < rem) ok[i1] = o1;
+    if (i0 < rem) ok[i0] = __dadd_rn(a[r0].x, vx);
+    if (i1 < rem) ok[i1] = __dsub_rn(a[r0].x, vx);
+  }
+}
+
+// The decode noise of a flooded whole-vector decode, added to the decoded outputs (fft_fwd_cols<LOGR,
+// true>'s stream: slot i takes normal i div S/16 of ChaCha20 block i mod S/16): one thread per (ciphertext,
+// block), 16 outputs each; sigma from the workgroup sums of fft_fwd_whole<true> (FloodArgs::part, G = 1).
+__global__ __launch_bounds__(256) void flood_add_kernel(double* __restrict__ out, uint64_t n, uint32_t logS,
+                                                        uint64_t K, FloodArgs fa) {
+  const uint32_t S = 1u << logS, S16 = S >> 4;
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= K * S16) return;
+  const uint64_t k = t / S16;
+  const uint32_t b = (uint32_t)(t % S16);
+  const double nso = flood_nsd(fa, k, b == 0 ? 0u : 1u, S) * sqrt((double)S);  // b == 0 records the flags
+  uint64_t wd[8];
+  chacha20_block(fa.key, b, (3ull << 56) | (fa.g0 + k), wd);
+  double* __restrict__ ok = out + k * S;
+  const uint32_t rem = n > k * S ? (uint32_t)std::min<uint64_t>(n - k * S, S) : 0u;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    double z0, z1;
+    flood_pair(wd[m], z0, z1);
+    const uint32_t i0 = b + S16 * (2 * m), i1 = i0 + S16;
+    if (i0 < rem) ok[i0] = __dadd_rn(ok[i0], __dmul_rn(nso, z0));
+    if (i1 < rem) ok[i1] = __dadd_rn(ok[i1], __dmul_rn(nso, z1));
   }
 }
 
@@ -2737,6 +2810,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const size_t lds = sizeof(double2) << fblkLog;
   FloodArgs fa{};
   bool fused_flood = false;
+  const bool whole = logS == kFftWholeLogS && switches().fft_whole;  // fft_fwd_whole
   if (dn && dn->enabled) {
     for (int i = 0; i < 8; ++i) fa.key.k[i] = dn->key[i];
     fa.two_p = ldexp(1.0, (int)dn->p_bits);
@@ -2746,7 +2820,9 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     fa.flags = dn->flags;
     fa.logN = p.logN;
     fused_flood = p.batch >= 64;  // decode_flood_kernel below 2^6 slots
-    if (fused_flood) {
+    if (fused_flood && whole) {  // fft_fwd_whole<true> sums its own statistics
+      if (dn->reset) SHELFI_HIP(hipMemsetAsync(dn->flags + 1, 0, 8, s));
+    } else if (fused_flood) {
       fa.G = flood_groups(p.batch);
       double2* part = fbuf + K * (uint64_t)p.batch;
       fa.part = part;
@@ -2759,11 +2835,19 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     }
     SHELFI_HIP(hipGetLastError());
   }
-  if (logS == kFftWholeLogS && switches().fft_whole) {  // one workgroup per vector, no HBM intermediate
-    if (fused_flood)
-      hipLaunchKernelGGL(fft_fwd_whole<true>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n, fa);
-    else
-      hipLaunchKernelGGL(fft_fwd_whole<false>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n, fa);
+  if (whole) {  // one workgroup per vector, no HBM intermediate
+    if (fused_flood) {
+      double2* part = fbuf + K * (uint64_t)p.batch;  // [K] sums (G = 1)
+      fa.part = part;
+      fa.G = 1;
+      hipLaunchKernelGGL(fft_fwd_whole<true>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n, part);
+      SHELFI_HIP(hipGetLastError());
+      const uint64_t th = K * (p.batch >> 4);
+      hipLaunchKernelGGL(flood_add_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, s, out, n, logS, K, fa);
+    } else {
+      hipLaunchKernelGGL(fft_fwd_whole<false>, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, dt.fft_fwd, out, n,
+                         (double2*)nullptr);
+    }
     SHELFI_HIP(hipGetLastError());
     return;
   }

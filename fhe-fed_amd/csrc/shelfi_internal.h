@@ -196,6 +196,7 @@ struct DeviceKeys {
 
 namespace shelfi {
 class Stager;
+class AsyncDrain;
 struct EvalState;  // eval.cpp: relinearization key + per-level tables
 }
 
@@ -207,6 +208,7 @@ struct shelfi_ctx {
   hipStream_t stream2 = nullptr;  // compute stream of the pipelined bytes API
   hipStream_t stream3 = nullptr;  // copy-out stream of the pipelined bytes API
   shelfi::Stager* stage = nullptr;  // pinned staging rings (host_stage.h), lazily created
+  shelfi::AsyncDrain* drain = nullptr;  // background output scatter of the direct-upload aggregation
   shelfi::DeviceTables dt;
   shelfi::DeviceKeys dk;
   std::vector<uint64_t> pk_host, sk_host;
