@@ -601,7 +601,6 @@ void reload_switches() {
   s.enc_vt = env_flag("SHELFI_ENC_VT", '0', true);
   s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
   s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
-  s.crt_swz = env_flag("SHELFI_CRT_SWZ", '0', true);
   if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;
   s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
   s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);
@@ -1264,11 +1263,13 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   const bool direct = switches().h2d_direct;
-  // chunk of input per learner-group buffer: direct uploads want >= 32 MiB per copy (8 MiB copies
-  // ran 51.6 GB/s, 2 MiB 41.3), so 512 MiB per 16 learners; through the ring ~128 MiB (round 4:
-  // 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x 64 cts,
-  // profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
-  const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 512 : 128;
+  // chunk of input per learner-group buffer: direct uploads want ~32 MiB per copy (8 MiB copies ran
+  // 51.6 GB/s, 2 MiB 41.3, 32 MiB 55.6), and the last chunk's wavg + D2H + drain is the call's tail,
+  // so 32 MiB per learner (512 MiB for 16 learners: 16 / 32 per learner ran 52.4 / 52.2 GB/s, 64 MiB
+  // 51.6, profiles/r05k); through the ring ~128 MiB per group (round 4: 32 / 64 / 128 / 256 MiB ran
+  // 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x 64 cts, profiles/r04w/api_chunk.txt);
+  // SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
+  const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 32 * group : 128;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;

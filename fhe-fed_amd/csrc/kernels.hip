@@ -2109,13 +2109,12 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
 // CRT-reconstructed exactly as crt_decode_kernel does (same operation order) and stored
 // at bitrev(slot).  Needs L R 512 B of LDS <= kCrtFuseLds and gap = N / 2S <= 64.
 // LDS rows: the CRT loop reads ys[t][r][u] with r fastest (8 consecutive lanes = 8 rows, 4
-// consecutive u per 32-lane ds_read_b64 group); rows of 64 u64 put those 8 rows on one bank.
-// SWZ (round 5): rows of 64 with column u stored at u ^ 4 (r mod 8) -- 32 distinct banks per
-// group, L R 512 B (32 KiB at 2^15 / L4: 5 workgroups per CU); else rows padded to 68 u64
-// (34 KiB, 4 per CU).
+// consecutive u per 32-lane ds_read_b64 group); rows of 64 u64 would put those 8 rows on one bank.
+// Round 5: column u is stored at u ^ 4 (r mod 8) -- 32 distinct banks per group in L R 512 B (32 KiB
+// at 2^15 / L4, 5 workgroups per CU; the round-4 rows padded to 68 u64 ran the same, 0.960 vs 0.959
+// us per decrypted ciphertext, profiles/r05d).
 constexpr size_t kCrtFuseLds = 48 << 10;
-constexpr int kCrtRowStride = 68;  // u64 per LDS row of ntt_inv_cols_crt<LOGR, false> (64 columns + 4)
-template <int LOGR, bool SWZ>
+template <int LOGR>
 __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restrict__ dbuf, uint32_t L,
                                                         uint32_t logN, uint32_t logS,
                                                         const uint64_t* __restrict__ tw,
@@ -2123,10 +2122,10 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
                                                         const TowerConst* __restrict__ tcs, uint64_t Qlo,
                                                         uint64_t Qhi, double inv_scale,
                                                         double2* __restrict__ fbuf) {
-  constexpr int R = 1 << LOGR, CW = 64, CWP = SWZ ? 64 : kCrtRowStride;
+  constexpr int R = 1 << LOGR, CW = 64, CWP = 64;
   extern __shared__ uint64_t ys_flat[];  // [L][R][CWP]
   uint64_t(*ys)[R][CWP] = reinterpret_cast<uint64_t(*)[R][CWP]>(ys_flat);
-  const auto ucol = [](uint32_t r, uint32_t u) { return SWZ ? u ^ ((r & 7u) << 2) : u; };
+  const auto ucol = [](uint32_t r, uint32_t u) { return u ^ ((r & 7u) << 2); };
   const uint32_t N = 1u << logN, BLK = N >> LOGR, S = 1u << logS;
   const uint32_t cpb = BLK / CW;
   const uint64_t k = blockIdx.x / cpb;
@@ -2743,8 +2742,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   // last pass fused with the CRT decode where its shape allows
   const uint32_t blkLog = ntt_block_log(p.logN);
   const int logR = (int)(p.logN - blkLog);
-  const bool crt_swz = switches().crt_swz;
-  const size_t fuse_lds = (size_t)p.L * (crt_swz ? 64 : kCrtRowStride) * sizeof(uint64_t) << (logR > 0 ? logR : 0);
+  const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
   const bool fuse = logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
                     ((p.N >> logR) % 64) == 0;
   {
@@ -2782,17 +2780,8 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                          logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh, sum_in ? 1 : 0, ct_L);
     if (logR > 0 && fuse) {
       const uint64_t nbf = K * ((p.N >> logR) / 64);
-#define CRT_LAUNCH(LR, SW)                                                                                   \
-  hipLaunchKernelGGL((ntt_inv_cols_crt<LR, SW>), dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, \
-                     logS, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale, fbuf)
-#define CRT_CASE(LR) \
-  case LR: if (crt_swz) CRT_LAUNCH(LR, true); else CRT_LAUNCH(LR, false); break;
-      switch (logR) {
-        CRT_CASE(1) CRT_CASE(2) CRT_CASE(3) CRT_CASE(4) CRT_CASE(5) CRT_CASE(6)
-        default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};
-      }
-#undef CRT_CASE
-#undef CRT_LAUNCH
+NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, logS,
+                   dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale, fbuf);
     } else if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, dbuf, p.L, p.logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);

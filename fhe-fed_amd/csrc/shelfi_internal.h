@@ -70,7 +70,6 @@ struct Switches {
   bool enc_vt = true;          // SHELFI_ENC_VT=0: v's columns pass in enc_cols_fused, not enc_vtab sums
   int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
   bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
-  bool crt_swz = true;         // SHELFI_CRT_SWZ=0: ntt_inv_cols_crt's padded LDS rows (68 u64, 4 WGs/CU)
   int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
   int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
   int pack_waves = 0;          // SHELFI_PACK_WAVES=2|8 (0: 4 rows per block)
@@ -78,7 +77,7 @@ struct Switches {
   int arena_stager = -1;       // SHELFI_ARENA_STAGER=0|1 (-1: by upload shape)
   uint64_t dev_chunk_mib = 4096;  // SHELFI_DEV_CHUNK_MIB: device encrypt / decrypt scratch per chain
   uint64_t wavg_chunk_mib = 0;    // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
-                                  // (0: 512 MiB with direct uploads, 128 through the staging ring)
+                                  // (0: 32 MiB per learner with direct uploads, 128 per group through the ring)
   bool h2d_direct = true;         // SHELFI_H2D_DIRECT=0: bytes-API aggregation uploads through the pinned ring
 };
 const Switches& switches();

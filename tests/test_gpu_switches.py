@@ -31,7 +31,6 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_ENC_VT", "0"),          # v's columns pass in enc_cols_fused, not table sums in the blocks pass
     ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
     ("SHELFI_DEC_ALL_TOWERS", "1"),  # decode over every tower, not the prefix
-    ("SHELFI_CRT_SWZ", "0"),         # ntt_inv_cols_crt's padded LDS rows
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
     ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
     ("SHELFI_ENC_TS", "0"),          # one column per thread over every tower (K = 7 defaults to one wave per tower)

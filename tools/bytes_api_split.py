@@ -17,11 +17,18 @@ import numpy as np  # noqa: E402
 import SHELFI_FHE as m  # noqa: E402
 from SHELFI_FHE import _lib  # noqa: E402
 
-Cl, Ka, B = 16, 64, 16384
+import argparse  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--k", type=int, default=64)
+ap.add_argument("--wire", default="palisade")
+a = ap.parse_args()
+Cl, Ka, B = 16, a.k, 16384
 d = "/tmp/keys_bytes_split/"
 os.makedirs(d, exist_ok=True)
 ck = m.CKKS("ckks", B, 52, d, multDepth=3, seed=7)
 assert ck.genCryptoContextAndKeyGen() == 1
+ck.set_wire_format(a.wire)
 x = np.random.default_rng(1).uniform(-1, 1, Ka * B)
 blobs = [ck.encrypt(x) for _ in range(Cl)]
 w = np.full(Cl, 1.0 / Cl, np.float32)
@@ -51,5 +58,5 @@ for _ in range(6):
     for k, v in (("size_query", t1 - t0), ("new_bytes", t2 - t1), ("into", t3 - t2), ("free", t4 - t3),
                  ("full", t5 - t4)):
         res[k].append(v * 1e3)
-print(json.dumps({"what": "ms, median of 6 (first included)", **{k: round(sorted(v)[len(v) // 2], 3) for k, v in res.items()},
+print(json.dumps({"what": "ms, median of 6 (first included)", "k": Ka, "wire": a.wire, **{k: round(sorted(v)[len(v) // 2], 3) for k, v in res.items()},
                   "in_MB": round(sum(len(b) for b in blobs) / 1e6, 1)}))

@@ -12,16 +12,16 @@ import csv
 import json
 import statistics
 
-ENCRYPT = ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
+ENCRYPT = ("fft_inv_whole", "fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
            "ntt_fwd_blocks_enc")
 _DEC_COMMON = ("ntt_inv_blocks_dec", "ntt_inv_blocks(", "ntt_inv_cols_crt", "ntt_inv_cols<", "crt_decode_kernel")
 # the decode FFT's passes as templates over FLOOD.  Since round 5 the noise is added in the last pass:
 # fft_fwd_cols<LOGR, FLOOD> (or fft_fwd_blocks<FLOOD> when one pass is the whole FFT), and the register-
 # chunk first pass fft_fwd_blocks_ct<BL, K1..K4, SWZ> serves both chains.  Rounds 3-4 profiles carry
 # fft_fwd_blocks_ct<BL, K1..K4, FLOOD, SWZ> and a flag-less fft_fwd_cols<LOGR> shared by both.
-DECRYPT = _DEC_COMMON + ("fft_fwd_blocks@false", "fft_fwd_cols@false")
-DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks@true", "fft_fwd_cols@true", "decode_stats_kernel",
-                                 "decode_flood_kernel")
+DECRYPT = _DEC_COMMON + ("fft_fwd_blocks@false", "fft_fwd_cols@false", "fft_fwd_whole@false")
+DECRYPT_FLOODED = _DEC_COMMON + ("fft_fwd_blocks@true", "fft_fwd_cols@true", "fft_fwd_whole@true",
+                                 "decode_stats_kernel", "decode_flood_kernel", "flood_add_kernel")
 
 
 def flood_arg(full):
@@ -31,7 +31,7 @@ def flood_arg(full):
     if "<" not in head:
         return None
     name, args = head[:head.index("<")], [a.strip() for a in head[head.index("<") + 1:head.rindex(">")].split(",")]
-    if name == "fft_fwd_blocks" and args:
+    if name in ("fft_fwd_blocks", "fft_fwd_whole") and args:  # FLOOD / STATS (round 5: the flooded whole pass)
         return args[0]
     if name == "fft_fwd_blocks_ct":
         return args[5] if len(args) >= 7 else "any"
@@ -45,8 +45,7 @@ def _matches(full, n):
     FLOOD argument is flag or that both chains run; else a prefix."""
     if "@" in n:
         f = flood_arg(full)
-        return f is not None and (f == n.split("@")[1] or f == "any") and \
-            full.startswith(n.split("@")[0][:len("fft_fwd_")])
+        return f is not None and (f == n.split("@")[1] or f == "any") and full.startswith(n.split("@")[0])
     return full.startswith(n) or n in full
 
 

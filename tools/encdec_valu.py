@@ -17,11 +17,12 @@ import statistics
 from encdec_traffic import _matches  # the decode FFT's FLOOD argument, by position
 
 CHAINS = {
-    "encrypt": ("fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
+    "encrypt": ("fft_inv_whole", "fft_inv_cols", "fft_inv_blocks", "enc_cols_fused", "enc_prep_kernel", "ntt_fwd_cols_enc",
                 "ntt_fwd_blocks_enc"),
-    "decrypt": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "fft_fwd_blocks@false", "fft_fwd_cols@false"),
+    "decrypt": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "fft_fwd_blocks@false", "fft_fwd_cols@false",
+                "fft_fwd_whole@false"),
     "decrypt_flooded": ("ntt_inv_blocks_dec", "ntt_inv_cols_crt", "decode_stats_kernel",
-                        "fft_fwd_blocks@true", "fft_fwd_cols@true"),
+                        "fft_fwd_blocks@true", "fft_fwd_cols@true", "fft_fwd_whole@true", "flood_add_kernel"),
 }
 
 
