@@ -611,6 +611,7 @@ void reload_switches() {
   if (const char* e = getenv("SHELFI_WAVG_CHUNK_MIB"))
     if (atoll(e) > 0) s.wavg_chunk_mib = (uint64_t)atoll(e);
   s.h2d_direct = env_flag("SHELFI_H2D_DIRECT", '0', true);
+  s.h2d_two = env_flag("SHELFI_H2D_TWO", '0', true);
   g_switches = s;
 }
 const Switches& switches() { return g_switches; }
@@ -724,6 +725,10 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     ctx->stage = nullptr;
     delete ctx->drain;
     ctx->drain = nullptr;
+    delete ctx->up2;
+    ctx->up2 = nullptr;
+    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
+    ctx->stream4 = nullptr;
     for (int i = 0; i < shelfi_ctx::kWeightRing; ++i) {
       if (ctx->wl_done[i]) (void)hipEventSynchronize(ctx->wl_done[i]);
       if (ctx->wl_done[i]) (void)hipEventDestroy(ctx->wl_done[i]);
@@ -1317,6 +1322,33 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
   if (direct && !ctx->drain) ctx->drain = new AsyncDrain(default_copy_threads());
+  const bool two = direct && switches().h2d_two && C > 1;
+  if (two && !ctx->up2) {
+    if (!ctx->stream4) SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream4, hipStreamNonBlocking));
+    ctx->up2 = new AsyncUpload();
+  }
+  hipEvent_t up2_done[2] = {nullptr, nullptr};
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int i = 0; i < 2; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } eg{up2_done};
+  if (two)
+    for (int i = 0; i < 2; ++i) SHELFI_HIP(hipEventCreateWithFlags(&up2_done[i], hipEventDisableTiming));
+  struct UpGuard {  // on an error: the second thread's posted copies are issued and done before we unwind
+    shelfi_ctx* c;
+    bool armed;
+    ~UpGuard() {
+      if (!armed) return;
+      try {
+        c->up2->wait();
+      } catch (...) {
+      }
+      (void)hipStreamSynchronize(c->stream4);
+    }
+  } ug{ctx, two};
   struct DrainGuard {  // on an error: the worker finishes what was posted before the streams go away
     AsyncDrain* d;
     bool armed;
@@ -1327,6 +1359,11 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         }
     }
   } dg{ctx->drain, direct};
+  if (direct) {  // the output's residue pages, first-touched on the drain worker during the uploads
+    dst.pieces(0, K, p, pcs);
+    const uint8_t* lo = pcs.front().p;
+    ctx->drain->prefault(const_cast<uint8_t*>(lo), (size_t)(pcs.back().p + pcs.back().n - lo));
+  }
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
   using clk = std::chrono::steady_clock;
@@ -1338,7 +1375,10 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
     for (size_t c0 = 0; c0 < C; c0 += group) {
       const size_t gc = std::min(group, C - c0);
-      if (ci >= 2 || c0 > 0) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));  // buffer free
+      if (ci >= 2 || c0 > 0) {  // buffer free
+        SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
+        if (two) SHELFI_HIP(hipStreamWaitEvent(ctx->stream4, pp.computed[b], 0));
+      }
       uint64_t* tabh = raw ? ctx->gather_host + b * runs_cap : nullptr;
       if (raw && (ci >= 2 || c0 > 0)) {  // tabh's last copy done
         const auto t0 = clk::now();
@@ -1357,13 +1397,21 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
           if (raw)
             for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
           const auto t0 = clk::now();
-          SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
+          if (two && (c & 1))  // every other learner from the second thread: two copies in flight
+            ctx->up2->post(land, lo, span, ctx->stream4);
+          else
+            SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
           if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
         } else {
           sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
         }
       }
       if (raw) SHELFI_HIP(hipMemcpyAsync(tabd[b], tabh, runs * 8, hipMemcpyHostToDevice, pp.a));
+      if (two) {  // the second thread's copies of this chunk join stream A
+        ctx->up2->wait();
+        SHELFI_HIP(hipEventRecord(up2_done[b], ctx->stream4));
+        SHELFI_HIP(hipStreamWaitEvent(pp.a, up2_done[b], 0));
+      }
       SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
       SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
       if (raw) launch_gather_runs(rawb[b], tabd[b], runs, (uint32_t)(p.N * 8), inb[b], pp.b);

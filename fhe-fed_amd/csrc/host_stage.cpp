@@ -367,9 +367,19 @@ void AsyncDrain::post(int slot, hipEvent_t ev, std::vector<HostPiece> pieces) {
   cv_.notify_all();
 }
 
+void AsyncDrain::prefault(uint8_t* p, size_t n) {
+  if (!n) return;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++prefaults_;
+    q_.push_back(Job{-1, nullptr, std::vector<HostPiece>{HostPiece{p, n}}});
+  }
+  cv_.notify_all();
+}
+
 void AsyncDrain::finish() {
   std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait(lk, [&] { return busy_[0] == 0 && busy_[1] == 0; });
+  cv_.wait(lk, [&] { return busy_[0] == 0 && busy_[1] == 0 && prefaults_ == 0; });
   if (!err_.empty()) {
     const std::string e = err_;
     err_.clear();
@@ -388,6 +398,16 @@ void AsyncDrain::run() {
       j = std::move(q_.front());
       q_.pop_front();
     }
+    if (j.slot < 0) {  // prefault: one write per 4 KiB page (the bytes are overwritten by the drains)
+      for (const HostPiece& h : j.pieces)
+        for (size_t o = 0; o < h.n; o += 4096) reinterpret_cast<volatile uint8_t*>(h.p)[o] = 0;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --prefaults_;
+      }
+      cv_.notify_all();
+      continue;
+    }
     const hipError_t e = hipEventSynchronize(j.ev);
     if (e == hipSuccess) {
       jobs.clear();
@@ -402,6 +422,57 @@ void AsyncDrain::run() {
       std::lock_guard<std::mutex> lk(mu_);
       if (e != hipSuccess && err_.empty()) err_ = std::string("staged copy: ") + hipGetErrorString(e);
       --busy_[j.slot];
+    }
+    cv_.notify_all();
+  }
+}
+
+// ----------------------------------------------------------- AsyncUpload ----
+AsyncUpload::AsyncUpload() { worker_ = std::thread([this] { run(); }); }
+
+AsyncUpload::~AsyncUpload() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+}
+
+void AsyncUpload::post(void* dst, const void* src, size_t n, hipStream_t stream) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++pending_;
+    q_.push_back(Job{dst, src, n, stream});
+  }
+  cv_.notify_all();
+}
+
+void AsyncUpload::wait() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return pending_ == 0; });
+  if (!err_.empty()) {
+    const std::string e = err_;
+    err_.clear();
+    throw Error{SHELFI_ERR_DEVICE, e};
+  }
+}
+
+void AsyncUpload::run() {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      j = q_.front();
+      q_.pop_front();
+    }
+    const hipError_t e = hipMemcpyAsync(j.dst, j.src, j.n, hipMemcpyHostToDevice, j.stream);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (e != hipSuccess && err_.empty()) err_ = std::string("upload: ") + hipGetErrorString(e);
+      --pending_;
     }
     cv_.notify_all();
   }

@@ -154,15 +154,19 @@ class AsyncDrain {
   uint8_t* buffer(int slot, size_t bytes);  // pinned; grown (the slot must be idle)
   void wait_slot(int slot);
   void post(int slot, hipEvent_t ev, std::vector<HostPiece> pieces);
+  // First-touch the pages of [p, p + n) on the worker (ahead of the drains into a fresh output, which
+  // would otherwise take the page faults in the call's tail)
+  void prefault(uint8_t* p, size_t n);
   void finish();
 
  private:
   void run();
   struct Job {
-    int slot;
+    int slot;  // -1: prefault the pieces
     hipEvent_t ev;
     std::vector<HostPiece> pieces;
   };
+  int prefaults_ = 0;  // posted, not yet done
   CopyPool pool_;
   std::thread worker_;
   std::mutex mu_;
@@ -172,6 +176,36 @@ class AsyncDrain {
   int busy_[2] = {0, 0};  // posted, not yet drained, per slot
   uint8_t* buf_[2] = {nullptr, nullptr};
   size_t cap_[2] = {0, 0};
+  std::string err_;
+};
+
+// A second uploading thread (round 5): the pageable hipMemcpyAsync returns only once the runtime has moved
+// the data, so two threads with a stream each keep two copies in flight -- one copy's setup overlaps the
+// other's transfer.  post() queues a copy on `stream`; wait() returns when every posted copy has been
+// issued and rethrows the first error.
+class AsyncUpload {
+ public:
+  AsyncUpload();
+  ~AsyncUpload();
+  AsyncUpload(const AsyncUpload&) = delete;
+  AsyncUpload& operator=(const AsyncUpload&) = delete;
+  void post(void* dst, const void* src, size_t n, hipStream_t stream);
+  void wait();
+
+ private:
+  void run();
+  struct Job {
+    void* dst;
+    const void* src;
+    size_t n;
+    hipStream_t stream;
+  };
+  std::thread worker_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  int pending_ = 0;
+  bool stop_ = false;
   std::string err_;
 };
 

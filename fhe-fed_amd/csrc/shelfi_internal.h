@@ -79,6 +79,7 @@ struct Switches {
   uint64_t wavg_chunk_mib = 0;    // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
                                   // (0: 32 MiB per learner with direct uploads, 128 per group through the ring)
   bool h2d_direct = true;         // SHELFI_H2D_DIRECT=0: bytes-API aggregation uploads through the pinned ring
+  bool h2d_two = true;            // SHELFI_H2D_TWO=0: direct uploads from the calling thread only
 };
 const Switches& switches();
 void reload_switches();
@@ -196,6 +197,7 @@ struct DeviceKeys {
 namespace shelfi {
 class Stager;
 class AsyncDrain;
+class AsyncUpload;
 struct EvalState;  // eval.cpp: relinearization key + per-level tables
 }
 
@@ -208,6 +210,8 @@ struct shelfi_ctx {
   hipStream_t stream3 = nullptr;  // copy-out stream of the pipelined bytes API
   shelfi::Stager* stage = nullptr;  // pinned staging rings (host_stage.h), lazily created
   shelfi::AsyncDrain* drain = nullptr;  // background output scatter of the direct-upload aggregation
+  shelfi::AsyncUpload* up2 = nullptr;   // second uploading thread of the direct-upload aggregation
+  hipStream_t stream4 = nullptr;        // its upload stream
   shelfi::DeviceTables dt;
   shelfi::DeviceKeys dk;
   std::vector<uint64_t> pk_host, sk_host;

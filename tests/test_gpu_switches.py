@@ -91,12 +91,13 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
 
 
 @pytest.mark.parametrize("wire", ["palisade", "shelfi", "packed"])
-@pytest.mark.parametrize("mode", ["chunk1", "ring", "ring_chunk1"])
+@pytest.mark.parametrize("mode", ["chunk1", "ring", "ring_chunk1", "one_thread"])
 def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
     """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (direct uploads, 512 MiB of
     input per learner group: one chunk here) against one ciphertext per chunk (7 chunks through the two
-    device buffer sets), the pinned staging ring (SHELFI_H2D_DIRECT=0), and both: the same aggregate, byte
-    for byte, in every wire format (archives take the raw-range + device gather path)."""
+    device buffer sets), the pinned staging ring (SHELFI_H2D_DIRECT=0), both, and direct uploads from the
+    calling thread alone (SHELFI_H2D_TWO=0): the same aggregate, byte for byte, in every wire format (archives
+    take the raw-range + device gather path)."""
     ck, x, _, _ = ctx
     xs = x.cpu().numpy()
     ck.set_wire_format(wire)
@@ -108,6 +109,8 @@ def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
             set_switch(monkeypatch, "SHELFI_WAVG_CHUNK_MIB", "1")
         if mode in ("ring", "ring_chunk1"):
             set_switch(monkeypatch, "SHELFI_H2D_DIRECT", "0")
+        if mode == "one_thread":
+            set_switch(monkeypatch, "SHELFI_H2D_TWO", "0")
         got = ck.computeWeightedAverage(blobs, w)
     finally:
         ck.set_wire_format("palisade")
