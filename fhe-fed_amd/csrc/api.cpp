@@ -255,6 +255,8 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
       prs[(size_t)t * N + i] = shoup(pr[(size_t)t * N + i], q);
       iprs[(size_t)t * N + i] = shoup(ipr[(size_t)t * N + i], q);
     }
+    c.ninv_qhat_w1 = (uint64_t)(((u128)c.ninv_qhat * ipr[(size_t)t * N + 1]) % q);
+    c.ninv_qhat_w1_shoup = shoup(c.ninv_qhat_w1, q);
   }
   dt.qmod128_lo = (uint64_t)Q128;
   dt.qmod128_hi = (uint64_t)(Q128 >> 64);

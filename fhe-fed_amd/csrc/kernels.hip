@@ -2142,7 +2142,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = a[(uint64_t)r * BLK];
 #pragma unroll
-    for (int v = 0; v < LOGR; ++v) {
+    for (int v = 0; v < LOGR - 1; ++v) {
       const int tr = 1 << v, h = R >> (v + 1);
 #pragma unroll
       for (int i = 0; i < h; ++i) {
@@ -2156,9 +2156,17 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
         }
       }
     }
+    // the last stage (one twiddle, w[1]) fused with the scale N^-1 (Q/q_t)^-1 (round 5): X = (x + y) c,
+    // Y = (x + B - y) (w[1] c) -- two products per pair instead of the butterfly's one and the scale's two
+    constexpr int TR = R / 2;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      ys[t][r][ucol(r, lane)] = canon4(shoup_lazy(x[r], c.ninv_qhat, c.ninv_qhat_shoup, q), q);
+    for (int jj = 0; jj < TR; ++jj) {
+      const uint64_t xv = x[jj], yv = x[jj + TR];
+      const uint64_t B = gs_in8<true>(LOGR - 1, jj) ? (q << 3) : (q << 2);  // the butterfly's input bound
+      ys[t][jj][ucol(jj, lane)] = canon4(shoup_lazy(xv + yv, c.ninv_qhat, c.ninv_qhat_shoup, q), q);
+      ys[t][jj + TR][ucol(jj + TR, lane)] =
+          canon4(shoup_lazy(xv + B - yv, c.ninv_qhat_w1, c.ninv_qhat_w1_shoup, q), q);
+    }
   }
   __syncthreads();
   const uint32_t gapLog = logN - 1 - logS, gap = 1u << gapLog;

@@ -132,6 +132,7 @@ struct TowerConst {
   uint32_t pad32;
   uint64_t bq62;  // floor(2^62 / q) q: v + bq62 in [0, 2^63) for |v| <= 2^61 + 2^7 (encrypt's m + e0)
   uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
+  uint64_t ninv_qhat_w1, ninv_qhat_w1_shoup;  // ninv_qhat * psi^-bitrev(1): the last INTT stage's twiddle, scaled
   // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^128 and (2^128 - Q) mod 2^128
   // (the same in every tower), limbs 0..3 of 30 bits and limb 4 of 8 bits
   uint32_t crt30[5], nq30[5], pad30[2];
