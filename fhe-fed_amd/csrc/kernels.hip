@@ -1100,27 +1100,33 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __re
 // launch and the [K][S] intermediate never goes through HBM (encode: 1.18 -> 0.39 MB per ciphertext;
 // decode: 0.92 -> 0.39).  The same butterflies on the same operands as fft_inv_cols<4> +
 // fft_inv_blocks_ct<10, ...> (fft_fwd_blocks_ct<10, ...> + fft_fwd_cols<4>): bit-identical outputs.
-// Rows <-> blocks go through LDS one component at a time (16 x 1024 doubles = 128 KiB, one workgroup
+// Rows <-> blocks go through LDS one component at a time (16 x 1088 doubles = 136 KiB, one workgroup
 // per CU); inside a block, a wave exchanges its own 1024 elements (8 KiB) with no workgroup barrier.
-// LDS rows padded by one double per 32 (fft_wpad): at most 2-way conflicts for the three set shapes used
-// (elements 4 s + m, 64 (s >> 2) + (s & 3) + 4 m, s + 64 m; none for the last, which the row <-> block
-// transposes use), counted with the ds_read_b64 / ds_write_b64 lane groups of MI355X_MICROARCH.md §LDS.
-// Unlike an XOR swizzle the padding keeps each thread's 16 addresses at compile-time offsets from one
-// base (an XOR swizzle's 32 live addresses spilled under the 128-VGPR cap of 1024-thread workgroups).
+// LDS layouts.  Padded rows (not an XOR swizzle) keep each thread's 16 addresses at compile-time offsets
+// from one base: an XOR swizzle's 32 live addresses spilled under the 128-VGPR cap of 1024-thread
+// workgroups.  Each exchange has its own padding, chosen with a model of the ds_read_b64 (2 x 32 lanes, 64
+// banks) and ds_write_b64 / read2 (4 x 16 lanes, 32 banks) groups of MI355X_MICROARCH.md §LDS so that both
+// of its access shapes are conflict-free (one shared padding left 2-way conflicts: SQ_LDS_BANK_CONFLICT 3.4
+// cycles per LDS instruction in fft_inv_whole, profiles/r05p):
+//   blocks <-> rows transposes and the flooding statistics, e + (e >> 5)   (fft_wpad, fft_wt1, fft_wx3)
+//   exchanges between 4 s + m and 64 (s >> 2) + (s & 3) + 4 m, e + (e >> 4)     (fft_xa1, fft_xa2)
+//   exchanges between 64 (s >> 2) + (s & 3) + 4 m and s + 64 m, e + 2 (e >> 5)  (fft_xb2, fft_xb3)
+// The closed forms below are those paddings of the set shapes 4 (l + 64 q) + r (m = 4 q + r),
+// 64 (l >> 2) + (l & 3) + 4 m and l + 64 m, for lane l and register m.
 constexpr uint32_t kFftWholeLogS = 14;
-constexpr uint32_t kFftWholeRow = 1056;  // padded doubles per 1024-element block
+constexpr uint32_t kFftWholeRow = 1088;  // doubles per 1024-element block slice (the largest padding, 1087)
 __device__ __forceinline__ uint32_t fft_wpad(uint32_t e) { return e + (e >> 5); }
+__device__ __forceinline__ uint32_t fft_wt1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
+__device__ __forceinline__ uint32_t fft_wx3(uint32_t l, int m) { return l + (l >> 5) + 66u * m; }
+__device__ __forceinline__ uint32_t fft_xa1(uint32_t l, int m) { return 4 * l + (l >> 2) + 272u * (m >> 2) + (m & 3); }
+__device__ __forceinline__ uint32_t fft_xa2(uint32_t l, int m) { return 68 * (l >> 2) + (l & 3) + 4u * m + (m >> 2); }
+__device__ __forceinline__ uint32_t fft_xb2(uint32_t l, int m) {
+  return 68 * (l >> 2) + (l & 3) + 4u * m + 2u * (m >> 3);
+}
+__device__ __forceinline__ uint32_t fft_xb3(uint32_t l, int m) { return l + 2 * (l >> 5) + 68u * m; }
 
 // A wave's exchange inside its block's 1024 elements: a[m] (at padded block position P(m)) -> a[m] (at
-// Q(m)), real parts first, then imaginary parts, through the wave's LDS slice.  P and Q return padded
-// positions as one per-lane base plus a compile-time offset per m (ds_* immediate offsets): the three
-// set shapes, padded (fft_wpad), are
-//   4 s + m, s = l + 64 q:          (4 l + (l >> 3)) + 264 q + m            (fft_wx1)
-//   64 (l >> 2) + (l & 3) + 4 m:    (66 (l >> 2) + (l & 3)) + 4 m + (m >> 3)  (fft_wx2)
-//   l + 64 m:                       (l + (l >> 5)) + 66 m                     (fft_wx3)
-__device__ __forceinline__ uint32_t fft_wx1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
-__device__ __forceinline__ uint32_t fft_wx2(uint32_t l, int m) { return 66 * (l >> 2) + (l & 3) + 4u * m + (m >> 3); }
-__device__ __forceinline__ uint32_t fft_wx3(uint32_t l, int m) { return l + (l >> 5) + 66u * m; }
+// Q(m)), real parts first, then imaginary parts, through the wave's LDS slice.
 template <class PF, class QF>
 __device__ __forceinline__ void fft_wave_xch(double2 (&a)[16], double* __restrict__ Ls, PF P, QF Q) {
 #pragma unroll
@@ -1203,9 +1209,9 @@ __global__ __launch_bounds__(1024) void fft_inv_whole(const double* __restrict__
   // 64 (l >> 2) + (l & 3) + 4 m), 2 .. 1 on sets l + 64 q (elements 4 (l + 64 q) + m)
   double* Ls = lds + w * kFftWholeRow;
   fft_dif_set<4, 6>(a, l, tw);
-  fft_wave_xch(a, Ls, [&](int m) { return fft_wx3(l, m); }, [&](int m) { return fft_wx2(l, m); });
+  fft_wave_xch(a, Ls, [&](int m) { return fft_xb3(l, m); }, [&](int m) { return fft_xb2(l, m); });
   fft_dif_set<4, 2>(a, l & 3, tw);
-  fft_wave_xch(a, Ls, [&](int m) { return fft_wx2(l, m); }, [&](int m) { return fft_wx1(l, m); });
+  fft_wave_xch(a, Ls, [&](int m) { return fft_xa2(l, m); }, [&](int m) { return fft_xa1(l, m); });
   double2* __restrict__ g = buf + k * S + (uint64_t)w * BLK;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -2585,7 +2591,7 @@ __device__ __forceinline__ double2 fft_whole_flood_stats(const double2 (&a)[16],
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) lds[w * kFftWholeRow + fft_wx1(l, i)] = part ? a[i].y : a[i].x;
+    for (int i = 0; i < 16; ++i) lds[w * kFftWholeRow + fft_wt1(l, i)] = part ? a[i].y : a[i].x;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -2659,10 +2665,10 @@ __global__ __launch_bounds__(1024) void fft_fwd_whole(const double2* __restrict_
   double* Ls = lds + w * kFftWholeRow;
   // (the empty asm statements keep each phase's twiddle loads in that phase: hoisted to the kernel
   // entry, 33 twiddles would not fit beside the data under the 128-VGPR cap)
-  fft_wave_xch(a, Ls, [&](int m) { return fft_wx1(l, m); }, [&](int m) { return fft_wx2(l, m); });
+  fft_wave_xch(a, Ls, [&](int m) { return fft_xa1(l, m); }, [&](int m) { return fft_xa2(l, m); });
   asm volatile("" ::: "memory");
   fft_dit_set<4, 2>(a, l & 3, tw);  // half-sizes 4 .. 32
-  fft_wave_xch(a, Ls, [&](int m) { return fft_wx2(l, m); }, [&](int m) { return fft_wx3(l, m); });
+  fft_wave_xch(a, Ls, [&](int m) { return fft_xb2(l, m); }, [&](int m) { return fft_xb3(l, m); });
   asm volatile("" ::: "memory");
   fft_dit_set<4, 6>(a, l, tw);  // half-sizes 64 .. 512
   asm volatile("" ::: "memory");
