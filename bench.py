@@ -110,6 +110,10 @@ def parse():
                     help="start the ranks through torch.distributed.run even at --gpus 1 (the launcher path)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher test: every rank reports its rendezvous and exits before any GPU call")
+    ap.add_argument("--api-repeat", action="store_true",
+                    help="time the default-wire bytes-API sample again after the other formats (probe)")
+    ap.add_argument("--api-cold-sets", type=int, default=3,
+                    help="fresh blob sets for the bytes-API cold-call sample (default wire only)")
     ap.add_argument("--api-cts", type=int, default=64,
                     help="ciphertexts per learner for the bytes-API (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
@@ -802,6 +806,21 @@ def main():
                    sample="%d learners x %d cts, bytes in -> bytes out through SHELFI_FHE.CKKS."
                           "computeWeightedAverage (H2D + wavg + D2H) in the default wire format (%s)"
                           % (Cl, Ka, default_wire))
+        # cold: the first call on freshly encrypted blobs, as an aggregator sees each round's uploads (the
+        # runtime has not touched their pages yet), median over fresh sets
+        cold = []
+        for _ in range(args.api_cold_sets):
+            del pblobs
+            pblobs = [ck.encrypt(xa) for _ in range(Cl)]
+            t0 = time.perf_counter()
+            res_c = ck.computeWeightedAverage(pblobs, weights)
+            cold.append(time.perf_counter() - t0)
+            del res_c
+        if cold:
+            dtc = sorted(cold)[len(cold) // 2]
+            api["cold"] = {"ms_per_call": round(dtc * 1e3, 2),
+                           "input_GB_per_s": round(sum(len(b) for b in pblobs) / dtc / 1e9, 2),
+                           "sets": len(cold), "sample": "first call on each fresh set of encrypt outputs, median"}
         del pblobs
         # the library's uint64 blob (64-byte header + raw [K][2][L][N])
         src = [out[:Ka].clone() for _ in range(Cl)]  # any valid ciphertexts of this key
@@ -817,6 +836,10 @@ def main():
             del kblobs
         finally:
             ck.set_wire_format(default_wire)
+        if args.api_repeat:
+            pblobs = [ck.encrypt(xa) for _ in range(Cl)]
+            api["repeat"] = api_sample(pblobs)
+            del pblobs
 
     # roofline of the dominant kernel: algorithmic bytes = the C learners' packed residues
     # (K * 2 * N * sum_t U_t / 8 each, U_t ~ bitlength(q_t)) read once

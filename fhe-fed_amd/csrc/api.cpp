@@ -612,7 +612,9 @@ void reload_switches() {
     if (atoll(e) > 0) s.dev_chunk_mib = (uint64_t)atoll(e);
   if (const char* e = getenv("SHELFI_WAVG_CHUNK_MIB"))
     if (atoll(e) > 0) s.wavg_chunk_mib = (uint64_t)atoll(e);
-  s.h2d_direct = env_flag("SHELFI_H2D_DIRECT", '0', true);
+  if (const char* e = getenv("SHELFI_STAGE_SLOT_MIB"))
+    if (atoll(e) > 0 && atoll(e) <= 256) s.stage_slot_mib = (uint64_t)atoll(e);
+  s.h2d_direct = env_flag("SHELFI_H2D_DIRECT", '1', false);
   s.h2d_two = env_flag("SHELFI_H2D_TWO", '0', true);
   g_switches = s;
 }
@@ -1092,9 +1094,18 @@ struct Pipe {
   }
 };
 
-// The ctx's pinned staging rings (8 x 8 MiB each way), created on first use.
+// The ctx's pinned staging rings (8 slots each way, SHELFI_STAGE_SLOT_MIB each), created on first use
+// and re-created between calls when the slot size switch changes (the ring is idle then).  16 MiB: a
+// bytes-API learner chunk (4 cts, 8 MiB + its archive headers) is one DMA; pinned copies of 8 / 16 / 32
+// MiB ran 53.5 / 55.4 / 56.3 GB/s (profiles/r05u/pinned_h2d.json) and the archive aggregation 45.1 -> 48.4
+// GB/s with 16 MiB slots, the other bytes-API rates within noise (profiles/r05u/bench_slot*).
 static Stager& stager(shelfi_ctx* ctx) {
-  if (!ctx->stage) ctx->stage = new Stager(8u << 20, 8, 8, default_copy_threads());
+  const size_t slot = (size_t)switches().stage_slot_mib << 20;
+  if (ctx->stage && ctx->stage->slot_bytes() != slot) {
+    delete ctx->stage;
+    ctx->stage = nullptr;
+  }
+  if (!ctx->stage) ctx->stage = new Stager(slot, 8, 8, default_copy_threads());
   return *ctx->stage;
 }
 
@@ -1256,13 +1267,17 @@ static std::vector<CtLayout> wavg_inputs(const shelfi_ctx* ctx, const uint8_t* c
 // Pipelined bytes -> bytes aggregation: the K ciphertexts are processed in chunks;
 // chunk i's H2D copies (all learners, stream A) overlap chunk i-1's wavg + D2H
 // (stream B), with two device buffer sets.  Writes the payload of the result.
-// Uploads (round 5, SHELFI_H2D_DIRECT): each learner's chunk is one contiguous byte range of its
-// blob, copied straight from the caller's pageable memory (the runtime's own pinned path: 55.6 GB/s
-// in 32 MiB copies vs 42.5 GB/s through the staging ring, tools/h2d_pageable_probe.py); a PALISADE
-// archive's range lands raw and its tower runs are gathered into [K][2][L][N] on the device.  The
-// staging ring (SHELFI_H2D_DIRECT=0) copies each residue run through pinned slots.  (Zero-copy
-// uploads registered in place with hipHostRegister measured slower than the ring and were removed in
-// round 5: tools/h2d_register_ab.py.)  The sum's D2H goes through the ring either way.
+// Uploads (round 5): each learner's chunk is one contiguous byte range of its blob -- a PALISADE
+// archive's range (tower headers included) lands raw and its tower runs are gathered into [K][2][L][N]
+// on the device.  By default the range goes through the pinned staging ring (pool threads memcpy it
+// into 16 MiB pinned slots that are DMA'd); SHELFI_H2D_DIRECT=1 copies it straight from the caller's
+// pageable memory instead, which is faster only on blobs the runtime has already pinned: on fresh blobs
+// (every aggregation round's uploads) the runtime pins their pages on each first copy.  16 x 64 cts of
+// archives, input GB/s fresh malloc'd / fresh encrypt outputs / warm: ring 48.2 / 48.9 / 48.5
+// (profiles/r05u/slot_size.json, 16 MiB), direct 18.7 / 34.4 / 53.7 (taper_palisade.json).  The sum's D2H lands
+// in a pinned buffer that the AsyncDrain worker scatters into the output, so the uploading thread never
+// stops to drain.  (Zero-copy uploads registered in place with hipHostRegister measured slower than
+// the ring and were removed in round 5: tools/h2d_register_ab.py.)
 static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in,
                                 const float* weights, size_t C, uint64_t K, const CtLayout& dst,
                                 const size_t* lens) {
@@ -1271,11 +1286,9 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   const bool direct = switches().h2d_direct;
   // chunk of input per learner-group buffer: direct uploads want ~32 MiB per copy (8 MiB copies ran
-  // 51.6 GB/s, 2 MiB 41.3, 32 MiB 55.6), and the last chunk's wavg + D2H + drain is the call's tail,
-  // so 32 MiB per learner (512 MiB for 16 learners: 16 / 32 per learner ran 52.4 / 52.2 GB/s, 64 MiB
-  // 51.6, profiles/r05k); through the ring ~128 MiB per group (round 4: 32 / 64 / 128 / 256 MiB ran
-  // 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x 64 cts, profiles/r04w/api_chunk.txt);
-  // SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
+  // 51.6 GB/s, 2 MiB 41.3, 32 MiB 55.6, on pinned-warm blobs), so 32 MiB per learner; through the ring
+  // ~128 MiB per group (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x
+  // 64 cts, profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
   const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 32 * group : 128;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
   kc = std::min<uint64_t>(kc, K);
@@ -1284,7 +1297,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   // output is packed before its D2H
   const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
   const bool pin = in.front().packed, pout = dst.packed;
-  const bool raw = direct && in.front().pal;  // archives: raw ranges, gathered on the device
+  const bool raw = in.front().pal;  // archives: raw ranges, gathered on the device
   const size_t pin_chunk = pin ? group * kc * pct : 0, pout_chunk = pout ? kc * pct : 0;
   const uint64_t nchunks = (K + kc - 1) / kc;
   std::vector<HostPiece> pcs;
@@ -1323,7 +1336,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   // A: H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
-  if (direct && !ctx->drain) ctx->drain = new AsyncDrain(default_copy_threads());
+  if (!ctx->drain) ctx->drain = new AsyncDrain(default_copy_threads());
   const bool two = direct && switches().h2d_two && C > 1;
   if (two && !ctx->up2) {
     if (!ctx->stream4) SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream4, hipStreamNonBlocking));
@@ -1360,8 +1373,8 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         } catch (...) {
         }
     }
-  } dg{ctx->drain, direct};
-  if (direct) {  // the output's residue pages, first-touched on the drain worker during the uploads
+  } dg{ctx->drain, true};
+  {  // the output's residue pages, first-touched on the drain worker during the uploads
     dst.pieces(0, K, p, pcs);
     const uint8_t* lo = pcs.front().p;
     ctx->drain->prefault(const_cast<uint8_t*>(lo), (size_t)(pcs.back().p + pcs.back().n - lo));
@@ -1404,8 +1417,17 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
           else
             SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
           if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
-        } else {
-          sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
+        } else {  // through the pinned ring: an archive's whole range (one piece), else the pieces
+          const auto t0 = clk::now();
+          if (raw) {
+            const uint8_t* lo = pcs.front().p;
+            for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
+            const HostPiece whole{const_cast<uint8_t*>(lo), (size_t)(pcs.back().p + pcs.back().n - lo)};
+            sr.s.h2dv(land, &whole, 1, pp.a);
+          } else {
+            sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
+          }
+          if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
         }
       }
       if (raw) SHELFI_HIP(hipMemcpyAsync(tabd[b], tabh, runs * 8, hipMemcpyHostToDevice, pp.a));
@@ -1444,28 +1466,23 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
         dst.pieces(k0, kn, p, pcs);
         const uint8_t* sum = pout ? poutb[b] : outb[b];
-        if (direct) {  // one DMA into the drain's pinned buffer; its worker scatters it to the pieces
-          size_t nbytes = 0;
-          for (const HostPiece& h : pcs) nbytes += h.n;
-          uint8_t* hb = ctx->drain->buffer(b, nbytes);  // waits until chunk ci - 2 is drained
-          SHELFI_HIP(hipMemcpyAsync(hb, sum, nbytes, hipMemcpyDeviceToHost, pp.c));
-          SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
-          ctx->drain->post(b, pp.out_free[b], pcs);
-        } else {
-          sr.s.d2hv(pcs.data(), pcs.size(), sum, pp.c);
-          SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
-        }
+        // one DMA into the drain's pinned buffer; its worker scatters it to the pieces
+        size_t nbytes = 0;
+        for (const HostPiece& h : pcs) nbytes += h.n;
+        uint8_t* hb = ctx->drain->buffer(b, nbytes);  // waits until chunk ci - 2 is drained
+        SHELFI_HIP(hipMemcpyAsync(hb, sum, nbytes, hipMemcpyDeviceToHost, pp.c));
+        SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+        ctx->drain->post(b, pp.out_free[b], pcs);
       }
-      if (!direct) sr.s.poll();
     }
   }
   const auto t_issued = clk::now();
-  if (direct) ctx->drain->finish();
+  ctx->drain->finish();
   sr.finish();
   pp.sync();
   if (trace)
-    std::fprintf(stderr, "[wavg-bytes] %s chunks %llu x %llu cts: issue %.2f ms (uploads %.2f, tab waits %.2f), "
-                 "tail %.2f ms\n", direct ? (raw ? "direct+gather" : "direct") : "ring", (unsigned long long)nchunks,
+    std::fprintf(stderr, "[wavg-bytes] %s%s chunks %llu x %llu cts: issue %.2f ms (uploads %.2f, tab waits %.2f), "
+                 "tail %.2f ms\n", direct ? "direct" : "ring", raw ? "+gather" : "", (unsigned long long)nchunks,
                  (unsigned long long)kc, std::chrono::duration<double>(t_issued - t_start).count() * 1e3, t_up * 1e3,
                  t_wait * 1e3, std::chrono::duration<double>(clk::now() - t_issued).count() * 1e3);
   uint32_t flag = 0;

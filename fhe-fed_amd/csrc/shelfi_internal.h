@@ -78,7 +78,8 @@ struct Switches {
   uint64_t dev_chunk_mib = 4096;  // SHELFI_DEV_CHUNK_MIB: device encrypt / decrypt scratch per chain
   uint64_t wavg_chunk_mib = 0;    // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
                                   // (0: 32 MiB per learner with direct uploads, 128 per group through the ring)
-  bool h2d_direct = true;         // SHELFI_H2D_DIRECT=0: bytes-API aggregation uploads through the pinned ring
+  uint64_t stage_slot_mib = 16;   // SHELFI_STAGE_SLOT_MIB: pinned staging-ring slot (DMA granule)
+  bool h2d_direct = false;        // SHELFI_H2D_DIRECT=1: bytes-API uploads straight from pageable memory
   bool h2d_two = true;            // SHELFI_H2D_TWO=0: direct uploads from the calling thread only
 };
 const Switches& switches();

@@ -71,3 +71,21 @@ torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 print(json.dumps({"pinned_bounce_1thread_64mib": True, "ms": round(dt * 1e3, 2), "GB_per_s": round(total / dt / 1e9, 2)}),
       flush=True)
+
+# source alignment (round 5): a PALISADE archive's residue range starts after its headers, at any byte
+for off in (0, 8, 64, 100, 4096, 4099):
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        o = 0
+        for b in blobs:
+            src = torch.frombuffer(b, dtype=torch.uint8)
+            for s0 in range(off, len(b) - (32 << 20), 32 << 20):
+                dev[o:o + (32 << 20)].copy_(src[s0:s0 + (32 << 20)], non_blocking=True)
+                o += 32 << 20
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[1]
+    print(json.dumps({"src_offset": off, "addr_mod_4096": (torch.frombuffer(blobs[0], dtype=torch.uint8).data_ptr() + off) % 4096,
+                      "ms": round(dt * 1e3, 2), "GB_per_s": round(o / dt / 1e9, 2)}), flush=True)
