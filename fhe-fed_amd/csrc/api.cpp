@@ -1283,47 +1283,70 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
                                 const size_t* lens) {
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
-  const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   const bool direct = switches().h2d_direct;
+  // learners per wavg launch: all of them (up to kWavgMaxLearners), except that a call whose cts fit
+  // one chunk is cut into ~4 learner groups so the uploads overlap the gathers / wavgs (accumulated
+  // mod q, so bit-identical): cfg2's 16 x 4 cts otherwise upload everything before any device work
+  size_t group = std::min<size_t>(C, kWavgMaxLearners);
+  if (!direct && C >= 4 && K * ct_bytes * group <= (128ull << 20)) group = (std::min<size_t>(C, kWavgMaxLearners) + 3) / 4;
   // chunk of input per learner-group buffer: direct uploads want ~32 MiB per copy (8 MiB copies ran
   // 51.6 GB/s, 2 MiB 41.3, 32 MiB 55.6, on pinned-warm blobs), so 32 MiB per learner; through the ring
   // ~128 MiB per group (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x
   // 64 cts, profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
   const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 32 * group : 128;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
-  kc = std::min<uint64_t>(kc, K);
-  const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
   // packed wire (version-2 blobs): uploads land packed and are unpacked on the device; a packed
   // output is packed before its D2H
   const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
   const bool pin = in.front().packed, pout = dst.packed;
   const bool raw = in.front().pal;  // archives: raw ranges, gathered on the device
+  // an archive's range (kc cts + their tower headers) is one ring slot: one DMA per learner chunk
+  if (raw && !direct && !switches().wavg_chunk_mib)
+    kc = std::min<uint64_t>(kc, std::max<uint64_t>(1, (stager(ctx).slot_bytes() * 15 / 16) / ct_bytes));
+  kc = std::min<uint64_t>(kc, K);
+  const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
   const size_t pin_chunk = pin ? group * kc * pct : 0, pout_chunk = pout ? kc * pct : 0;
   const uint64_t nchunks = (K + kc - 1) / kc;
   std::vector<HostPiece> pcs;
-  // raw ranges: the largest byte range any learner's chunk spans (tower headers included)
-  size_t raw_cap = 0, runs_cap = 0;
+  // raw ranges: the largest byte range any learner's chunk spans (tower headers included), and the
+  // whole call's gather table -- every step's run offsets into its raw buffer, written once into pinned
+  // memory and uploaded by one copy ahead of the data (no per-step table copies or host waits)
+  size_t raw_cap = 0, runs_total = 0;
+  std::vector<size_t> step_run0;  // step (chunk, learner group) -> its first table entry
   if (raw) {
     for (uint64_t ci = 0; ci < nchunks; ++ci) {
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
       for (size_t c = 0; c < C; ++c) {
         in[c].pieces(k0, kn, p, pcs);
         raw_cap = std::max<size_t>(raw_cap, (size_t)(pcs.back().p + pcs.back().n - pcs.front().p));
+        runs_total += pcs.size();
       }
     }
     raw_cap = (raw_cap + 64 + 255) & ~(size_t)255;  // + the gather's read-ahead of one dword
-    runs_cap = group * kc * 2 * p.L;
-    if (ctx->gather_cap < runs_cap) {
+    if (ctx->gather_cap < runs_total) {
       if (ctx->gather_host) SHELFI_HIP(hipHostFree(ctx->gather_host));
       ctx->gather_host = nullptr;
       ctx->gather_cap = 0;
-      SHELFI_HIP(hipHostMalloc((void**)&ctx->gather_host, 2 * runs_cap * 8, hipHostMallocDefault));
-      ctx->gather_cap = runs_cap;
+      SHELFI_HIP(hipHostMalloc((void**)&ctx->gather_host, runs_total * 8, hipHostMallocDefault));
+      ctx->gather_cap = runs_total;
     }
+    size_t r = 0;
+    for (uint64_t ci = 0; ci < nchunks; ++ci) {
+      const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+      for (size_t c0 = 0; c0 < C; c0 += group) {
+        step_run0.push_back(r);
+        for (size_t c = 0; c < std::min(group, C - c0); ++c) {
+          in[c0 + c].pieces(k0, kn, p, pcs);
+          const uint8_t* lo = pcs.front().p;
+          for (const HostPiece& h : pcs) ctx->gather_host[r++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
+        }
+      }
+    }
+    step_run0.push_back(r);
   }
-  const size_t raw_chunk = raw ? group * raw_cap : 0, tab_chunk = raw ? runs_cap * 8 : 0;
+  const size_t raw_chunk = raw ? group * raw_cap : 0, tab_bytes = (runs_total * 8 + 255) & ~(size_t)255;
   uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes,
-                                 2 * (in_chunk + out_chunk + pin_chunk + pout_chunk + raw_chunk + tab_chunk));
+                                 2 * (in_chunk + out_chunk + pin_chunk + pout_chunk + raw_chunk) + tab_bytes);
   uint8_t* inb[2] = {io, io + in_chunk};
   uint8_t* outb[2] = {io + 2 * in_chunk, io + 2 * in_chunk + out_chunk};
   uint8_t* const pbase = io + 2 * (in_chunk + out_chunk);
@@ -1331,7 +1354,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   uint8_t* poutb[2] = {pbase + 2 * pin_chunk, pbase + 2 * pin_chunk + pout_chunk};
   uint8_t* const rbase = pbase + 2 * (pin_chunk + pout_chunk);
   uint8_t* rawb[2] = {rbase, rbase + raw_chunk};
-  uint64_t* tabd[2] = {(uint64_t*)(rbase + 2 * raw_chunk), (uint64_t*)(rbase + 2 * raw_chunk + tab_chunk)};
+  uint64_t* const tabd = (uint64_t*)(rbase + 2 * raw_chunk);
   const ArenaPack ap = arena_pack(p);
   // A: H2D of the learners' slices; B: wavg; C: staged D2H of the sum
   Pipe pp(ctx);
@@ -1381,36 +1404,31 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   }
   uint32_t* bad = ctx->dev_flag + 3;  // an upload residue >= q (the kernels assume canonical inputs)
   SHELFI_HIP(hipMemsetAsync(bad, 0, 4, pp.b));
+  if (raw) SHELFI_HIP(hipMemcpyAsync(tabd, ctx->gather_host, runs_total * 8, hipMemcpyHostToDevice, pp.a));
   using clk = std::chrono::steady_clock;
   const bool trace = sr.s.trace();
   const auto t_start = clk::now();
-  double t_up = 0.0, t_wait = 0.0;  // SHELFI_STAGE_TRACE: host seconds in the direct uploads / tab waits
+  double t_up = 0.0;  // SHELFI_STAGE_TRACE: host seconds in the uploads
+  // input buffers alternate by step (a learner group of a chunk), the sum's buffers by chunk
+  uint64_t st = 0;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
     for (size_t c0 = 0; c0 < C; c0 += group) {
       const size_t gc = std::min(group, C - c0);
-      if (ci >= 2 || c0 > 0) {  // buffer free
-        SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
-        if (two) SHELFI_HIP(hipStreamWaitEvent(ctx->stream4, pp.computed[b], 0));
+      const int bi = (int)(st & 1);
+      if (st >= 2) {  // buffer free
+        SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[bi], 0));
+        if (two) SHELFI_HIP(hipStreamWaitEvent(ctx->stream4, pp.computed[bi], 0));
       }
-      uint64_t* tabh = raw ? ctx->gather_host + b * runs_cap : nullptr;
-      if (raw && (ci >= 2 || c0 > 0)) {  // tabh's last copy done
-        const auto t0 = clk::now();
-        SHELFI_HIP(hipEventSynchronize(pp.in_ready[b]));
-        if (trace) t_wait += std::chrono::duration<double>(clk::now() - t0).count();
-      }
-      uint64_t runs = 0;
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
         // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked), or
         // (archives) its raw range, gathered below
-        uint8_t* land = raw ? rawb[b] + c * raw_cap : pin ? pinb[b] + c * kn * pct : inb[b] + c * kn * ct_bytes;
+        uint8_t* land = raw ? rawb[bi] + c * raw_cap : pin ? pinb[bi] + c * kn * pct : inb[bi] + c * kn * ct_bytes;
         if (direct) {
           const uint8_t* lo = pcs.front().p;
           const size_t span = (size_t)(pcs.back().p + pcs.back().n - lo);
-          if (raw)
-            for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
           const auto t0 = clk::now();
           if (two && (c & 1))  // every other learner from the second thread: two copies in flight
             ctx->up2->post(land, lo, span, ctx->stream4);
@@ -1421,7 +1439,6 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
           const auto t0 = clk::now();
           if (raw) {
             const uint8_t* lo = pcs.front().p;
-            for (const HostPiece& h : pcs) tabh[runs++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
             const HostPiece whole{const_cast<uint8_t*>(lo), (size_t)(pcs.back().p + pcs.back().n - lo)};
             sr.s.h2dv(land, &whole, 1, pp.a);
           } else {
@@ -1430,23 +1447,24 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
           if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
         }
       }
-      if (raw) SHELFI_HIP(hipMemcpyAsync(tabd[b], tabh, runs * 8, hipMemcpyHostToDevice, pp.a));
       if (two) {  // the second thread's copies of this chunk join stream A
         ctx->up2->wait();
-        SHELFI_HIP(hipEventRecord(up2_done[b], ctx->stream4));
-        SHELFI_HIP(hipStreamWaitEvent(pp.a, up2_done[b], 0));
+        SHELFI_HIP(hipEventRecord(up2_done[bi], ctx->stream4));
+        SHELFI_HIP(hipStreamWaitEvent(pp.a, up2_done[bi], 0));
       }
-      SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
-      SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
-      if (raw) launch_gather_runs(rawb[b], tabd[b], runs, (uint32_t)(p.N * 8), inb[b], pp.b);
+      SHELFI_HIP(hipEventRecord(pp.in_ready[bi], pp.a));
+      SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[bi], 0));
+      if (raw)
+        launch_gather_runs(rawb[bi], tabd + step_run0[st], step_run0[st + 1] - step_run0[st], (uint32_t)(p.N * 8),
+                           inb[bi], pp.b);
       if (pin)  // unpacked on the compute stream, so the upload stream moves on to the next chunk
         for (size_t c = 0; c < gc; ++c)
-          launch_blob_unpack((const uint32_t*)(pinb[b] + c * kn * pct), kn, p.L, p.logN, ap,
-                             (uint64_t*)(inb[b] + c * kn * ct_bytes), pp.b);
+          launch_blob_unpack((const uint32_t*)(pinb[bi] + c * kn * pct), kn, p.L, p.logN, ap,
+                             (uint64_t*)(inb[bi] + c * kn * ct_bytes), pp.b);
       if (ci >= 2 && c0 == 0) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
       WavgArgs a;
       std::memset(&a, 0, sizeof(a));
-      for (size_t c = 0; c < gc; ++c) a.ptrs[c] = (const uint64_t*)(inb[b] + c * kn * ct_bytes);
+      for (size_t c = 0; c < gc; ++c) a.ptrs[c] = (const uint64_t*)(inb[bi] + c * kn * ct_bytes);
       fill_weights(a, p, weights + c0, gc);
       a.out = (uint64_t*)outb[b];
       a.rows = kn * 2 * p.L;
@@ -1456,14 +1474,15 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       a.accumulate = c0 ? 1 : 0;
       a.bad = bad;
       launch_wavg(a, ctx->dt.tc, pp.b);
-      SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+      SHELFI_HIP(hipEventRecord(pp.computed[bi], pp.b));
+      ++st;
       if (c0 + gc >= C) {
         if (pout) {  // the sum is canonical: the residue check cannot fire
           launch_blob_pack((const uint64_t*)outb[b], kn, p.L, p.logN, ap, ctx->dt.tc, (uint32_t*)poutb[b],
                            ctx->dev_flag + 5, pp.b);
-          SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+          SHELFI_HIP(hipEventRecord(pp.computed[bi], pp.b));
         }
-        SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
+        SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[bi], 0));
         dst.pieces(k0, kn, p, pcs);
         const uint8_t* sum = pout ? poutb[b] : outb[b];
         // one DMA into the drain's pinned buffer; its worker scatters it to the pieces
@@ -1481,10 +1500,11 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   sr.finish();
   pp.sync();
   if (trace)
-    std::fprintf(stderr, "[wavg-bytes] %s%s chunks %llu x %llu cts: issue %.2f ms (uploads %.2f, tab waits %.2f), "
-                 "tail %.2f ms\n", direct ? "direct" : "ring", raw ? "+gather" : "", (unsigned long long)nchunks,
-                 (unsigned long long)kc, std::chrono::duration<double>(t_issued - t_start).count() * 1e3, t_up * 1e3,
-                 t_wait * 1e3, std::chrono::duration<double>(clk::now() - t_issued).count() * 1e3);
+    std::fprintf(stderr, "[wavg-bytes] %s%s chunks %llu x %llu cts, %llu learners per group: issue %.2f ms "
+                 "(uploads %.2f), tail %.2f ms\n", direct ? "direct" : "ring", raw ? "+gather" : "",
+                 (unsigned long long)nchunks, (unsigned long long)kc, (unsigned long long)group,
+                 std::chrono::duration<double>(t_issued - t_start).count() * 1e3, t_up * 1e3,
+                 std::chrono::duration<double>(clk::now() - t_issued).count() * 1e3);
   uint32_t flag = 0;
   SHELFI_HIP(hipMemcpy(&flag, bad, 4, hipMemcpyDeviceToHost));
   if (flag) throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed learner data)"};

@@ -259,7 +259,7 @@ struct shelfi_ctx {
   size_t scratch_bytes = 0;
   void* io = nullptr;            // bytes-API staging arena (inputs/outputs)
   size_t io_bytes = 0;
-  uint64_t* gather_host = nullptr;  // pinned run-offset tables of the direct uploads (2 x gather_cap words)
+  uint64_t* gather_host = nullptr;  // pinned run-offset table of a bytes-API aggregation of archives (gather_cap words)
   size_t gather_cap = 0;
   shelfi::EvalState* ev = nullptr;  // EvalMult / ModReduce state (eval.cpp), lazily created
   // RCCL communicator of the multi-GPU combine (comm.cpp; ncclComm_t, opaque here)

@@ -20,10 +20,11 @@ import SHELFI_FHE as m  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--k", type=int, default=64)
+ap.add_argument("--learners", type=int, default=16)
 ap.add_argument("--wire", default="palisade")
 ap.add_argument("settings", nargs="+")
 a = ap.parse_args()
-Cl, Ka, B = 16, a.k, 16384
+Cl, Ka, B = a.learners, a.k, 16384
 d = "/tmp/keys_bytes_cold/"
 os.makedirs(d, exist_ok=True)
 ck = m.CKKS("ckks", B, 52, d, multDepth=3, seed=7)
