@@ -4,7 +4,8 @@ FFT's first pass is one template for both decodes, so the chains are told apart 
 argument -- the 6th of fft_fwd_blocks_ct<BL, K1..K4, FLOOD, SWZ> since round 4's SWZ argument
 (before it, the last one; matching on the last argument silently dropped the exact decode's FFT
 and counted both in the flooded one).  Round 5: the noise moved to the last pass (fft_fwd_cols<LOGR,
-FLOOD>, or the whole-vector fft_fwd_whole<STATS> + flood_add_kernel), and fft_fwd_blocks_ct serves both.
+FLOOD>, or the whole-vector fft_fwd_whole<FLOOD> beside flood_noise_kernel -- flood_add_kernel in the
+r05p data), and fft_fwd_blocks_ct serves both.
 Checked against the committed round-4 and round-5 PMC data."""
 import json
 import os
@@ -47,7 +48,8 @@ def test_each_decrypt_chain_takes_one_fft_pass():
 
 def test_committed_jsons_carry_both_fft_passes():
     """Round 5's committed chains: the exact decrypt takes fft_fwd_whole<false>, the flooded one
-    fft_fwd_whole<true> (its statistics) and flood_add_kernel, and neither takes the other's."""
+    fft_fwd_whole<true> and its noise kernel (flood_noise_kernel; flood_add_kernel in the r05p
+    data), and neither takes the other's."""
     for name in ("encdec_traffic.json", "encdec_valu.json"):
         d = json.load(open(os.path.join(ROOT, "profiles", name)))
         key = "kernels_bytes_per_call" if "traffic" in name else "kernels_wave_instr_per_ct"
@@ -55,7 +57,8 @@ def test_committed_jsons_carry_both_fft_passes():
         fl = [k for k in d["decrypt_flooded"][key] if k.startswith("fft_fwd")]
         assert [ET.flood_arg(k) for k in ex] == ["false"], (name, ex)
         assert [ET.flood_arg(k) for k in fl] == ["true"], (name, fl)
-        assert "flood_add_kernel" in d["decrypt_flooded"][key] and "flood_add_kernel" not in d["decrypt"][key]
+        noise = [k for k in d["decrypt_flooded"][key] if k in ("flood_add_kernel", "flood_noise_kernel")]
+        assert len(noise) == 1 and noise[0] not in d["decrypt"][key], (name, noise)
         assert any(k.startswith("fft_inv_whole") for k in d["encrypt"][key]), name
 
 
