@@ -2,8 +2,9 @@
 """Effective clock per dispatch of the encrypt and decrypt chains (MI355X_MICROARCH.md 'DVFS':
 GRBM_GUI_ACTIVE / 8 XCDs / wall time), from one rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace run:
 counter_collection.csv joined with kernel_trace.csv on the dispatch id.  A call starts at its first
-kernel (fft_inv_cols: encrypt, ntt_inv_blocks_dec: decrypt); a decrypt is labelled exact or flooded by
-its FFT pass (fft_fwd_blocks_ct<..., false|true>).  Prints per call each kernel's us and GHz, then the
+kernel (fft_inv_cols / fft_inv_whole since round 5: encrypt, ntt_inv_blocks_dec: decrypt); a decrypt is
+labelled exact or flooded by its FFT pass's FLOOD argument (tools/encdec_traffic.py flood_arg: fft_fwd_blocks_ct
+in rounds 3-4, fft_fwd_cols / fft_fwd_whole since round 5) or a flooding kernel of its own.  Prints per call each kernel's us and GHz, then the
 medians per label (and writes them as JSON with -o).
   python tools/grbm_clock.py DIR [-o clock.json]"""
 import collections
@@ -14,7 +15,11 @@ import statistics
 import json
 import sys
 
-STARTS = ("fft_inv_cols", "ntt_inv_blocks_dec")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from encdec_traffic import flood_arg  # noqa: E402
+
+STARTS = ("fft_inv_cols", "fft_inv_whole", "ntt_inv_blocks_dec")
+FLOOD_KERNELS = ("flood_add_kernel", "decode_stats_kernel", "decode_flood_kernel")
 
 
 def main():
@@ -50,14 +55,11 @@ def main():
         names = [n for n, _, _ in c]
         if not names[0].startswith(STARTS):
             continue
-        # fft_fwd_blocks_ct<BL, K1, K2, K3, K4, FLOOD[, SWZ]>: the sixth template argument
-        def flood_arg(n):
-            args = n[n.index("<") + 1:n.rindex(">")].split(",")
-            return len(args) >= 6 and args[5].strip() == "true"
-        if names[0].startswith("fft_inv_cols"):
+        if names[0].startswith(("fft_inv_cols", "fft_inv_whole")):
             label = "encrypt"
         else:
-            label = "flooded" if any(n.startswith("fft_fwd_blocks_ct") and flood_arg(n) for n in names) else "exact"
+            label = "flooded" if any(n.startswith(FLOOD_KERNELS) or (n.startswith("fft_fwd") and flood_arg(n) == "true")
+                                     for n in names) else "exact"
         print("%-8s " % label + "  ".join("%s %.1fus %.2fGHz" % (n.split("<")[0], us, g) for n, us, g in c
                                          if not n.startswith("__amd")))
         for n, us, g in c:
