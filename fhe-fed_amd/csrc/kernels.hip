@@ -1114,6 +1114,11 @@ __global__ __launch_bounds__(1 << (BL - 3)) void fft_inv_blocks_ct(double2* __re
 // The closed forms below are those paddings of the set shapes 4 (l + 64 q) + r (m = 4 q + r),
 // 64 (l >> 2) + (l & 3) + 4 m and l + 64 m, for lane l and register m.
 constexpr uint32_t kFftWholeLogS = 14;
+// One 1024-thread workgroup per vector fills the chip only for batches of hundreds of ciphertexts: below
+// kFftWholeMinK the multi-pass FFTs (many workgroups per vector) are faster -- at K = 4 / 16 / 64 encrypt
+// 21.3 / 6.9 / 3.70 vs 24.9 / 7.7 / 3.73 us/ct, decrypt 10.5 / 3.5 / 1.53 vs 13.7 / 4.2 / 1.64; at K = 256
+// the whole-vector kernels win, 2.93 vs 2.97 and 0.99 vs 1.03 (profiles/r05zc/small_k.txt)
+constexpr uint64_t kFftWholeMinK = 128;
 constexpr uint32_t kFftWholeRow = 1088;  // doubles per 1024-element block slice (the largest padding, 1087)
 __device__ __forceinline__ uint32_t fft_wpad(uint32_t e) { return e + (e >> 5); }
 __device__ __forceinline__ uint32_t fft_wt1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
@@ -1642,7 +1647,7 @@ static void launch_encode_fft(const Params& p, const DeviceTables& dt, const dou
   const uint32_t blkLog = fft_block_log(logS);
   const int logR = (int)(logS - blkLog);
   const size_t lds = sizeof(double2) << blkLog;
-  if (logS == kFftWholeLogS && switches().fft_whole) {  // one workgroup per vector, no HBM intermediate
+  if (logS == kFftWholeLogS && K >= kFftWholeMinK && switches().fft_whole) {  // a workgroup per vector
     hipLaunchKernelGGL(fft_inv_whole, dim3((uint32_t)K), dim3(1024), 0, s, x, n, fbuf, dt.fft_inv);
   } else if (logR > 0) {
     const uint64_t nb = K * ((p.batch >> logR) / 256);
@@ -2813,7 +2818,7 @@ NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s
   const size_t lds = sizeof(double2) << fblkLog;
   FloodArgs fa{};
   bool fused_flood = false;
-  const bool whole = logS == kFftWholeLogS && switches().fft_whole;  // fft_fwd_whole
+  const bool whole = logS == kFftWholeLogS && K >= kFftWholeMinK && switches().fft_whole;  // fft_fwd_whole
   if (dn && dn->enabled) {
     for (int i = 0; i < 8; ++i) fa.key.k[i] = dn->key[i];
     fa.two_p = ldexp(1.0, (int)dn->p_bits);

@@ -23,7 +23,7 @@ from SHELFI_FHE import device as D  # noqa: E402
 ENC_DEC_SWITCHES = [
     ("SHELFI_NTT_WL", "0"),          # workgroup barrier at every block-pass exchange
     ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
-    ("SHELFI_FFT_WHOLE", "0"),       # separate columns / blocks FFT passes at 2^14 slots
+    ("SHELFI_FFT_WHOLE", "0"),       # no-op at K = 7 (whole-vector FFTs from K = 128: test_whole_vector_ffts_match_multipass)
     ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
     ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
     ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
@@ -91,27 +91,63 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
 
 
 @pytest.mark.parametrize("wire", ["palisade", "shelfi", "packed"])
-@pytest.mark.parametrize("mode", ["chunk1", "ring", "ring_chunk1", "one_thread"])
+@pytest.mark.parametrize("mode", ["chunk1", "direct", "direct_chunk1", "direct_one_thread"])
 def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
-    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (direct uploads, 512 MiB of
-    input per learner group: one chunk here) against one ciphertext per chunk (7 chunks through the two
-    device buffer sets), the pinned staging ring (SHELFI_H2D_DIRECT=0), both, and direct uploads from the
-    calling thread alone (SHELFI_H2D_TWO=0): the same aggregate, byte for byte, in every wire format (archives
-    take the raw-range + device gather path)."""
+    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (the pinned staging ring; 5
+    learners x 7 cts fit one chunk, so they are cut into learner groups of 2 whose sums accumulate) against one
+    ciphertext per chunk (7 chunks through the two device buffer sets), direct pageable uploads
+    (SHELFI_H2D_DIRECT=1: no learner groups), both, and direct uploads from the calling thread alone
+    (SHELFI_H2D_TWO=0): the same aggregate, byte for byte, in every wire format (archives take the raw-range +
+    device gather path)."""
     ck, x, _, _ = ctx
     xs = x.cpu().numpy()
     ck.set_wire_format(wire)
     try:
-        blobs = [ck.encrypt(xs * (i + 1) / 4) for i in range(3)]
-        w = [0.5, 0.25, 0.25]
+        blobs = [ck.encrypt(xs * (i + 1) / 4) for i in range(5)]
+        w = [0.4, 0.2, 0.2, 0.1, 0.1]
         ref = ck.computeWeightedAverage(blobs, w)
-        if mode in ("chunk1", "ring_chunk1"):
+        if mode in ("chunk1", "direct_chunk1"):
             set_switch(monkeypatch, "SHELFI_WAVG_CHUNK_MIB", "1")
-        if mode in ("ring", "ring_chunk1"):
-            set_switch(monkeypatch, "SHELFI_H2D_DIRECT", "0")
-        if mode == "one_thread":
+        if mode.startswith("direct"):
+            set_switch(monkeypatch, "SHELFI_H2D_DIRECT", "1")
+        if mode == "direct_one_thread":
             set_switch(monkeypatch, "SHELFI_H2D_TWO", "0")
         got = ck.computeWeightedAverage(blobs, w)
     finally:
         ck.set_wire_format("palisade")
     assert got == ref
+
+
+def test_whole_vector_ffts_match_multipass(tmp_path, monkeypatch):
+    """The whole-vector encode / decode FFTs (fft_inv_whole, fft_fwd_whole<flag>) run only for batches of
+    >= kFftWholeMinK = 128 ciphertexts at 2^14 slots: 130 ciphertexts through them and through the multi-pass
+    FFTs (SHELFI_FFT_WHOLE=0) give the same ciphertexts and the same exact and flooded decodes, bit for bit
+    (the multi-pass chains are pinned against the oracle in test_gpu_parity / test_gpu_decode_noise)."""
+    d = str(tmp_path) + os.sep
+    ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
+    assert ck.genCryptoContextAndKeyGen() == 1
+    inf = ck.info()
+    K = 130
+    g = torch.Generator(device="cuda").manual_seed(12)
+    x = torch.rand(K * inf["batch"] - 5, generator=g, device="cuda", dtype=torch.float64) * 2 - 1
+
+    def run():
+        ck.set_seed(SEED)
+        ct = D.encrypt(ck, x)
+        ck.set_decode_noise(False)
+        dec = D.decrypt(ck, ct, x.numel(), inf["delta"])
+        ck.set_seed(SEED + 1)
+        ck.set_decode_noise(True)
+        fl = D.decrypt(ck, ct, x.numel(), inf["delta"])
+        ck.set_decode_noise(False)
+        torch.cuda.synchronize()
+        return ct, dec, fl
+
+    ct1, dec1, fl1 = run()
+    set_switch(monkeypatch, "SHELFI_FFT_WHOLE", "0")
+    ct0, dec0, fl0 = run()
+    assert torch.equal(ct1, ct0)
+    assert torch.equal(dec1, dec0)
+    assert torch.equal(fl1, fl0)
+    assert float((dec1 - x).abs().max()) < 1e-8
+    assert not torch.equal(fl1, dec1) and float((fl1 - x).abs().max()) < 1e-6
