@@ -1119,6 +1119,7 @@ constexpr uint32_t kFftWholeLogS = 14;
 // 21.3 / 6.9 / 3.70 vs 24.9 / 7.7 / 3.73 us/ct, decrypt 10.5 / 3.5 / 1.53 vs 13.7 / 4.2 / 1.64; at K = 256
 // the whole-vector kernels win, 2.93 vs 2.97 and 0.99 vs 1.03 (profiles/r05zc/small_k.txt)
 constexpr uint64_t kFftWholeMinK = 128;
+constexpr uint64_t kEncNoredMinK = 192;  // launch_encrypt: the NORED tower split from this many ciphertexts
 constexpr uint32_t kFftWholeRow = 1088;  // doubles per 1024-element block slice (the largest padding, 1087)
 __device__ __forceinline__ uint32_t fft_wpad(uint32_t e) { return e + (e >> 5); }
 __device__ __forceinline__ uint32_t fft_wt1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
@@ -1695,7 +1696,11 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   while (t_split < p.L && p.q[t_split] >= kNoRedQ) ++t_split;
   for (uint32_t t = t_split; t < p.L; ++t)
     if (p.q[t] >= kNoRedQ) t_split = p.L;
-  if (!pp || !sw.enc_nored) t_split = p.L;
+  // the two tower classes take one blocks-pass launch each, in series; below kEncNoredMinK ciphertexts a
+  // call is latency-bound and one launch over every tower (all reduced) is faster: K = 4 / 16 / 64 / 128
+  // encrypt 18.7 / 6.5 / 3.67 / 3.23 vs 21.2 / 6.9 / 3.76 / 3.28 us/ct, K = 256 2.92 vs 2.88
+  // (profiles/r05zc/nored_k.txt; tests/test_gpu_switches.py checks both paths bit for bit at K = 200)
+  if (!pp || !sw.enc_nored || K < kEncNoredMinK) t_split = p.L;
   bool vt = false;  // NTT(v)'s columns pass as enc_vtab sums in the blocks pass (round 5)
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower

@@ -23,10 +23,10 @@ from SHELFI_FHE import device as D  # noqa: E402
 ENC_DEC_SWITCHES = [
     ("SHELFI_NTT_WL", "0"),          # workgroup barrier at every block-pass exchange
     ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
-    ("SHELFI_FFT_WHOLE", "0"),       # no-op at K = 7 (whole-vector FFTs from K = 128: test_whole_vector_ffts_match_multipass)
+    ("SHELFI_FFT_WHOLE", "0"),       # no-op at K = 7 (whole-vector FFTs from K = 128: test_large_batch_paths_...)
     ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
     ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
-    ("SHELFI_ENC_NORED", "0"),       # reductions in every tower
+    ("SHELFI_ENC_NORED", "0"),       # no-op at K = 7 (the NORED split from K = 192: test_large_batch_paths_...)
     ("SHELFI_ENC_TAB", "0"),         # butterflies instead of the small-polynomial tables
     ("SHELFI_ENC_VT", "0"),          # v's columns pass in enc_cols_fused, not table sums in the blocks pass
     ("SHELFI_ENC_FUSED_COLS", "0"),  # enc_prep_kernel + three column passes
@@ -118,16 +118,18 @@ def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
     assert got == ref
 
 
-def test_whole_vector_ffts_match_multipass(tmp_path, monkeypatch):
-    """The whole-vector encode / decode FFTs (fft_inv_whole, fft_fwd_whole<flag>) run only for batches of
-    >= kFftWholeMinK = 128 ciphertexts at 2^14 slots: 130 ciphertexts through them and through the multi-pass
-    FFTs (SHELFI_FFT_WHOLE=0) give the same ciphertexts and the same exact and flooded decodes, bit for bit
-    (the multi-pass chains are pinned against the oracle in test_gpu_parity / test_gpu_decode_noise)."""
+def test_large_batch_paths_match_small_batch_paths(tmp_path, monkeypatch):
+    """Two choices depend on the batch: the whole-vector encode / decode FFTs (fft_inv_whole,
+    fft_fwd_whole<flag>) run from kFftWholeMinK = 128 ciphertexts at 2^14 slots, and the encrypt's NORED tower
+    split (two blocks-pass launches) from kEncNoredMinK = 192.  200 ciphertexts through the large-batch paths,
+    through the multi-pass FFTs (SHELFI_FFT_WHOLE=0) and through one all-reduced blocks pass
+    (SHELFI_ENC_NORED=0) give the same ciphertexts and the same exact and flooded decodes, bit for bit (the
+    small-batch chains are pinned against the oracle in test_gpu_parity / test_gpu_decode_noise)."""
     d = str(tmp_path) + os.sep
     ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
     inf = ck.info()
-    K = 130
+    K = 200
     g = torch.Generator(device="cuda").manual_seed(12)
     x = torch.rand(K * inf["batch"] - 5, generator=g, device="cuda", dtype=torch.float64) * 2 - 1
 
@@ -144,10 +146,12 @@ def test_whole_vector_ffts_match_multipass(tmp_path, monkeypatch):
         return ct, dec, fl
 
     ct1, dec1, fl1 = run()
-    set_switch(monkeypatch, "SHELFI_FFT_WHOLE", "0")
-    ct0, dec0, fl0 = run()
-    assert torch.equal(ct1, ct0)
-    assert torch.equal(dec1, dec0)
-    assert torch.equal(fl1, fl0)
+    for var in ("SHELFI_FFT_WHOLE", "SHELFI_ENC_NORED"):
+        set_switch(monkeypatch, var, "0")
+        ct0, dec0, fl0 = run()
+        assert torch.equal(ct1, ct0), var
+        assert torch.equal(dec1, dec0), var
+        assert torch.equal(fl1, fl0), var
+        set_switch(monkeypatch, var, None)
     assert float((dec1 - x).abs().max()) < 1e-8
     assert not torch.equal(fl1, dec1) and float((fl1 - x).abs().max()) < 1e-6
