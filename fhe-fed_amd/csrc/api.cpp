@@ -1114,7 +1114,7 @@ static Stager& stager(shelfi_ctx* ctx) {
 struct StageRun {
   Stager& s;
   bool done = false;
-  explicit StageRun(Stager& st) : s(st) {}
+  explicit StageRun(Stager& st) : s(st) { s.begin(); }
   void finish() {
     s.finish();
     done = true;
@@ -1300,26 +1300,29 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
   const bool pin = in.front().packed, pout = dst.packed;
   const bool raw = in.front().pal;  // archives: raw ranges, gathered on the device
-  // an archive's range (kc cts + their tower headers) is one ring slot: one DMA per learner chunk
-  if (raw && !direct && !switches().wavg_chunk_mib)
-    kc = std::min<uint64_t>(kc, std::max<uint64_t>(1, (stager(ctx).slot_bytes() * 15 / 16) / ct_bytes));
   kc = std::min<uint64_t>(kc, K);
   const size_t in_chunk = group * kc * ct_bytes, out_chunk = kc * ct_bytes;
   const size_t pin_chunk = pin ? group * kc * pct : 0, pout_chunk = pout ? kc * pct : 0;
   const uint64_t nchunks = (K + kc - 1) / kc;
   std::vector<HostPiece> pcs;
-  // raw ranges: the largest byte range any learner's chunk spans (tower headers included), and the
-  // whole call's gather table -- every step's run offsets into its raw buffer, written once into pinned
-  // memory and uploaded by one copy ahead of the data (no per-step table copies or host waits)
-  size_t raw_cap = 0, runs_total = 0;
-  std::vector<size_t> step_run0;  // step (chunk, learner group) -> its first table entry
+  // raw ranges: a step's (chunk, learner group) learners' byte ranges (tower headers included) land back to
+  // back in its raw buffer, so the ring packs them into full slots (one DMA per slot, not per learner: each
+  // DMA costs ~17 us of gap on the copy engine, profiles/r05cp); the whole call's gather table -- every
+  // step's run offsets into its raw buffer -- is written once into pinned memory and uploaded by one copy
+  // ahead of the data (no per-step table copies or host waits)
+  size_t raw_cap = 0, runs_total = 0;  // raw_cap: the largest step's bytes
+  std::vector<size_t> step_run0;       // step -> its first table entry
   if (raw) {
     for (uint64_t ci = 0; ci < nchunks; ++ci) {
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
-      for (size_t c = 0; c < C; ++c) {
-        in[c].pieces(k0, kn, p, pcs);
-        raw_cap = std::max<size_t>(raw_cap, (size_t)(pcs.back().p + pcs.back().n - pcs.front().p));
-        runs_total += pcs.size();
+      for (size_t c0 = 0; c0 < C; c0 += group) {
+        size_t bytes = 0;
+        for (size_t c = c0; c < std::min(C, c0 + group); ++c) {
+          in[c].pieces(k0, kn, p, pcs);
+          bytes += (size_t)(pcs.back().p + pcs.back().n - pcs.front().p);
+          runs_total += pcs.size();
+        }
+        raw_cap = std::max(raw_cap, bytes);
       }
     }
     raw_cap = (raw_cap + 64 + 255) & ~(size_t)255;  // + the gather's read-ahead of one dword
@@ -1335,16 +1338,18 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
       for (size_t c0 = 0; c0 < C; c0 += group) {
         step_run0.push_back(r);
-        for (size_t c = 0; c < std::min(group, C - c0); ++c) {
-          in[c0 + c].pieces(k0, kn, p, pcs);
+        size_t off = 0;
+        for (size_t c = c0; c < std::min(C, c0 + group); ++c) {
+          in[c].pieces(k0, kn, p, pcs);
           const uint8_t* lo = pcs.front().p;
-          for (const HostPiece& h : pcs) ctx->gather_host[r++] = (uint64_t)(c * raw_cap + (size_t)(h.p - lo));
+          for (const HostPiece& h : pcs) ctx->gather_host[r++] = (uint64_t)(off + (size_t)(h.p - lo));
+          off += (size_t)(pcs.back().p + pcs.back().n - lo);
         }
       }
     }
     step_run0.push_back(r);
   }
-  const size_t raw_chunk = raw ? group * raw_cap : 0, tab_bytes = (runs_total * 8 + 255) & ~(size_t)255;
+  const size_t raw_chunk = raw ? raw_cap : 0, tab_bytes = (runs_total * 8 + 255) & ~(size_t)255;
   uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes,
                                  2 * (in_chunk + out_chunk + pin_chunk + pout_chunk + raw_chunk) + tab_bytes);
   uint8_t* inb[2] = {io, io + in_chunk};
@@ -1411,6 +1416,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   double t_up = 0.0;  // SHELFI_STAGE_TRACE: host seconds in the uploads
   // input buffers alternate by step (a learner group of a chunk), the sum's buffers by chunk
   uint64_t st = 0;
+  std::vector<HostPiece> grp;  // a step's host pieces, in landing order
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
@@ -1421,31 +1427,35 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
         SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[bi], 0));
         if (two) SHELFI_HIP(hipStreamWaitEvent(ctx->stream4, pp.computed[bi], 0));
       }
+      // where the uploads land: the learners' uint64 slots, or their packed staging (then unpacked), or
+      // (archives) their raw ranges back to back, gathered below -- contiguous in every case, so through
+      // the ring the whole group is one gather of pieces
+      uint8_t* const land0 = raw ? rawb[bi] : pin ? pinb[bi] : inb[bi];
+      size_t off = 0;
+      grp.clear();
       for (size_t c = 0; c < gc; ++c) {
         in[c0 + c].pieces(k0, kn, p, pcs);
-        // where the upload lands: the learner's uint64 slot, or its packed staging (then unpacked), or
-        // (archives) its raw range, gathered below
-        uint8_t* land = raw ? rawb[bi] + c * raw_cap : pin ? pinb[bi] + c * kn * pct : inb[bi] + c * kn * ct_bytes;
-        if (direct) {
-          const uint8_t* lo = pcs.front().p;
-          const size_t span = (size_t)(pcs.back().p + pcs.back().n - lo);
+        const uint8_t* lo = pcs.front().p;
+        const size_t span = (size_t)(pcs.back().p + pcs.back().n - lo);
+        if (direct) {  // one pageable copy of the learner's whole range
+          uint8_t* land = land0 + (raw ? off : c * kn * (pin ? pct : ct_bytes));
           const auto t0 = clk::now();
           if (two && (c & 1))  // every other learner from the second thread: two copies in flight
             ctx->up2->post(land, lo, span, ctx->stream4);
           else
             SHELFI_HIP(hipMemcpyAsync(land, lo, span, hipMemcpyHostToDevice, pp.a));
           if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
-        } else {  // through the pinned ring: an archive's whole range (one piece), else the pieces
-          const auto t0 = clk::now();
-          if (raw) {
-            const uint8_t* lo = pcs.front().p;
-            const HostPiece whole{const_cast<uint8_t*>(lo), (size_t)(pcs.back().p + pcs.back().n - lo)};
-            sr.s.h2dv(land, &whole, 1, pp.a);
-          } else {
-            sr.s.h2dv(land, pcs.data(), pcs.size(), pp.a);
-          }
-          if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
+        } else if (raw) {
+          grp.push_back(HostPiece{const_cast<uint8_t*>(lo), span});
+        } else {
+          grp.insert(grp.end(), pcs.begin(), pcs.end());
         }
+        off += span;
+      }
+      if (!direct) {
+        const auto t0 = clk::now();
+        sr.s.h2dv(land0, grp.data(), grp.size(), pp.a);
+        if (trace) t_up += std::chrono::duration<double>(clk::now() - t0).count();
       }
       if (two) {  // the second thread's copies of this chunk join stream A
         ctx->up2->wait();
@@ -1482,15 +1492,18 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
                            ctx->dev_flag + 5, pp.b);
           SHELFI_HIP(hipEventRecord(pp.computed[bi], pp.b));
         }
-        SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[bi], 0));
+        // the last chunk's D2H follows its wavg on the compute stream (nothing is left to overlap, and the
+        // cross-stream event cost ~0.1 ms before it: profiles/r05cp)
+        const hipStream_t ds = ci + 1 == nchunks ? pp.b : pp.c;
+        if (ds == pp.c) SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[bi], 0));
         dst.pieces(k0, kn, p, pcs);
         const uint8_t* sum = pout ? poutb[b] : outb[b];
         // one DMA into the drain's pinned buffer; its worker scatters it to the pieces
         size_t nbytes = 0;
         for (const HostPiece& h : pcs) nbytes += h.n;
         uint8_t* hb = ctx->drain->buffer(b, nbytes);  // waits until chunk ci - 2 is drained
-        SHELFI_HIP(hipMemcpyAsync(hb, sum, nbytes, hipMemcpyDeviceToHost, pp.c));
-        SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+        SHELFI_HIP(hipMemcpyAsync(hb, sum, nbytes, hipMemcpyDeviceToHost, ds));
+        SHELFI_HIP(hipEventRecord(pp.out_free[b], ds));
         ctx->drain->post(b, pp.out_free[b], pcs);
       }
     }

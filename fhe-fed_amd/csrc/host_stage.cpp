@@ -240,8 +240,9 @@ void Stager::h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s) 
     wait_in_slot(sl);
     size_t fill = 0;
     jobs.clear();
-    while (pi < np && fill < slot_bytes_) {
-      const size_t take = std::min(pieces[pi].n - po, slot_bytes_ - fill);
+    const size_t cap = ramp_ < 2 ? slot_bytes_ >> (2 - ramp_) : slot_bytes_;
+    while (pi < np && fill < cap) {
+      const size_t take = std::min(pieces[pi].n - po, cap - fill);
       if (take) jobs.push_back(CopyJob{sl.host + fill, pieces[pi].p + po, take});
       fill += take;
       po += take;
@@ -251,6 +252,7 @@ void Stager::h2dv(void* dev, const HostPiece* pieces, size_t np, hipStream_t s) 
       }
     }
     if (!fill) break;
+    if (ramp_ < 2) ++ramp_;
     const auto t0 = std::chrono::steady_clock::now();
     pool_.copy_many(jobs.data(), jobs.size(), h2d_parts_);
     if (trace_) {

@@ -92,6 +92,10 @@ class Stager {
   // Scatter: contiguous device bytes at `dev` go to the pieces, in order (written
   // later, like d2h).
   void d2hv(const HostPiece* pieces, size_t np, const void* dev, hipStream_t s);
+  // A call's first uploads ramp up: the first input slots are filled to a quarter and a half of a slot, so
+  // the copy engine starts after a 4 MiB fill instead of a 16 MiB one (the fill runs ~2x the DMA rate, so
+  // each slot is ready before the previous DMA ends).
+  void begin() { ramp_ = 0; }
   // Drain every output slot whose DMA has completed (non-blocking).
   void poll();
   // Drain all outputs and wait for all inputs.  Must be called before the host
@@ -129,6 +133,7 @@ class Stager {
   // compete with the DMA engine reading pinned memory; 4 of 8 measured +8-16% H2D,
   // DESIGN.md §5.3).  Drains into fresh output pages keep the whole pool (page faults).
   int h2d_parts_ = 1;
+  int ramp_ = 2;  // begin(): 0, then the first slots hold slot_bytes_ >> (2 - ramp_)
 };
 
 // Ask for transparent huge pages on the 2 MiB-aligned interior of a large output
