@@ -1284,11 +1284,10 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   const Params& p = ctx->p;
   const size_t ct_bytes = 2ull * p.L * p.N * 8;
   const bool direct = switches().h2d_direct;
-  // learners per wavg launch: all of them (up to kWavgMaxLearners), except that a call whose cts fit
-  // one chunk is cut into ~4 learner groups so the uploads overlap the gathers / wavgs (accumulated
-  // mod q, so bit-identical): cfg2's 16 x 4 cts otherwise upload everything before any device work
-  size_t group = std::min<size_t>(C, kWavgMaxLearners);
-  if (!direct && C >= 4 && K * ct_bytes * group <= (128ull << 20)) group = (std::min<size_t>(C, kWavgMaxLearners) + 3) / 4;
+  // learners per wavg launch: all of them, up to kWavgMaxLearners (more: accumulated groups).  Cutting a
+  // single-chunk call (cfg2's 16 x 4 cts) into 2 / 4 / 8 groups to overlap uploads with the device work
+  // measured the same as one group once a step's learners share the ring's slots (profiles/r05ct)
+  const size_t group = std::min<size_t>(C, kWavgMaxLearners);
   // chunk of input per learner-group buffer: direct uploads want ~32 MiB per copy (8 MiB copies ran
   // 51.6 GB/s, 2 MiB 41.3, 32 MiB 55.6, on pinned-warm blobs), so 32 MiB per learner; through the ring
   // ~128 MiB per group (round 4: 32 / 64 / 128 / 256 MiB ran 60.4 / 52.4 / 48.2 / 48.7 ms for 16 learners x
@@ -1508,6 +1507,7 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
       }
     }
   }
+  SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 3, bad, 4, hipMemcpyDeviceToHost, pp.b));  // pinned: no sync copy
   const auto t_issued = clk::now();
   ctx->drain->finish();
   sr.finish();
@@ -1518,9 +1518,8 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
                  (unsigned long long)nchunks, (unsigned long long)kc, (unsigned long long)group,
                  std::chrono::duration<double>(t_issued - t_start).count() * 1e3, t_up * 1e3,
                  std::chrono::duration<double>(clk::now() - t_issued).count() * 1e3);
-  uint32_t flag = 0;
-  SHELFI_HIP(hipMemcpy(&flag, bad, 4, hipMemcpyDeviceToHost));
-  if (flag) throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed learner data)"};
+  if (ctx->host_flag[3])  // read back on pp.b before the sync above
+    throw Error{SHELFI_ERR_FORMAT, "ciphertext residue >= its tower modulus (malformed learner data)"};
 }
 
 int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, const size_t* lens,

@@ -93,12 +93,11 @@ def test_wavg_switch_bitexact(ctx, monkeypatch, var, val, C):
 @pytest.mark.parametrize("wire", ["palisade", "shelfi", "packed"])
 @pytest.mark.parametrize("mode", ["chunk1", "direct", "direct_chunk1", "direct_one_thread"])
 def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
-    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (the pinned staging ring; 5
-    learners x 7 cts fit one chunk, so they are cut into learner groups of 2 whose sums accumulate) against one
-    ciphertext per chunk (7 chunks through the two device buffer sets), direct pageable uploads
-    (SHELFI_H2D_DIRECT=1: no learner groups), both, and direct uploads from the calling thread alone
-    (SHELFI_H2D_TWO=0): the same aggregate, byte for byte, in every wire format (archives take the raw-range +
-    device gather path)."""
+    """The bytes API's aggregation pipeline (wavg_bytes_pipeline) at its default (the pinned staging ring, a
+    step's learners packed back to back into its slots; 5 learners x 7 cts fit one chunk) against one ciphertext
+    per chunk (7 chunks through the two device buffer sets), direct pageable uploads (SHELFI_H2D_DIRECT=1: one
+    copy per learner), both, and direct uploads from the calling thread alone (SHELFI_H2D_TWO=0): the same
+    aggregate, byte for byte, in every wire format (archives take the raw-range + device gather path)."""
     ck, x, _, _ = ctx
     xs = x.cpu().numpy()
     ck.set_wire_format(wire)
