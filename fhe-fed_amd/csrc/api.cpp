@@ -1294,6 +1294,10 @@ static void wavg_bytes_pipeline(shelfi_ctx* ctx, const std::vector<CtLayout>& in
   // 64 cts, profiles/r04w/api_chunk.txt); SHELFI_WAVG_CHUNK_MIB overrides (A/B probe switch)
   const uint64_t chunk_mib = switches().wavg_chunk_mib ? switches().wavg_chunk_mib : direct ? 32 * group : 128;
   uint64_t kc = std::max<uint64_t>(1, (chunk_mib << 20) / (ct_bytes * group));
+  // at least ~4 chunks through the ring, so a small call's gather + wavg + D2H overlap its later uploads: cfg2's
+  // 16 x 4 cts in 4 chunks ran 41.0 / 44.4 / 42.8 GB/s (fresh copies / fresh encrypt outputs / warm) vs 39.0 /
+  // 41.8 / 40.5 in one (profiles/r05cy)
+  if (!direct && !switches().wavg_chunk_mib) kc = std::min<uint64_t>(kc, std::max<uint64_t>(1, (K + 3) / 4));
   // packed wire (version-2 blobs): uploads land packed and are unpacked on the device; a packed
   // output is packed before its D2H
   const uint64_t pct = 2 * packed_poly_bytes(p, p.L);
