@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 5: cfg2-shaped bytes-API calls cut into 1 / 2 / 4 / 8 learner groups (temporary A/B)
+# (SHELFI_WAVG_GROUPS_AB was a temporary switch of that A/B build; removed with the group split: DESIGN.md §5.3)
 set -uo pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 5: flooded decrypt, noise drawn on a side stream vs in line (bench, alternated)
+# (SHELFI_FLOOD_SIDE belonged to the reverted side-stream build; the switch no longer exists: DESIGN.md §4.3 item 8)
 set -uo pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
