@@ -146,7 +146,40 @@ static void validate_params(uint32_t N, uint32_t L, uint32_t scale_bits, uint32_
     throw Error{SHELFI_ERR_ARG, "firstModBits must be in [scaleFactorBits, 60]"};
 }
 
+// Little-endian 30-bit limbs (the decode CRT's tables): the product of q[0..L) (except q[skip]), its
+// two's-complement negation, mod 2^(30 n).
+static std::vector<uint64_t> mw30_mul(std::vector<uint64_t> a, uint64_t m) {
+  u128 carry = 0;
+  for (auto& x : a) {
+    const u128 v = (u128)x * m + carry;
+    x = (uint64_t)v & ((1u << 30) - 1);
+    carry = v >> 30;
+  }
+  return a;
+}
+static std::vector<uint64_t> mw30_qhat(const uint64_t* q, uint32_t L, uint32_t skip, uint32_t n) {
+  std::vector<uint64_t> a(n, 0);
+  a[0] = 1;
+  for (uint32_t u = 0; u < L; ++u)
+    if (u != skip) a = mw30_mul(std::move(a), q[u]);
+  return a;
+}
+static std::vector<uint64_t> mw30_prod(const uint64_t* q, uint32_t L, uint32_t n) {
+  return mw30_qhat(q, L, L, n);
+}
+static std::vector<uint64_t> mw30_neg(std::vector<uint64_t> a, uint32_t n) {
+  uint64_t carry = 1;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t v = ((~a[j]) & ((1u << 30) - 1)) + carry;
+    a[j] = v & ((1u << 30) - 1);
+    carry = v >> 30;
+  }
+  return a;
+}
+
 void free_ntt_tables(DeviceTables& dt) {
+  dfree_t(dt.crt_mw);
+  dt.crt_nc = 0;
   dfree_t(dt.tc);
   dfree_t(dt.psi_rev);
   dfree_t(dt.psi_rev_sh);
@@ -194,8 +227,6 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
   const uint32_t N = p.N, L = p.L;
   std::vector<TowerConst> tc(L);
   std::vector<uint64_t> pr((size_t)L * N), prs((size_t)L * N), ipr((size_t)L * N), iprs((size_t)L * N);
-  u128 Q128 = 1;
-  for (uint32_t t = 0; t < L; ++t) Q128 *= p.q[t];  // Q mod 2^128
   for (uint32_t t = 0; t < L; ++t) {
     const uint64_t q = p.q[t];
     TowerConst& c = tc[t];
@@ -211,22 +242,18 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
     c.ninv = invmod(N % q, q);
     c.ninv_shoup = shoup(c.ninv, q);
     uint64_t qhat_mod = 1;
-    u128 qhat128 = 1;
     for (uint32_t u = 0; u < L; ++u)
-      if (u != t) {
-        qhat_mod = (uint64_t)(((u128)qhat_mod * (p.q[u] % q)) % q);
-        qhat128 *= p.q[u];
-      }
+      if (u != t) qhat_mod = (uint64_t)(((u128)qhat_mod * (p.q[u] % q)) % q);
     c.qhat_inv = invmod(qhat_mod, q);
     c.qhat_inv_shoup = shoup(c.qhat_inv, q);
     c.ninv_qhat = (uint64_t)(((u128)c.ninv * c.qhat_inv) % q);
     c.ninv_qhat_shoup = shoup(c.ninv_qhat, q);
-    c.qhat_lo = (uint64_t)qhat128;
-    c.qhat_hi = (uint64_t)(qhat128 >> 64);
-    const u128 nQ = (u128)0 - Q128;  // 2^128 - Q mod 2^128
-    for (int j = 0; j < 5; ++j) {
-      c.crt30[j] = (uint32_t)((qhat128 >> (30 * j)) & ((1u << 30) - 1));
-      c.nq30[j] = (uint32_t)((nQ >> (30 * j)) & ((1u << 30) - 1));
+    {
+      const std::vector<uint64_t> qh = mw30_qhat(p.q, L, t, 7), nq = mw30_neg(mw30_prod(p.q, L, 7), 7);
+      for (int j = 0; j < 7; ++j) {
+        c.crt30[j] = (uint32_t)qh[j];
+        c.nq30[j] = (uint32_t)nq[j];
+      }
     }
     c.inv_q = 1.0 / (double)q;
     c.nq = (uint64_t)0 - q;
@@ -258,8 +285,30 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
     c.ninv_qhat_w1 = (uint64_t)(((u128)c.ninv_qhat * ipr[(size_t)t * N + 1]) % q);
     c.ninv_qhat_w1_shoup = shoup(c.ninv_qhat_w1, q);
   }
-  dt.qmod128_lo = (uint64_t)Q128;
-  dt.qmod128_hi = (uint64_t)(Q128 >> 64);
+  {
+    // decode's CRT (DeviceTables::crt_nc / crt_mw): |sum_t y_t Q/q_t - k Q| < L Q, plus a sign bit
+    uint32_t qbits = 0;
+    for (uint32_t t = 0; t < L; ++t) qbits += 64 - (uint32_t)__builtin_clzll(p.q[t]);
+    const uint32_t need = qbits + (32 - (uint32_t)__builtin_clz(L)) + 1;
+    const uint32_t nc = std::max<uint32_t>(5, (need + 29) / 30);
+    dt.crt_nc = (L <= 7 && nc <= 7) ? nc : 0;
+    const uint32_t NL = (need + 1 + 29) / 30, NW = (qbits + 63) / 64 + 1;
+    if (NL > (uint32_t)kCrtMwMaxLimbs) throw Error{SHELFI_ERR_ARG, "tower chain too wide for the exact CRT"};
+    std::vector<uint32_t> mw(4 + (size_t)(L + 2) * NL, 0);
+    mw[0] = NL;
+    mw[1] = NW;
+    const std::vector<uint64_t> Qm = mw30_prod(p.q, L, NL), nQ = mw30_neg(Qm, NL);
+    for (uint32_t t = 0; t < L; ++t) {
+      const std::vector<uint64_t> qh = mw30_qhat(p.q, L, t, NL);
+      for (uint32_t j = 0; j < NL; ++j) mw[4 + (size_t)t * NL + j] = (uint32_t)qh[j];
+    }
+    for (uint32_t j = 0; j < NL; ++j) {
+      mw[4 + (size_t)L * NL + j] = (uint32_t)nQ[j];
+      // (Q - 1) / 2 = Q >> 1 (Q odd)
+      mw[4 + (size_t)(L + 1) * NL + j] = (uint32_t)((Qm[j] >> 1) | (j + 1 < NL ? (Qm[j + 1] & 1) << 29 : 0));
+    }
+    dt.crt_mw = upload(mw.data(), mw.size());
+  }
   dt.tc = upload(tc.data(), L);
   dt.red_ok = true;
   for (uint32_t t = 0; t < L; ++t) dt.red_ok = dt.red_ok && tc[t].red_ok;
@@ -1641,12 +1690,14 @@ int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
   return SHELFI_OK;
 }
 
-// Towers the decode needs: the shortest prefix of q_0 .. q_{towers-1} whose product exceeds
-// 2^130.  The decode reads the centred CRT value X mod 2^128 as a signed integer (crt_value),
-// exact for |X| < 2^127; over a prefix modulus Q' > 2^130 the centred residue of X is X itself
-// and |X| / Q' < 2^-3 keeps k's estimate clear of its rounding boundary, so the towers past the
-// prefix change no output bit.  2^15 / L4 (60 + 3 x 52 bits): 3 of 4 towers.
-// SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe switch).
+// Towers the decode's fast path reads: the shortest prefix of q_0 .. q_{towers-1} whose product
+// exceeds 2^130.  crt_value decodes X exactly over that prefix Q' while |X| < 2^127: the centred
+// residue of X mod Q' is X itself, and |X| / Q' < 2^-3 keeps k's estimate clear of its rounding
+// boundary, so the towers past the prefix change no output bit.  A coefficient
+// outside that range sets the CRT range flag and the call is redone over every tower through
+// crt_exact_kernel (round 6), as PALISADE's BigInteger decode, up to (Q - 1) / 2.  2^15 / L4
+// (60 + 3 x 52 bits): 3 of 4 towers.  SHELFI_DEC_ALL_TOWERS=1 decodes with every tower (A/B probe
+// switch; on chains too wide for crt_value's columns that is crt_exact_kernel).
 static uint32_t decode_towers(const Params& p, uint32_t towers) {
   if (switches().dec_all_towers) return towers;
   uint32_t bits = 0;
@@ -1667,55 +1718,67 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     const CtLayout h = open_cts(ctx, blob, len);
     if (n > h.K * (uint64_t)p.batch)
       throw Error{SHELFI_ERR_ARG, "decrypt: data_dimensions exceeds the slots in the ciphertexts"};
-    Params pd = p;  // the decode's tower prefix (decode_towers): only those towers are uploaded
-    pd.L = decode_towers(p, p.L);
-    const DeviceTables& dtd = pd.L == p.L ? ctx->dt : level_tables(ctx, pd.L);
     if (!n) return;
     // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
     const uint64_t K = (n + p.batch - 1) / p.batch;
-    const size_t ct_bytes = 2ull * pd.L * p.N * 8;  // only the decode's towers travel
-    uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
-    kc = std::min<uint64_t>(kc, K);
-    const size_t cin = kc * ct_bytes, dout = kc * p.batch * 8;
-    // a packed blob's tower prefix lands packed and is unpacked on the device
-    const uint64_t ppre = 2 * packed_poly_bytes(p, pd.L);  // packed bytes of one ciphertext's prefix
-    const size_t pin = h.packed ? kc * ppre : 0;
-    uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout + pin));
-    uint8_t* cb[2] = {io, io + cin};
-    uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
-    uint8_t* pb[2] = {io + 2 * (cin + dout), io + 2 * (cin + dout) + pin};
-    const ArenaPack apd = arena_pack_prefix(p, pd.L);
-    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(pd, kc));
-    Pipe pp(ctx);
-    StageRun sr(stager(ctx));
     advise_huge(out, n * 8);
-    DecodeNoise dn = decode_noise_begin(ctx, K, pp.b);
-    std::vector<HostPiece> pcs;
-    const uint64_t nchunks = (K + kc - 1) / kc;
-    for (uint64_t ci = 0; ci < nchunks; ++ci) {
-      const int b = (int)(ci & 1);
-      const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
-      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
-      if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
-      h.pieces(k0, kn, p, pcs, pd.L);
-      sr.s.h2dv(h.packed ? pb[b] : cb[b], pcs.data(), pcs.size(), pp.a);
-      SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
-      SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
-      if (h.packed) launch_blob_unpack((const uint32_t*)pb[b], kn, pd.L, p.logN, apd, (uint64_t*)cb[b], pp.b);
-      if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
-      dn.g0 += (ci ? kc : 0);
-      launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
-                     scratch, pp.b, &dn);
-      dn.reset = 0;
-      SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
-      SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
-      sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
-      SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
-      sr.s.poll();
-    }
-    decode_noise_readback(ctx, dn, pp.b);
-    sr.finish();
-    pp.sync();
+    DecodeNoise dn = decode_noise_begin(ctx, K, ctx->stream2);
+    const uint64_t g0 = dn.g0;
+    // one pipelined pass over the call: the decode's tower prefix (decode_towers: only those towers
+    // are uploaded) with the fast CRT, or (exact) every tower through crt_exact_kernel
+    const auto run = [&](bool exact) {
+      Params pd = p;
+      pd.L = exact ? p.L : decode_towers(p, p.L);
+      const DeviceTables& dtd = pd.L == p.L ? ctx->dt : level_tables(ctx, pd.L);
+      const size_t ct_bytes = 2ull * pd.L * p.N * 8;  // only the decode's towers travel
+      uint64_t kc = std::max<uint64_t>(1, (64ull << 20) / ct_bytes);
+      kc = std::min<uint64_t>(kc, K);
+      const size_t cin = kc * ct_bytes, dout = kc * p.batch * 8;
+      // a packed blob's tower prefix lands packed and is unpacked on the device
+      const uint64_t ppre = 2 * packed_poly_bytes(p, pd.L);  // packed bytes of one ciphertext's prefix
+      const size_t pin = h.packed ? kc * ppre : 0;
+      uint8_t* io = (uint8_t*)ensure(ctx->io, ctx->io_bytes, 2 * (cin + dout + pin));
+      uint8_t* cb[2] = {io, io + cin};
+      uint8_t* ob[2] = {io + 2 * cin, io + 2 * cin + dout};
+      uint8_t* pb[2] = {io + 2 * (cin + dout), io + 2 * (cin + dout) + pin};
+      const ArenaPack apd = arena_pack_prefix(p, pd.L);
+      void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(pd, kc));
+      Pipe pp(ctx);
+      StageRun sr(stager(ctx));
+      if (!exact) SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, pp.b));
+      dn.g0 = g0;
+      dn.reset = 1;
+      std::vector<HostPiece> pcs;
+      const uint64_t nchunks = (K + kc - 1) / kc;
+      for (uint64_t ci = 0; ci < nchunks; ++ci) {
+        const int b = (int)(ci & 1);
+        const uint64_t k0 = ci * kc, kn = std::min<uint64_t>(kc, K - k0);
+        const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kn * p.batch);
+        if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.a, pp.computed[b], 0));
+        h.pieces(k0, kn, p, pcs, pd.L);
+        sr.s.h2dv(h.packed ? pb[b] : cb[b], pcs.data(), pcs.size(), pp.a);
+        SHELFI_HIP(hipEventRecord(pp.in_ready[b], pp.a));
+        SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.in_ready[b], 0));
+        if (h.packed) launch_blob_unpack((const uint32_t*)pb[b], kn, pd.L, p.logN, apd, (uint64_t*)cb[b], pp.b);
+        if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
+        dn.g0 += (ci ? kc : 0);
+        launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
+                       scratch, pp.b, &dn, false, 0, ctx->dev_flag + 7, exact);
+        dn.reset = 0;
+        SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
+        SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
+        sr.s.d2h(out + o0, ob[b], on * 8, pp.c);
+        SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
+        sr.s.poll();
+      }
+      decode_noise_readback(ctx, dn, pp.b);
+      if (!exact)  // pinned, before the one synchronisation
+        SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, pp.b));
+      sr.finish();
+      pp.sync();
+    };
+    run(false);
+    if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
     decode_noise_end(ctx, dn);
   });
 }
@@ -2236,28 +2299,40 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
     require_keys(ctx);
     DeviceGuard g(ctx->device);
     if (towers < 1 || towers > ctx->p.L) throw Error{SHELFI_ERR_ARG, "tower count out of range for this context"};
-    Params p = ctx->p;
-    p.L = decode_towers(ctx->p, towers);  // Q' = q_0 .. q_{p.L-1}; the secret key's first towers
-    const DeviceTables& dt = p.L == ctx->p.L ? ctx->dt : level_tables(ctx, p.L);
-    if (n > (uint64_t)K * p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
+    if (n > (uint64_t)K * ctx->p.batch) throw Error{SHELFI_ERR_ARG, "n exceeds the slots in K ciphertexts"};
     hipStream_t s = (hipStream_t)stream;  // 0 = legacy default stream
-    const uint64_t Kn = (n + p.batch - 1) / p.batch;
+    const uint64_t Kn = (n + ctx->p.batch - 1) / ctx->p.batch;
     if (!Kn) return;
-    const uint64_t kc_max = dev_chunk(Kn, decrypt_scratch_bytes(p, 1));
-    void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
-    const size_t ct_words = 2ull * towers * p.N;
+    const size_t ct_words = 2ull * towers * ctx->p.N;
     DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
     const uint64_t g0 = dn.g0;
-    for (uint64_t k0 = 0; k0 < Kn; k0 += kc_max) {
-      const uint64_t kc = std::min(kc_max, Kn - k0);
-      const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
-      dn.g0 = g0 + k0;
-      launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
-                     sum_in, towers);
-      dn.reset = 0;  // the flags are reset by the first chunk's flooding only
-    }
-    decode_noise_readback(ctx, dn, s);
+    // one pass over the call: the decode's tower prefix with the fast CRT, or (exact) every tower
+    // through crt_exact_kernel
+    const auto run = [&](bool exact) {
+      Params p = ctx->p;
+      p.L = exact ? towers : decode_towers(ctx->p, towers);  // Q' = q_0 .. q_{p.L-1}; the secret key's first towers
+      const DeviceTables& dt = p.L == ctx->p.L ? ctx->dt : level_tables(ctx, p.L);
+      const uint64_t kc_max = dev_chunk(Kn, decrypt_scratch_bytes(p, 1));
+      void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(p, kc_max));
+      dn.reset = 1;
+      for (uint64_t k0 = 0; k0 < Kn; k0 += kc_max) {
+        const uint64_t kc = std::min(kc_max, Kn - k0);
+        const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
+        dn.g0 = g0 + k0;
+        launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
+                       sum_in, towers, ctx->dev_flag + 7, exact);
+        dn.reset = 0;  // the flags are reset by the first chunk's flooding only
+      }
+      decode_noise_readback(ctx, dn, s);
+    };
+    SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, s));
+    run(false);
+    SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, s));  // pinned
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
+    if (ctx->host_flag[7]) {  // a value outside the fast CRT's range: the whole call again, exactly
+      run(true);
+      SHELFI_HIP(hipStreamSynchronize(s));
+    }
     decode_noise_end(ctx, dn);
   });
 }

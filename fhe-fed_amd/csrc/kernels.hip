@@ -1979,79 +1979,59 @@ void launch_encrypt_approx(const Params& p, const DeviceTables& dt, const Device
   SHELFI_HIP(hipStreamSynchronize(s));  // the host tables above are uploaded from pageable memory
 }
 
-// One coefficient of the exact centered CRT: y(t) in [0, q_t) are b_t (Q/q_t)^-1 mod q_t
-// for the L towers; X = sum_t y_t (Q/q_t) - k Q with k = round(sum_t y_t / q_t), read as a
-// signed 128-bit integer, then (double)X * (1/scale) (PALISADE Decode: ConvertToDouble *
-// scalingFactorPre * 2^-p).  For L <= 7 the 128-bit sum runs in 30-bit limb columns
-// (y_t = a + b 2^30; every column is a sum of <= 2L products below 2^60 plus k times a
-// 30-bit limb, below 2^64 without carries: one v_mad_u64_u32 per product), then one carry
-// pass; X is exact either way, so the two paths give the same bits.
+// One coefficient of the centred CRT over the decode's towers: y(t) in [0, q_t) are
+// b_t (Q/q_t)^-1 mod q_t for the L <= 7 towers; X = sum_t y_t (Q/q_t) - k Q with k = round(sum_t
+// y_t / q_t), then (double)X * (1/scale) (PALISADE Decode: ConvertToDouble * scalingFactorPre *
+// 2^-p), X read as a signed 128-bit integer: (double)|X|_hi 2^64 + (double)|X|_lo with its sign
+// (the oracle's or_mw_to_double restricted to two words).
 //
-// k (round 3): sum_t y_t / q_t = k + X / Q exactly (Q here is the decoded prefix's modulus Q',
-// decode_towers: the shortest tower prefix above 2^130, or every tower when the chain is
-// shorter).  Every X this decode represents has |X| < 2^127 (the signed 128-bit read below), so
-// over a prefix above 2^130 X / Q' is within 2^-3 of 0: k = round(sum) has 3/8 of headroom on
-// either side of its rounding boundary.  The binary32 estimate spends at most ~L * 2^-21 of it:
-// terms (y_t >> s_t) * (2^s_t / q_t) with y_t >> s_t < 2^32 (TowerConst::crt_sh) are each within
-// 2^-31 + 2^-23 of y_t / q_t, and L <= 7 float additions of values below 8 round by <= 2^-21
-// each; round half up.  Correctness therefore needs |X| < 2^127, which every decryptable
-// ciphertext meets while |x| * scale^depth < 2^127 (|X| ~ |m| * scale: fresh ciphertexts of |x| < 2^75 and
-// depth-2 aggregates of |sum w x| < 2^23 at scale ~ 2^52; PALISADE's bigint decode reaches Q / 2), not a runtime check;
-// tests/test_gpu_decode_towers.py::test_prefix_decode_near_the_2_127_limit decodes |X| ~ 2^125
-// over a 2^132 prefix.  Over a chain below 2^130 the decode is the plain centred CRT mod Q, and a
-// valid decryption has |X| << Q / 2.  The oracle's CRT is exact (multi-word centring); the two
-// agree wherever the decode is defined.  For L <= 7, k <= L fits a 32-bit limb multiplier.
-template <class YF>
+// The sum runs in NC 30-bit limb columns (y_t = a + b 2^30; every column is a sum of <= 2L
+// products below 2^60 plus k times a 30-bit limb, below 2^64 without carries: one v_mad_u64_u32
+// per product), then one carry pass.  NC (DeviceTables::crt_nc) is chosen so that the columns
+// hold X' = sum_t y_t (Q/q_t) - k Q exactly in two's complement (|X'| < L Q): whatever k's binary32
+// estimate gave, X' is a representative of X mod Q, and it is the centred one exactly when it lies
+// in (-2^127, 2^127) -- the value range of this path (round 6).  Bits 127 .. 30 NC - 1 of X' all
+// equal is therefore the exact test of "this output is right": otherwise *wide is set and the
+// caller redoes the call through crt_exact_kernel over every tower (any |X| <= (Q - 1) / 2, as
+// PALISADE's BigInteger decode).  No X in the old range sets it: over the prefix decode_towers keeps
+// (Q > 2^130), |X| < 2^127 puts sum_t y_t / q_t within 2^-3 of k, and the binary32 estimate errs by
+// at most ~L 2^-21 (terms (y_t >> s_t) * (2^s_t / q_t), y_t >> s_t < 2^32, TowerConst::crt_sh), so
+// k is exact and the output bits are the round-5 ones.
+template <int NC, class YF>
 __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst* __restrict__ tcs,
-                                            uint64_t Qlo, uint64_t Qhi, double inv_scale) {
-  double frac = 0.0;
-  uint64_t xlo = 0, xhi = 0;
-  if (L <= 7) {
-    constexpr uint32_t M30 = (1u << 30) - 1;
-    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-    float f = 0.f;
+                                            double inv_scale, bool& wide) {
+  static_assert(NC >= 5 && NC <= 7, "crt columns");
+  constexpr uint32_t M30 = (1u << 30) - 1;
+  uint64_t sc[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) sc[j] = 0;
+  float f = 0.f;
 #pragma unroll 1
-    for (uint32_t t = 0; t < L; ++t) {
-      const TowerConst& c = tcs[t];
-      const uint64_t y = yf(t);
-      const uint32_t ytop = __builtin_amdgcn_alignbit((uint32_t)(y >> 32), (uint32_t)y, c.crt_sh);
-      f = __fadd_rn(f, __fmul_rn((float)ytop, c.inv_q32));
-      const uint32_t a = (uint32_t)y & M30, b = (uint32_t)(y >> 30);
-      s0 += (uint64_t)a * c.crt30[0];
-      s1 += (uint64_t)a * c.crt30[1] + (uint64_t)b * c.crt30[0];
-      s2 += (uint64_t)a * c.crt30[2] + (uint64_t)b * c.crt30[1];
-      s3 += (uint64_t)a * c.crt30[3] + (uint64_t)b * c.crt30[2];
-      s4 += (uint64_t)a * c.crt30[4] + (uint64_t)b * c.crt30[3];
-    }
-    const uint32_t kk = (uint32_t)__fadd_rn(f, 0.5f);  // <= L
-    const uint32_t* nq = tcs[0].nq30;
-    s0 += (uint64_t)kk * nq[0];
-    s1 += (uint64_t)kk * nq[1] + (s0 >> 30);
-    s2 += (uint64_t)kk * nq[2] + (s1 >> 30);
-    s3 += (uint64_t)kk * nq[3] + (s2 >> 30);
-    s4 += (uint64_t)kk * nq[4] + (s3 >> 30);
-    xlo = (s0 & M30) | ((s1 & M30) << 30) | (s2 << 60);
-    xhi = ((s2 & M30) >> 4) | ((s3 & M30) << 26) | (s4 << 56);
-  } else {
-#pragma unroll 1
-    for (uint32_t t = 0; t < L; ++t) {
-      const TowerConst& c = tcs[t];
-      const uint64_t y = yf(t);
-      frac += (double)y * c.inv_q;
-      const uint64_t plo = y * c.qhat_lo;
-      const uint64_t phi = __umul64hi(y, c.qhat_lo) + y * c.qhat_hi;
-      xlo += plo;
-      xhi += phi + (xlo < plo ? 1 : 0);
-    }
-    const uint64_t kk = (uint64_t)(frac + 0.5);
-    const uint64_t slo = kk * Qlo;
-    const uint64_t shi = __umul64hi(kk, Qlo) + kk * Qhi;
-    const uint64_t borrow = xlo < slo ? 1 : 0;
-    xlo -= slo;
-    xhi = xhi - shi - borrow;
+  for (uint32_t t = 0; t < L; ++t) {
+    const TowerConst& c = tcs[t];
+    const uint64_t y = yf(t);
+    const uint32_t ytop = __builtin_amdgcn_alignbit((uint32_t)(y >> 32), (uint32_t)y, c.crt_sh);
+    f = __fadd_rn(f, __fmul_rn((float)ytop, c.inv_q32));
+    const uint32_t a = (uint32_t)y & M30, b = (uint32_t)(y >> 30);
+    sc[0] += (uint64_t)a * c.crt30[0];
+#pragma unroll
+    for (int j = 1; j < NC; ++j) sc[j] += (uint64_t)a * c.crt30[j] + (uint64_t)b * c.crt30[j - 1];
   }
-  // sign-magnitude -> double (the oracle's or_i128_to_double)
+  const uint32_t kk = (uint32_t)__fadd_rn(f, 0.5f);  // <= L
+  const uint32_t* nq = tcs[0].nq30;
+  sc[0] += (uint64_t)kk * nq[0];
+#pragma unroll
+  for (int j = 1; j < NC; ++j) sc[j] += (uint64_t)kk * nq[j] + (sc[j - 1] >> 30);
+  uint64_t xlo = (sc[0] & M30) | ((sc[1] & M30) << 30) | (sc[2] << 60);
+  uint64_t xhi = ((sc[2] & M30) >> 4) | ((sc[3] & M30) << 26) | (sc[4] << 56);
+  // bits 127 .. 30 NC - 1 must be X's sign
   const bool neg = (int64_t)xhi < 0;
+  const uint32_t ext = neg ? M30 : 0u;
+  bool bad = (((uint32_t)sc[4] & M30) >> 7) != (ext >> 7);
+#pragma unroll
+  for (int j = 5; j < NC; ++j) bad |= ((uint32_t)sc[j] & M30) != ext;
+  wide |= bad;
+  // sign-magnitude -> double (the oracle's or_i128_to_double)
   if (neg) {
     xlo = ~xlo + 1;
     xhi = ~xhi + (xlo == 0 ? 1 : 0);
@@ -2061,19 +2041,124 @@ __device__ __forceinline__ double crt_value(YF yf, uint32_t L, const TowerConst*
   return __dmul_rn(v, inv_scale);
 }
 
+// Bits [pos, pos + 64) of a little-endian 30-bit-limb integer of NL limbs.
+__device__ __forceinline__ uint64_t mw30_bits64(const uint64_t* a, uint32_t NL, uint32_t pos) {
+  uint64_t r = 0;
+#pragma unroll 1
+  for (uint32_t l = pos / 30; l < NL && 30 * l < pos + 64; ++l) {
+    const int sh = (int)(30 * l) - (int)pos;
+    r |= sh >= 0 ? (a[l] << sh) : (a[l] >> -sh);
+  }
+  return r;
+}
+
+// a += m * b (mod 2^(30 NL)), a normalised to 30-bit limbs
+__device__ __forceinline__ void mw30_addmul(uint64_t* a, const uint32_t* b, uint64_t m, uint32_t NL) {
+  constexpr uint64_t M30 = (1u << 30) - 1;
+  uint64_t carry = 0;
+#pragma unroll 1
+  for (uint32_t j = 0; j < NL; ++j) {
+    const uint64_t v = a[j] + m * b[j] + carry;
+    a[j] = v & M30;
+    carry = v >> 30;
+  }
+}
+
+// compare two NL-limb magnitudes: -1, 0, 1
+__device__ __forceinline__ int mw30_cmp(const uint64_t* a, const uint32_t* b, uint32_t NL) {
+#pragma unroll 1
+  for (int j = (int)NL - 1; j >= 0; --j)
+    if (a[j] != b[j]) return a[j] < b[j] ? -1 : 1;
+  return 0;
+}
+
+__device__ __forceinline__ void mw30_negate(uint64_t* a, uint32_t NL) {
+  constexpr uint64_t M30 = (1u << 30) - 1;
+  uint64_t carry = 1;
+#pragma unroll 1
+  for (uint32_t j = 0; j < NL; ++j) {
+    const uint64_t v = ((~a[j]) & M30) + carry;
+    a[j] = v & M30;
+    carry = v >> 30;
+  }
+}
+
+// The exact centred CRT over any tower set (round 6; PALISADE's CRTInterpolate to a BigInteger and
+// centring mod Q before Decode, ckks.cpp:189): X in [-(Q - 1) / 2, (Q - 1) / 2]
+// from V = sum_t y_t (Q/q_t) (< L Q) in NL 30-bit limbs (DeviceTables::crt_mw), k = round(sum_t
+// y_t / q_t) in binary64, X' = V - k Q in two's complement, then at most two corrections by Q
+// against (Q - 1) / 2 (exact comparisons), so k's estimate only has to be within 1.  |X| becomes
+// NW 64-bit words w and (double) by Horner from the top, d = d 2^64 + (double)w_i, the oracle's
+// or_mw_to_double; leading zero words leave d unchanged, so below 2^127 this is crt_value's
+// two-word conversion bit for bit.  A slow path: limbs live in scratch (private memory).
+template <class YF>
+__device__ __forceinline__ double crt_exact_value(YF yf, uint32_t L, const TowerConst* __restrict__ tcs,
+                                                  const uint32_t* __restrict__ mw, double inv_scale) {
+  constexpr uint64_t M30 = (1u << 30) - 1;
+  const uint32_t NL = mw[0], NW = mw[1];
+  const uint32_t* qh = mw + 4;
+  const uint32_t* nQ = qh + (size_t)L * NL;
+  const uint32_t* half = nQ + NL;
+  uint64_t acc[kCrtMwMaxLimbs];
+#pragma unroll 1
+  for (uint32_t j = 0; j < NL; ++j) acc[j] = 0;
+  double f = 0.0;
+#pragma unroll 1
+  for (uint32_t t = 0; t < L; ++t) {
+    const uint64_t y = yf(t);
+    f = __dadd_rn(f, __dmul_rn((double)y, tcs[t].inv_q));
+    const uint64_t a = y & M30, b = y >> 30;
+    const uint32_t* h = qh + (size_t)t * NL;
+    uint64_t carry = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < NL; ++j) {
+      const uint64_t v = acc[j] + a * h[j] + (j ? b * h[j - 1] : 0) + carry;
+      acc[j] = v & M30;
+      carry = v >> 30;
+    }
+  }
+  mw30_addmul(acc, nQ, (uint64_t)__dadd_rn(f, 0.5), NL);  // X' = V - k Q
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const bool neg = (acc[NL - 1] >> 29) & 1;
+    if (!neg) {
+      if (mw30_cmp(acc, half, NL) <= 0) break;
+      mw30_addmul(acc, nQ, 1, NL);  // X' - Q
+    } else {
+      mw30_negate(acc, NL);
+      const bool over = mw30_cmp(acc, half, NL) > 0;
+      mw30_negate(acc, NL);
+      if (!over) break;
+      // X' + Q = X' - (2^(30 NL) - Q) mod 2^(30 NL)
+      mw30_negate(acc, NL);
+      mw30_addmul(acc, nQ, 1, NL);
+      mw30_negate(acc, NL);
+    }
+  }
+  const bool neg = (acc[NL - 1] >> 29) & 1;
+  if (neg) mw30_negate(acc, NL);
+  double d = (double)mw30_bits64(acc, NL, 64 * (NW - 1));
+#pragma unroll 1
+  for (int w = (int)NW - 2; w >= 0; --w)
+    d = __dadd_rn(__dmul_rn(d, 18446744073709551616.0), (double)mw30_bits64(acc, NL, 64 * (uint32_t)w));
+  if (neg) d = -d;
+  return __dmul_rn(d, inv_scale);
+}
 
 // -------------------------------------------------------------- decrypt ----
-// Exact centered CRT: y_t = b_t (Q/q_t)^-1 mod q_t; X = sum y_t (Q/q_t) - k Q with
-// k = round(sum y_t / q_t) (exact while |X| << Q/2), evaluated mod 2^128 and read
-// as a signed 128-bit integer; then (double)X * (1/scale) (PALISADE Decode:
-// ConvertToDouble * scalingFactorPre * 2^-p).  Written at bitrev(i) for FFTSpecial.
+// Centred CRT: y_t = b_t (Q/q_t)^-1 mod q_t; X = sum y_t (Q/q_t) - k Q with k = round(sum y_t / q_t)
+// (crt_value: NC exact columns, *wide set when X is outside the 128-bit range); then (double)X *
+// (1/scale) (PALISADE Decode: ConvertToDouble * scalingFactorPre * 2^-p).  Written at bitrev(i) for
+// FFTSpecial.  EXACT: crt_exact_kernel's arithmetic (crt_exact_value, every |X| <= (Q - 1) / 2).
+template <int NC, bool EXACT = false>
 __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restrict__ dbuf,
                                                          uint64_t K, uint32_t logN, uint32_t logS,
                                                          uint32_t L,
                                                          const TowerConst* __restrict__ tcs,
-                                                         uint64_t Qlo, uint64_t Qhi,
+                                                         const uint32_t* __restrict__ mw,
                                                          double inv_scale,
-                                                         double2* __restrict__ fbuf) {
+                                                         double2* __restrict__ fbuf,
+                                                         uint32_t* __restrict__ wide_flag) {
   const uint32_t N = 1u << logN, S = 1u << logS;
   // S >= 256: a block owns the 256 slots i = hi.2^(logS-4) | mid.16 | lo (hi, lo < 16) of one
   // middle value, so the tower reads (16 consecutive i) and, after a transpose through LDS,
@@ -2094,16 +2179,20 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
   const uint32_t gapLog = logN - 1 - logS;
   const uint64_t* __restrict__ d = dbuf + k * ((uint64_t)L << logN);
   double res[2];
+  bool wide = false;
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
     const uint32_t j = (part ? (N >> 1) : 0) + (i << gapLog);
-    res[part] = crt_value(
-        [&](uint32_t t) {
-          const TowerConst& c = tcs[t];
-          return shoup_mul(d[((uint64_t)t << logN) + j], c.qhat_inv, c.qhat_inv_shoup, c.q);
-        },
-        L, tcs, Qlo, Qhi, inv_scale);
+    const auto yf = [&](uint32_t t) {
+      const TowerConst& c = tcs[t];
+      return shoup_mul(d[((uint64_t)t << logN) + j], c.qhat_inv, c.qhat_inv_shoup, c.q);
+    };
+    if constexpr (EXACT)
+      res[part] = crt_exact_value(yf, L, tcs, mw, inv_scale);
+    else
+      res[part] = crt_value<NC>(yf, L, tcs, inv_scale, wide);
   }
+  if (wide) atomicOr(wide_flag, 1u);
   if (!tiled) {
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
     return;
@@ -2130,14 +2219,14 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
 // at 2^15 / L4, 5 workgroups per CU; the round-4 rows padded to 68 u64 ran the same, 0.960 vs 0.959
 // us per decrypted ciphertext, profiles/r05d).
 constexpr size_t kCrtFuseLds = 48 << 10;
-template <int LOGR>
+template <int LOGR, int NC>
 __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restrict__ dbuf, uint32_t L,
                                                         uint32_t logN, uint32_t logS,
                                                         const uint64_t* __restrict__ tw,
                                                         const uint64_t* __restrict__ twp,
-                                                        const TowerConst* __restrict__ tcs, uint64_t Qlo,
-                                                        uint64_t Qhi, double inv_scale,
-                                                        double2* __restrict__ fbuf) {
+                                                        const TowerConst* __restrict__ tcs, double inv_scale,
+                                                        double2* __restrict__ fbuf,
+                                                        uint32_t* __restrict__ wide_flag) {
   constexpr int R = 1 << LOGR, CW = 64, CWP = 64;
   extern __shared__ uint64_t ys_flat[];  // [L][R][CWP]
   uint64_t(*ys)[R][CWP] = reinterpret_cast<uint64_t(*)[R][CWP]>(ys_flat);
@@ -2186,6 +2275,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
   }
   __syncthreads();
   const uint32_t gapLog = logN - 1 - logS, gap = 1u << gapLog;
+  bool wide = false;
   // pair p -> half-row r (< R/2) fastest, so 8 consecutive threads store 8 consecutive
   // bit-reversed slots (one 128-byte segment)
 #pragma unroll 1
@@ -2197,11 +2287,12 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
       const uint32_t rr = r + part * (R / 2);
-      res[part] = crt_value([&](uint32_t t) { return ys[t][rr][ucol(rr, u)]; }, L, tcs, Qlo, Qhi, inv_scale);
+      res[part] = crt_value<NC>([&](uint32_t t) { return ys[t][rr][ucol(rr, u)]; }, L, tcs, inv_scale, wide);
     }
     const uint32_t i = (col + BLK * r) >> gapLog;
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
   }
+  if (wide) atomicOr(wide_flag, 1u);
 }
 
 // ------------------------------------------------- decode noise flooding ----
@@ -2755,10 +2846,14 @@ size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
 
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
-                    void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in, uint32_t ct_L) {
+                    void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in, uint32_t ct_L,
+                    uint32_t* crt_flag, bool exact) {
   if (!K) return;
   if (!ct_L) ct_L = p.L;
   if (ct_L < p.L) throw Error{SHELFI_ERR_ARG, "decrypt: fewer ciphertext towers than decoded towers"};
+  exact = exact || dt.crt_nc == 0;  // towers too wide for crt_value's columns: always exact
+  if (exact && !dt.crt_mw) throw Error{SHELFI_ERR_STATE, "decrypt: no exact CRT table for these towers"};
+  if (!exact && !crt_flag) throw Error{SHELFI_ERR_STATE, "decrypt: the fast CRT needs a range flag"};
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
@@ -2767,7 +2862,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   const uint32_t blkLog = ntt_block_log(p.logN);
   const int logR = (int)(p.logN - blkLog);
   const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
-  const bool fuse = logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
+  const bool fuse = !exact && logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
                     ((p.N >> logR) % 64) == 0;
   {
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
@@ -2804,8 +2899,23 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                          logR == 0 ? 1 : 0, ct, dk.sk, dk.sk_sh, sum_in ? 1 : 0, ct_L);
     if (logR > 0 && fuse) {
       const uint64_t nbf = K * ((p.N >> logR) / 64);
-NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, logS,
-                   dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale, fbuf);
+#define CRT_FUSED(LR, NCC)                                                                                    \
+  hipLaunchKernelGGL((ntt_inv_cols_crt<LR, NCC>), dim3((uint32_t)nbf), dim3(256), fuse_lds, s, dbuf, p.L, p.logN, \
+                     logS, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc, 1.0 / scale, fbuf, crt_flag)
+#define CRT_FUSED_NC(LR)                                  \
+  if (dt.crt_nc == 5) CRT_FUSED(LR, 5);                   \
+  else if (dt.crt_nc == 6) CRT_FUSED(LR, 6);              \
+  else CRT_FUSED(LR, 7);
+      switch (logR) {
+        case 1: CRT_FUSED_NC(1) break;
+        case 2: CRT_FUSED_NC(2) break;
+        case 3: CRT_FUSED_NC(3) break;
+        case 4: CRT_FUSED_NC(4) break;
+        case 5: CRT_FUSED_NC(5) break;
+        default: throw Error{SHELFI_ERR_ARG, "unsupported ring dimension"};
+      }
+#undef CRT_FUSED_NC
+#undef CRT_FUSED
     } else if (logR > 0) {
       NTT_DISPATCH(logR, ntt_inv_cols, dim3((uint32_t)nbCols), dim3(256), 0, s, dbuf, p.L, p.logN,
                    dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc);
@@ -2813,10 +2923,21 @@ NTT_DISPATCH(logR, ntt_inv_cols_crt, dim3((uint32_t)nbf), dim3(256), fuse_lds, s
     SHELFI_HIP(hipGetLastError());
   }
   const uint64_t slots = K * (uint64_t)p.batch;
-  if (!fuse)
-    hipLaunchKernelGGL(crt_decode_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, s,
-                       dbuf, K, p.logN, logS, p.L, dt.tc, dt.qmod128_lo, dt.qmod128_hi, 1.0 / scale,
-                       fbuf);
+  if (!fuse) {
+    const dim3 cg((uint32_t)((slots + 255) / 256));
+    if (exact)
+      hipLaunchKernelGGL((crt_decode_kernel<5, true>), cg, dim3(256), 0, s, dbuf, K, p.logN, logS, p.L, dt.tc,
+                         dt.crt_mw, 1.0 / scale, fbuf, crt_flag);
+    else if (dt.crt_nc == 5)
+      hipLaunchKernelGGL((crt_decode_kernel<5>), cg, dim3(256), 0, s, dbuf, K, p.logN, logS, p.L, dt.tc,
+                         dt.crt_mw, 1.0 / scale, fbuf, crt_flag);
+    else if (dt.crt_nc == 6)
+      hipLaunchKernelGGL((crt_decode_kernel<6>), cg, dim3(256), 0, s, dbuf, K, p.logN, logS, p.L, dt.tc,
+                         dt.crt_mw, 1.0 / scale, fbuf, crt_flag);
+    else
+      hipLaunchKernelGGL((crt_decode_kernel<7>), cg, dim3(256), 0, s, dbuf, K, p.logN, logS, p.L, dt.tc,
+                         dt.crt_mw, 1.0 / scale, fbuf, crt_flag);
+  }
   SHELFI_HIP(hipGetLastError());
   const uint32_t fblkLog = fft_block_log(logS);
   const int flogR = (int)(logS - fblkLog);

@@ -120,8 +120,7 @@ struct TowerConst {
   uint64_t r64, r64_shoup;  // 2^64 mod q
   uint64_t ninv, ninv_shoup;  // N^-1 mod q
   uint64_t qhat_inv, qhat_inv_shoup;  // (Q/q_t)^-1 mod q_t
-  uint64_t qhat_lo, qhat_hi;  // (Q/q_t) mod 2^128
-  double inv_q;               // 1.0 / q (CRT k estimate)
+  double inv_q;               // 1.0 / q (crt_exact_value's k estimate)
   uint64_t nq, n4q, n8q;      // 2^64 - q, - 4q, - 8q (borrow-free conditional subtractions)
   // any u64 x -> [0, 2q): k = (x_hi * red_r) >> (32 + red_sh), x - k q (red_any; needs
   // q >= 2^40, red_ok): red_r = floor(2^(32 + E) / q) < 2^32, E = bitlength(q) - 1
@@ -134,9 +133,9 @@ struct TowerConst {
   uint64_t bq62;  // floor(2^62 / q) q: v + bq62 in [0, 2^63) for |v| <= 2^61 + 2^7 (encrypt's m + e0)
   uint64_t ninv_qhat, ninv_qhat_shoup;  // N^-1 (Q/q_t)^-1 mod q_t (INTT scale fused with the CRT)
   uint64_t ninv_qhat_w1, ninv_qhat_w1_shoup;  // ninv_qhat * psi^-bitrev(1): the last INTT stage's twiddle, scaled
-  // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^128 and (2^128 - Q) mod 2^128
-  // (the same in every tower), limbs 0..3 of 30 bits and limb 4 of 8 bits
-  uint32_t crt30[5], nq30[5], pad30[2];
+  // the CRT in 30-bit limbs (crt_value, L <= 7): (Q/q_t) mod 2^210 and (2^210 - Q) mod 2^210
+  // (the same in every tower), limbs 0..6 of 30 bits; a launch uses the first DeviceTables::crt_nc
+  uint32_t crt30[7], nq30[7];
 };
 
 constexpr int kEncVTab = 4 * 81, kEncETab = 128, kEncTab = kEncVTab + kEncETab;
@@ -166,8 +165,15 @@ struct DeviceTables {
   // canonical; the row's value is the sum over the 4 groups.  nullptr for other shapes.
   uint64_t* enc_vtab = nullptr;
   int cdt_len = 0;
-  uint64_t qmod128_lo = 0, qmod128_hi = 0;  // Q mod 2^128
+  // Decode's CRT (round 6).  crt_nc: 30-bit columns crt_value needs to hold sum_t y_t (Q/q_t) - k Q
+  // exactly (ceil((bits(Q) + bits(L) + 1) / 30), at least 5), or 0 when that exceeds 7 or L > 7: such
+  // tower sets always decode through crt_exact_kernel.  crt_mw: that kernel's table (uint32 words):
+  // [0] NL limbs, [1] NW 64-bit words of |X|, [2..3] 0, then (Q/q_t) [L][NL], 2^(30 NL) - Q [NL],
+  // (Q - 1) / 2 [NL], all in 30-bit limbs.
+  uint32_t crt_nc = 0;
+  uint32_t* crt_mw = nullptr;
 };
+constexpr int kCrtMwMaxLimbs = 36;  // crt_exact_kernel: 16 towers below 2^60, times L, plus sign
 
 // NTT / CRT tables of an arbitrary tower list p.q[0..p.L) (api.cpp); free_ntt_tables frees
 // only what build_ntt_tables allocates (not the FFT / Gaussian tables of a context).
@@ -227,7 +233,8 @@ struct shelfi_ctx {
   uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
                                  // [2] max decode logError (noise flooding), [3] bytes-API
                                  // upload residue >= q, [4] arena upload residue >= q, [5] the
-                                 // packed wire's pack check, [6] shelfi_dev_check_residues
+                                 // packed wire's pack check, [6] shelfi_dev_check_residues,
+                                 // [7] decode CRT value outside the fast path's range (redo exact)
   // arena slots whose last upload was refused (shelfi_dev_arena_put*): an aggregation
   // over an arena range holding one fails instead of summing the refused residues
   // (an entry names the arena by its base, its shelfi_arena_words(C, K) span and C, so a later
@@ -352,7 +359,11 @@ struct DecodeNoise {
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
                     void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr, bool sum_in = false,
-                    uint32_t ct_L = 0);  // ct_L: towers of the ciphertexts (0 = p.L; >= p.L)
+                    uint32_t ct_L = 0,  // ct_L: towers of the ciphertexts (0 = p.L; >= p.L)
+                    uint32_t* crt_flag = nullptr, bool exact = false);
+// crt_flag: the fast CRT (crt_value) sets *crt_flag = 1 when a coefficient's centred value is not
+// in (-2^127, 2^127) over these towers -- the caller redoes the call with every tower and exact =
+// true (crt_exact_kernel, any |X| <= (Q - 1) / 2).  A fast-path launch needs crt_flag.
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
 void launch_keygen(const Params& p, const DeviceTables& dt, const uint32_t key[8], uint64_t* sk,
                    uint64_t* pk, void* scratch, hipStream_t s);

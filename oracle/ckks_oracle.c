@@ -592,33 +592,33 @@ void or_wavg_fast(const uint64_t* const* cts, const float* w, size_t C, size_t K
 /* what the symmetrisation computes before the noise.                         */
 /* ------------------------------------------------------------------------ */
 
-/* multiword helpers for the exact CRT (little-endian u64 limbs) */
-#define MW 10
-static void mw_mul_small(const uint64_t* a, uint64_t b, uint64_t* r) {
+/* multiword helpers for the exact CRT (little-endian u64 limbs; n of the MW words used) */
+#define MW 17 /* 16 towers below 2^60 times L, plus the sign */
+static void mw_mul_small(const uint64_t* a, uint64_t b, uint64_t* r, int n) {
   u128 carry = 0;
-  for (int i = 0; i < MW; ++i) {
+  for (int i = 0; i < n; ++i) {
     u128 p = (u128)a[i] * b + carry;
     r[i] = (uint64_t)p;
     carry = p >> 64;
   }
 }
-static void mw_add(uint64_t* a, const uint64_t* b) {
+static void mw_add(uint64_t* a, const uint64_t* b, int n) {
   u128 carry = 0;
-  for (int i = 0; i < MW; ++i) {
+  for (int i = 0; i < n; ++i) {
     u128 s = (u128)a[i] + b[i] + carry;
     a[i] = (uint64_t)s;
     carry = s >> 64;
   }
 }
-static int mw_cmp(const uint64_t* a, const uint64_t* b) {
-  for (int i = MW - 1; i >= 0; --i) {
+static int mw_cmp(const uint64_t* a, const uint64_t* b, int n) {
+  for (int i = n - 1; i >= 0; --i) {
     if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
   }
   return 0;
 }
-static void mw_sub(uint64_t* a, const uint64_t* b) {
+static void mw_sub(uint64_t* a, const uint64_t* b, int n) {
   uint64_t borrow = 0;
-  for (int i = 0; i < MW; ++i) {
+  for (int i = 0; i < n; ++i) {
     u128 d = (u128)a[i] - b[i] - borrow;
     a[i] = (uint64_t)d;
     borrow = (uint64_t)((d >> 64) & 1);
@@ -638,42 +638,84 @@ double or_i128_to_double(int64_t hi, uint64_t lo) {
   return neg ? -d : d;
 }
 
-/* exact centered CRT of residues r[t] (t < L) -> (hi, lo) two's complement
- * i128; returns 0, or -3 if |X| >= 2^127 (out of the product's range). */
-int or_crt_centered(const uint64_t* r, uint32_t L, const uint64_t* q, int64_t* hi,
-                    uint64_t* lo) {
-  uint64_t Q[MW] = {0}, X[MW] = {0}, tmp[MW], qhat[MW];
-  Q[0] = 1;
+/* |X| (MW little-endian u64 words) with its sign -> double: Horner from the top word,
+ * d = d * 2^64 + (double)w_i (round 6).  Leading zero words leave d unchanged, so for
+ * |X| < 2^128 this is or_i128_to_double's (double)hi * 2^64 + (double)lo.  PALISADE's
+ * BigInteger::ConvertToDouble rounding is not pinned (no reference fixture decodes |X| >= 2^64). */
+double or_mw_to_double(const uint64_t* mag, int neg) {
+  double d = (double)mag[MW - 1];
+  for (int i = MW - 2; i >= 0; --i) d = d * 18446744073709551616.0 + (double)mag[i];
+  return neg ? -d : d;
+}
+
+/* Q, (Q - 1) / 2, Q/q_t and (Q/q_t)^-1 mod q_t of a tower set, computed once per call */
+typedef struct {
+  uint32_t L;
+  int n; /* words in use: L Q < 2^(64 n) */
+  const uint64_t* q;
+  uint64_t Q[MW], half[MW], qhat[16][MW], qhat_inv[16];
+} crt_plan;
+
+static void crt_plan_init(crt_plan* P, uint32_t L, const uint64_t* q) {
+  uint64_t tmp[MW];
+  memset(P, 0, sizeof(*P));
+  P->L = L;
+  P->q = q;
+  P->n = MW;
+  P->Q[0] = 1;
   for (uint32_t t = 0; t < L; ++t) {
-    mw_mul_small(Q, q[t], tmp);
-    memcpy(Q, tmp, sizeof(Q));
+    mw_mul_small(P->Q, q[t], tmp, MW);
+    memcpy(P->Q, tmp, sizeof(tmp));
   }
+  for (int i = 0; i < MW; ++i) P->half[i] = (P->Q[i] >> 1) | (i + 1 < MW ? P->Q[i + 1] << 63 : 0);
+  int top = MW - 1;
+  while (top > 0 && !P->Q[top]) --top;
+  P->n = top + 2 < MW ? top + 2 : MW; /* room for L Q */
   for (uint32_t t = 0; t < L; ++t) {
-    memset(qhat, 0, sizeof(qhat));
-    qhat[0] = 1;
+    P->qhat[t][0] = 1;
     uint64_t qhat_mod = 1;
     for (uint32_t u = 0; u < L; ++u)
       if (u != t) {
-        mw_mul_small(qhat, q[u], tmp);
-        memcpy(qhat, tmp, sizeof(qhat));
+        mw_mul_small(P->qhat[t], q[u], tmp, MW);
+        memcpy(P->qhat[t], tmp, sizeof(tmp));
         qhat_mod = mulmod(qhat_mod, q[u] % q[t], q[t]);
       }
-    uint64_t y = mulmod(r[t], inv_mod(qhat_mod, q[t]), q[t]);
-    mw_mul_small(qhat, y, tmp);
-    mw_add(X, tmp);
+    P->qhat_inv[t] = inv_mod(qhat_mod, q[t]);
   }
-  while (mw_cmp(X, Q) >= 0) mw_sub(X, Q);
+}
+
+/* exact centered CRT of residues r[t] (t < L): X in [-(Q-1)/2, (Q-1)/2] for Q = prod q_t
+ * (PALISADE's CRTInterpolate + centring mod Q before Decode, ckks.cpp:189)
+ * as magnitude words mag[MW] and a sign. */
+static void crt_plan_centered(const crt_plan* P, const uint64_t* r, uint64_t* mag, int* neg_out) {
+  uint64_t X[MW] = {0}, tmp[MW];
+  const int n = P->n;
+  for (uint32_t t = 0; t < P->L; ++t) {
+    uint64_t y = mulmod(r[t], P->qhat_inv[t], P->q[t]);
+    mw_mul_small(P->qhat[t], y, tmp, n);
+    mw_add(X, tmp, n);
+  }
+  while (mw_cmp(X, P->Q, n) >= 0) mw_sub(X, P->Q, n);
   /* center: X > Q/2 -> X - Q (negative) */
-  uint64_t half[MW];
-  memcpy(half, Q, sizeof(Q));
-  for (int i = 0; i < MW; ++i) half[i] = (Q[i] >> 1) | (i + 1 < MW ? Q[i + 1] << 63 : 0);
-  int neg = mw_cmp(X, half) > 0;
+  int neg = mw_cmp(X, P->half, n) > 0;
   if (neg) { /* |X| = Q - X */
     uint64_t A[MW];
-    memcpy(A, Q, sizeof(Q));
-    mw_sub(A, X);
+    memcpy(A, P->Q, sizeof(A));
+    mw_sub(A, X, n);
     memcpy(X, A, sizeof(A));
   }
+  memcpy(mag, X, sizeof(X));
+  *neg_out = neg;
+}
+
+/* the centred value as a two's-complement i128 (hi, lo); returns 0, or -3 if |X| >= 2^127 */
+int or_crt_centered(const uint64_t* r, uint32_t L, const uint64_t* q, int64_t* hi,
+                    uint64_t* lo) {
+  crt_plan P;
+  uint64_t X[MW];
+  int neg;
+  crt_plan_init(&P, L, q);
+  crt_plan_centered(&P, r, X, &neg);
   for (int i = 2; i < MW; ++i)
     if (X[i]) return -3;
   if (X[1] >> 63) return -3;
@@ -682,6 +724,16 @@ int or_crt_centered(const uint64_t* r, uint32_t L, const uint64_t* q, int64_t* h
   *hi = (int64_t)(v >> 64);
   *lo = (uint64_t)v;
   return 0;
+}
+
+/* the centred value as a double (or_mw_to_double), any |X| <= (Q - 1) / 2 */
+double or_crt_centered_double(const uint64_t* r, uint32_t L, const uint64_t* q) {
+  crt_plan P;
+  uint64_t X[MW];
+  int neg;
+  crt_plan_init(&P, L, q);
+  crt_plan_centered(&P, r, X, &neg);
+  return or_mw_to_double(X, neg);
 }
 
 /* decrypt one ciphertext ct[2][L][N] with sk[L][N] (EVAL).  Writes the first
@@ -703,21 +755,21 @@ int or_decrypt_coeffs(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32
   }
   double inv_scale = 1.0 / scale;
   uint32_t gap = N / (2 * slots);
-  uint64_t r[16];
-  int rc = 0;
-  for (uint32_t i = 0; i < slots && !rc; ++i) {
-    for (int part = 0; part < 2 && !rc; ++part) {
+  uint64_t r[16], X[MW];
+  crt_plan P;
+  crt_plan_init(&P, L, q);
+  for (uint32_t i = 0; i < slots; ++i) {
+    for (int part = 0; part < 2; ++part) {
       uint32_t j = (part ? N / 2 : 0) + i * gap;
+      int neg;
       for (uint32_t t = 0; t < L; ++t) r[t] = b[(size_t)t * N + j];
-      int64_t hi;
-      uint64_t lo;
-      rc = or_crt_centered(r, L, q, &hi, &lo);
-      double v = or_i128_to_double(hi, lo) * inv_scale;
+      crt_plan_centered(&P, r, X, &neg);
+      double v = or_mw_to_double(X, neg) * inv_scale;
       if (part) im[i] = v; else re[i] = v;
     }
   }
   free(b);
-  return rc;
+  return 0;
 }
 
 int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,

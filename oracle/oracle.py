@@ -78,6 +78,7 @@ def _load():
                                 C.c_uint32, u64p, C.c_double, u64p, C.c_int]),
         "or_crt_centered": (C.c_int, [u64p, C.c_uint32, u64p, i64p, u64p]),
         "or_i128_to_double": (C.c_double, [C.c_int64, C.c_uint64]),
+        "or_crt_centered_double": (C.c_double, [u64p, C.c_uint32, u64p]),
         "or_decrypt": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
                                  C.c_double, C.c_size_t, f64p]),
         "or_chacha20_block": (None, [u32p, C.c_uint64, C.c_uint64, u32p]),
@@ -309,6 +310,13 @@ def crt_centered(r, q):
     if rc:
         raise ValueError("crt out of range")
     return (hi.value << 64) + lo.value
+
+
+def crt_centered_double(r, q) -> float:
+    """The centred CRT value of residues r as the decode's double (any |X| <= (Q-1)/2; round 6)."""
+    r = u64(r)
+    q = u64(q)
+    return lib.or_crt_centered_double(_p(r, u64p), len(q), _p(q, u64p))
 
 
 def decrypt(ct, sk, q, psi, slots: int, scale: float, n: int) -> np.ndarray:
