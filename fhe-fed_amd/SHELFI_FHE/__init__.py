@@ -151,7 +151,9 @@ class CKKS(Scheme):
         once keys are generated or loaded in PALISADE's files), "shelfi" = this library's
         blob, "packed" = this library's blob with the residues at their moduli's bit widths
         (version 2; 15% fewer bytes at 2^15/L4 over the network and PCIe).  The choice
-        sticks across later loadCryptoParams / genCryptoContextAndKeyGen calls.
+        sticks across later loadCryptoParams / genCryptoContextAndKeyGen / set_keys calls
+        ("palisade" needs keys from PALISADE files or genCryptoContextAndKeyGen; after
+        set_keys it answers in "shelfi").
         computeWeightedAverage and decrypt accept all three and computeWeightedAverage
         answers in its inputs' format."""
         if fmt not in _WIRE_CODES:
@@ -181,6 +183,16 @@ class CKKS(Scheme):
         value PALISADE floods), which is what the parity tests compare."""
         check(self._lib.shelfi_set_decode_noise(self._ctx, 1 if enabled else 0, float(m_factor)),
               "set_decode_noise")
+
+    def set_decode_exact(self, exact: bool = True) -> None:
+        """Decode range (round 6).  Off (default): decrypt reads the shortest tower prefix above
+        2^130 and is exact for centred values in [-2^127, 2^127); anything outside that range is
+        detected and the call is redone over every tower through the exact multi-word CRT, up to
+        (Q-1)/2 as PALISADE's BigInteger decode (ckks.cpp:189).  The prefix cannot see a value of
+        |X| >= Q'/2 whose residue mod Q' falls inside that range (2^15 / L4: |X| >= 2^163).  On:
+        every decrypt reads every tower through the exact CRT (the same bits wherever both are
+        defined, ~25% slower at 2^15 / L4)."""
+        check(self._lib.shelfi_set_decode_exact(self._ctx, 1 if exact else 0), "set_decode_exact")
 
     def last_log_precision(self):
         """PALISADE Plaintext::GetLogPrecision of the last flooded decrypt (worst
@@ -221,6 +233,7 @@ class CKKS(Scheme):
             raise ValueError("key shapes must be [2][L][N] and [L][N]")
         check(self._lib.shelfi_set_keys(self._ctx, pk.ctypes.data_as(_lib.u64p),
                                         sk.ctypes.data_as(_lib.u64p)))
+        self._apply_wire()  # the chosen format sticks; "palisade" falls back to "shelfi"
 
     def get_keys(self):
         inf = self.info()

@@ -108,6 +108,7 @@ SIGNATURES = {
     "shelfi_palisade_embed_context": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(u8p),
                                                 C.POINTER(C.c_size_t)]),
     "shelfi_set_decode_noise": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "shelfi_set_decode_exact": (C.c_int, [C.c_void_p, C.c_int]),
     "shelfi_decode_log_error": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "shelfi_encrypt_into": (C.c_int, [C.c_void_p, f64p, C.c_size_t, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]),

@@ -11,6 +11,7 @@
 // per-ciphertext operation is a kernel in kernels.hip.
 #include <sys/random.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -623,7 +624,10 @@ static int arena_weight_slot(shelfi_ctx* ctx, const float* w, size_t C, hipStrea
   return i;
 }
 
-static Switches g_switches;
+// Process-wide switches: each reload publishes a new immutable snapshot through an
+// atomic pointer; snapshots are never freed (a few dozen bytes per reload), so a launch path on
+// another thread reads a consistent struct, never one being written.
+static std::atomic<const Switches*> g_switches{nullptr};
 
 static bool env_flag(const char* name, char off_or_on, bool dflt) {
   const char* e = getenv(name);
@@ -656,6 +660,8 @@ void reload_switches() {
   s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
   s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);
   s.wavg_rows = env_choice("SHELFI_WAVG_ROWS", {1, 2}, 0);
+  if (const char* e = getenv("SHELFI_WAVG_STRANDS"))
+    if (atoi(e) > 1 && atoi(e) <= 4096) s.wavg_strands = (uint32_t)atoi(e);
   s.arena_stager = env_choice("SHELFI_ARENA_STAGER", {0, 1}, -1);
   if (const char* e = getenv("SHELFI_DEV_CHUNK_MIB"))
     if (atoll(e) > 0) s.dev_chunk_mib = (uint64_t)atoll(e);
@@ -665,9 +671,9 @@ void reload_switches() {
     if (atoll(e) > 0 && atoll(e) <= 256) s.stage_slot_mib = (uint64_t)atoll(e);
   s.h2d_direct = env_flag("SHELFI_H2D_DIRECT", '1', false);
   s.h2d_two = env_flag("SHELFI_H2D_TWO", '0', true);
-  g_switches = s;
+  g_switches.store(new Switches(s), std::memory_order_release);
 }
-const Switches& switches() { return g_switches; }
+const Switches& switches() { return *g_switches.load(std::memory_order_acquire); }
 static const bool g_switches_read = (reload_switches(), true);
 
 }  // namespace shelfi
@@ -728,7 +734,7 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
   *out = nullptr;
   shelfi_ctx* ctx = new (std::nothrow) shelfi_ctx();
   if (!ctx) return SHELFI_ERR_DEVICE;
-  reload_switches();  // the probe switches are read once per context
+  reload_switches();  // the process-wide probe switches are re-read when a context is created
   int rc = guarded([&] {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -1683,6 +1689,13 @@ int shelfi_set_decode_noise(shelfi_ctx* ctx, int enabled, double m_factor) {
   return SHELFI_OK;
 }
 
+int shelfi_set_decode_exact(shelfi_ctx* ctx, int exact) {
+  if (!ctx) return SHELFI_ERR_ARG;
+  std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
+  ctx->decode_exact = exact ? 1 : 0;
+  return SHELFI_OK;
+}
+
 int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
   if (!ctx || !log_error) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
@@ -1777,8 +1790,12 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       sr.finish();
       pp.sync();
     };
-    run(false);
-    if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
+    if (ctx->decode_exact)
+      run(true);
+    else {
+      run(false);
+      if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
+    }
     decode_noise_end(ctx, dn);
   });
 }
@@ -2325,14 +2342,16 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
       }
       decode_noise_readback(ctx, dn, s);
     };
-    SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, s));
-    run(false);
-    SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, s));  // pinned
-    SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
-    if (ctx->host_flag[7]) {  // a value outside the fast CRT's range: the whole call again, exactly
+    if (ctx->decode_exact) {
       run(true);
+    } else {
+      SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, s));
+      run(false);
+      SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, s));  // pinned
       SHELFI_HIP(hipStreamSynchronize(s));
+      if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
     }
+    SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);
   });
 }

@@ -55,8 +55,9 @@ inline uint32_t ntt_block_log(uint32_t logN) {
   return logN < b ? logN : b;
 }
 
-// A/B probe switches (none changes an output bit), read from the environment
-// when a context is created and by shelfi_reload_switches() -- never on a launch path.
+// A/B probe switches (none changes an output bit), process-wide: read from the
+// environment when a context is created and by shelfi_reload_switches() -- never on a launch path --
+// and published as an immutable snapshot (api.cpp), so concurrent calls never see a torn struct.
 struct Switches {
   bool xcd_order = true;       // SHELFI_XCD_ORDER=0: natural block order in the NTT block passes
   bool ntt_wl = true;          // SHELFI_NTT_WL=0: a workgroup barrier at every block-pass exchange
@@ -74,6 +75,7 @@ struct Switches {
   int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
   int pack_waves = 0;          // SHELFI_PACK_WAVES=2|8 (0: 4 rows per block)
   int wavg_rows = 0;           // SHELFI_WAVG_ROWS=1|2 (0: by shape)
+  uint32_t wavg_strands = 0;   // SHELFI_WAVG_STRANDS=n: wavg_packed's blocks in n interleaved strands (0: in order)
   int arena_stager = -1;       // SHELFI_ARENA_STAGER=0|1 (-1: by upload shape)
   uint64_t dev_chunk_mib = 4096;  // SHELFI_DEV_CHUNK_MIB: device encrypt / decrypt scratch per chain
   uint64_t wavg_chunk_mib = 0;    // SHELFI_WAVG_CHUNK_MIB: bytes-API aggregation chunk per learner group
@@ -249,6 +251,7 @@ struct shelfi_ctx {
   std::vector<ArenaRefusal> arena_refused;
   int decode_noise = 1;          // shelfi_set_decode_noise (PALISADE floods every decode)
   double decode_m_factor = 1.0;
+  int decode_exact = 0;          // shelfi_set_decode_exact: every decrypt over every tower, exact CRT
   int last_log_error = -1;       // of the last flooded decrypt, -1 if none
   std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)
   std::string pal_keytag;        // PALISADE keys: key tag

@@ -324,11 +324,21 @@ __global__ __launch_bounds__(64 * WV) void wavg_packed(const uint32_t* __restric
                                                       const uint32_t* __restrict__ wl, uint32_t C, uint32_t crow,
                                                       uint64_t lstride, uint64_t rows, uint32_t L, uint32_t logN,
                                                       ArenaPack ap, const TowerConst* __restrict__ tcs,
-                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pout) {
+                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pout,
+                                                      uint32_t strands, uint32_t nblocks) {
   // the running sum of the rows' residues across learner groups (C > 16): 8 x 64 per wave
   __shared__ uint64_t run_lds[WV][8 * 64];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t r = (uint64_t)blockIdx.x * WV + wave;
+  // strands > 1 (probe): dispatch order interleaves `strands` contiguous runs of blocks spread over
+  // the buffers (block b -> (b mod strands) * per + b / strands), so the blocks in flight read and
+  // write `strands` separate windows of the arena and the output instead of one
+  uint32_t bi = blockIdx.x;
+  if (strands > 1) {
+    const uint32_t per = (nblocks + strands - 1) / strands;
+    bi = (bi % strands) * per + bi / strands;
+    if (bi >= nblocks) return;
+  }
+  const uint64_t r = (uint64_t)bi * WV + wave;
   if (r >= rows) return;
   const uint32_t lane = threadIdx.x & 63;
   uint64_t x[8];
@@ -523,9 +533,11 @@ void launch_wavg_packed_ex(const uint32_t* in, const uint32_t* wl_dev, uint32_t 
   }
   const uint64_t blocks = (nrows + wvs - 1) / wvs;
   if (blocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "aggregation batch too large"};
+  const uint32_t strands = sw.wavg_strands > 1 && blocks >= 4ull * sw.wavg_strands ? sw.wavg_strands : 0;
+  const uint64_t grid = strands ? (blocks + strands - 1) / strands * strands : blocks;
 #define WPK(UU, WW, PO, STK)                                                                                 \
-  hipLaunchKernelGGL((wavg_packed<UU, WW, PO, STK>), dim3((uint32_t)blocks), dim3(64 * WW), 0, s, in, wl_dev,  \
-                     C, crow, lstride, nrows, L, logN, ap, tc, out, pout)
+  hipLaunchKernelGGL((wavg_packed<UU, WW, PO, STK>), dim3((uint32_t)grid), dim3(64 * WW), 0, s, in, wl_dev,    \
+                     C, crow, lstride, nrows, L, logN, ap, tc, out, pout, strands, (uint32_t)blocks)
   if (stk && po)
     throw Error{SHELFI_ERR_ARG, "stacked inputs with a packed output"};
   else if (stk)

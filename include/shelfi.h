@@ -126,6 +126,15 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
  * the exact, deterministic decode (parity mode).  Applies to shelfi_decrypt and
  * shelfi_dev_decrypt.  Randomness: the ctx's seeded / OS-random ChaCha20 stream. */
 int shelfi_set_decode_noise(shelfi_ctx* ctx, int enabled, double m_factor);
+/* Decode range (round 6).  exact = 0 (default): decrypt reads the shortest tower prefix whose
+ * modulus Q' exceeds 2^130 and reconstructs each coefficient exactly while its centred value is in
+ * [-2^127, 2^127); a coefficient outside that range is detected and the call is redone over every
+ * tower through an exact multi-word CRT, up to (Q - 1) / 2 (PALISADE's BigInteger decode,
+ * ckks.cpp:189).  The prefix cannot see a value of |X| >= Q'/2 whose residue mod Q' falls inside
+ * [-2^127, 2^127) (|X| >= 2^163 at 2^15 / L4).  exact = 1: every decrypt reads every tower and
+ * decodes through the exact CRT (same output bits wherever both are defined; ~25% slower at
+ * 2^15 / L4).  Applies to shelfi_decrypt and the shelfi_dev_decrypt* calls. */
+int shelfi_set_decode_exact(shelfi_ctx* ctx, int exact);
 /* logError of the last flooded decrypt (max over its ciphertexts; PALISADE
  * Plaintext::GetLogError), -1 if none.  Precision = scale_bits - logError. */
 int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error);

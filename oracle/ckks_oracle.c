@@ -788,6 +788,57 @@ int or_decrypt(const uint64_t* ct, const uint64_t* sk, uint32_t N, uint32_t L,
   return rc;
 }
 
+/* ckks.cpp:61-104 encrypt() and ckks.cpp:170-213 decrypt() over a whole vector, with the
+ * reference's schedule: "#pragma omp parallel for" over ciphertexts (ckks.cpp:70, :186), here with
+ * nthreads threads (the CPU baseline's all-core figure, bench.py).  Ciphertext k of encrypt holds
+ * x[k*slots .. min(n, (k+1)*slots)) with the seeded sampler's stream g0 + k (encrypt_vector in
+ * oracle.py); decrypt's ciphertext k contributes min(slots, n - k*slots) values (:192-196).
+ * Returns 0, or the first failing ciphertext's code. */
+void or_sample_encrypt(uint64_t seed, uint64_t g, uint32_t N, double sigma, int64_t* v, int64_t* e0,
+                       int64_t* e1);
+int or_encrypt_vector(const double* x, size_t n, const uint64_t* pk, uint32_t N, uint32_t L,
+                      const uint64_t* q, const uint64_t* psi, uint32_t slots, double delta, double sigma,
+                      uint64_t seed, uint64_t g0, uint64_t* out, int nthreads) {
+  const size_t K = n ? (n + slots - 1) / slots : 1;
+  int rc = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+  for (size_t k = 0; k < K; ++k) {
+    uint64_t* m = malloc(sizeof(uint64_t) * (size_t)L * N);
+    int64_t* v = malloc(sizeof(int64_t) * 3 * (size_t)N);
+    const size_t lo = k * slots, len = n > lo ? (n - lo < slots ? n - lo : slots) : 0;
+    int r = or_encode(x + lo, len, N, slots, delta, L, q, psi, m);
+    if (!r) {
+      or_sample_encrypt(seed, g0 + k, N, sigma, v, v + N, v + 2 * (size_t)N);
+      or_encrypt(pk, m, v, v + N, v + 2 * (size_t)N, N, L, q, psi, out + k * 2 * (size_t)L * N);
+    }
+    if (r) {
+#pragma omp critical
+      if (!rc) rc = r;
+    }
+    free(m);
+    free(v);
+  }
+  return rc;
+}
+
+int or_decrypt_vector(const uint64_t* cts, size_t K, const uint64_t* sk, uint32_t N, uint32_t L,
+                      const uint64_t* q, const uint64_t* psi, uint32_t slots, double scale, size_t n,
+                      double* out, int nthreads) {
+  int rc = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+  for (size_t k = 0; k < K; ++k) {
+    const size_t lo = k * slots;
+    if (lo >= n) continue;
+    const size_t len = n - lo < slots ? n - lo : slots;
+    int r = or_decrypt(cts + k * 2 * (size_t)L * N, sk, N, L, q, psi, slots, scale, len, out + lo);
+    if (r) {
+#pragma omp critical
+      if (!rc) rc = r;
+    }
+  }
+  return rc;
+}
+
 /* PALISADE 1.11 CKKSPackedEncoding::Decode noise flooding [PALISADE-1.11, SURVEY
  * App. B.6], restated on the coefficient pairs above (output units; PALISADE's
  * 2^p-scaled values are these times 2^p, an exact power-of-two rescaling):

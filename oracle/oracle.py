@@ -79,6 +79,10 @@ def _load():
         "or_crt_centered": (C.c_int, [u64p, C.c_uint32, u64p, i64p, u64p]),
         "or_i128_to_double": (C.c_double, [C.c_int64, C.c_uint64]),
         "or_crt_centered_double": (C.c_double, [u64p, C.c_uint32, u64p]),
+        "or_encrypt_vector": (C.c_int, [f64p, C.c_size_t, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
+                                        C.c_double, C.c_double, C.c_uint64, C.c_uint64, u64p, C.c_int]),
+        "or_decrypt_vector": (C.c_int, [u64p, C.c_size_t, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
+                                        C.c_double, C.c_size_t, f64p, C.c_int]),
         "or_decrypt": (C.c_int, [u64p, u64p, C.c_uint32, C.c_uint32, u64p, u64p, C.c_uint32,
                                  C.c_double, C.c_size_t, f64p]),
         "or_chacha20_block": (None, [u32p, C.c_uint64, C.c_uint64, u32p]),
@@ -389,6 +393,33 @@ def encrypt_vector(x, pk, q, psi, N: int, slots: int, delta: float, seed: int, g
         m = encode(chunk, N, slots, delta, q, psi)
         v, e0, e1 = sample_encrypt(seed, g0 + k, N)
         out[k] = encrypt(pk, m, v, e0, e1, q, psi)
+    return out
+
+
+def encrypt_vector_omp(x, pk, q, psi, N: int, slots: int, delta: float, seed: int, g0: int = 0,
+                       nthreads: int = 1):
+    """encrypt_vector in one C call, OpenMP over ciphertexts as ckks.cpp:70 (the CPU baseline's
+    all-core figure); bit-identical to encrypt_vector."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    K = max(1, -(-len(x) // slots))
+    q, psi, pk = u64(q), u64(psi), u64(pk)
+    out = np.zeros((K, 2, len(q), N), np.uint64)
+    rc = lib.or_encrypt_vector(_p(x, f64p), len(x), _p(pk, u64p), N, len(q), _p(q, u64p), _p(psi, u64p), slots,
+                               float(delta), SIGMA, seed, g0, _p(out, u64p), int(nthreads))
+    if rc:
+        raise ValueError("encrypt failed rc=%d" % rc)
+    return out
+
+
+def decrypt_vector_omp(cts, sk, q, psi, slots: int, scale: float, n: int, nthreads: int = 1):
+    """decrypt_vector in one C call, OpenMP over ciphertexts as ckks.cpp:186."""
+    cts, sk, q, psi = u64(cts), u64(sk), u64(q), u64(psi)
+    K, _, L, N = cts.shape
+    out = np.zeros(n, np.float64)
+    rc = lib.or_decrypt_vector(_p(cts, u64p), K, _p(sk, u64p), N, L, _p(q, u64p), _p(psi, u64p), slots,
+                               float(scale), n, _p(out, f64p), int(nthreads))
+    if rc:
+        raise ValueError("decrypt failed rc=%d" % rc)
     return out
 
 

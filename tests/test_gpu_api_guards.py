@@ -111,3 +111,24 @@ def test_bytes_api_rejects_residues_not_below_q(ck, C, where):
     # the context stays usable
     out = ck.decrypt(ck.computeWeightedAverage([good] * C, [1.0 / C] * C), 5000)
     assert np.abs(out - x).max() < 1e-7
+
+
+def test_wire_format_sticks_across_set_keys():
+    """set_keys re-applies the chosen wire format ("packed" stays "packed"; "palisade",
+    which needs PALISADE key files, answers in "shelfi" after keys of unknown origin)."""
+    src = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=22, decodeNoise=False)
+    src.loadCryptoParams()
+    pk, sk = src.get_keys()
+    assert src.wire_format() == "palisade"
+    c = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=23, decodeNoise=False)
+    c.loadCryptoParams()
+    c.set_wire_format("packed")
+    c.set_keys(pk, sk)
+    assert c.wire_format() == "packed"
+    x = np.linspace(-1, 1, 300)
+    assert np.abs(c.decrypt(c.encrypt(x), 300) - x).max() < 1e-9
+    d = m.CKKS("ckks", 4096, 52, PALISADE_DIR, seed=24, decodeNoise=False)
+    d.loadCryptoParams()
+    assert d.wire_format() == "palisade"
+    d.set_keys(pk, sk)
+    assert d.wire_format() == "shelfi"

@@ -200,3 +200,34 @@ def test_flooded_decode_failure_matches_oracle(cfg2):
             ck.decrypt(blob, S)
     finally:
         ck.set_decode_noise(False)
+
+
+def test_exact_mode(cfg2):
+    """set_decode_exact(True) (shelfi_set_decode_exact): every decrypt over every tower through the
+    exact CRT.  Same bits as the default on narrow and wide ciphertexts (bytes and device API), and
+    the true value of a ciphertext the prefix cannot see: coefficient 0 raised by 7 Q' (Q' = q0 q1
+    q2, the default path's prefix) leaves the prefix residues unchanged, while X_0 ~ 2^167 < Q/2."""
+    ck = cfg2
+    q, psi, N, S, delta = _arrays(ck)
+    _, sk = ck.get_keys()
+    x = np.random.default_rng(11).uniform(-1, 1, 2 * S)
+    x[S:] *= 2.0 ** 90
+    ck.set_seed(111)
+    blob = ck.encrypt(x)
+    res = m.blob_residues(blob, N, len(q))
+    a = ck.decrypt(blob, 2 * S)
+    Qp = int(q[0]) * int(q[1]) * int(q[2])
+    mod = res[:1].copy()
+    for t in range(len(q)):  # EVAL domain: a constant polynomial is that constant at every point
+        mod[0, 0, t, :] = (mod[0, 0, t, :] + np.uint64(7 * Qp % int(q[t]))) % q[t]
+    ck.set_decode_exact(True)
+    try:
+        b = ck.decrypt(blob, 2 * S)
+        bd = D.decrypt(ck, torch.from_numpy(res.view(np.int64)).cuda(), 2 * S, delta).cpu().numpy()
+        e = ck.decrypt(m.blob_pack(ck, mod), S)
+    finally:
+        ck.set_decode_exact(False)
+    assert np.array_equal(a, b) and np.array_equal(bd, a)
+    assert np.array_equal(a, O.decrypt_vector(res, sk, q, psi, S, delta, 2 * S))
+    assert np.array_equal(e, O.decrypt_vector(mod, sk, q, psi, S, delta, S))
+    assert np.abs(e - x[:S]).max() > 2.0 ** 100  # the 7 Q' term is in the decode

@@ -473,3 +473,35 @@ def test_modq_after_sum(cfg2):
         for t in range(L):
             ref[:, :, t] = (ref[:, :, t] + a[:, :, t]) % q[t]
     assert np.array_equal(dev.cpu().numpy().view(np.uint64), ref)
+
+
+def test_negative_and_mixed_sign_weights(cfg2):
+    """EvalMult's integer weight for w < 0 (ckks.cpp:287-288):
+    W = (int64)((double)(float)w Delta + 0.5) truncates toward zero, which differs from llround when
+    the fraction of |w| Delta exceeds 1/2 -- the survey's reading, unpinned vs PALISADE (no
+    reference fixture aggregates with a negative weight).  The weights below include such cases
+    (checked here), through the device wavg, the packed arena and the bytes API, bit-exact vs
+    the oracle, and the decrypted aggregate is sum (float)w_i x_i."""
+    inf, q, psi, N, S, delta = _ctx_arrays(cfg2)
+    w = [-0.3, 0.7, -1e-3, 0.45, -0.05, 0.2]
+    trunc = [int(float(np.float32(v)) * delta + 0.5) for v in w]
+    nearest = [round(float(np.float32(v)) * delta) for v in w]
+    assert any(a != b for a, b in zip(trunc, nearest))  # the truncation is exercised
+    C, K = len(w), 2
+    rng = np.random.default_rng(88)
+    xs = [rng.uniform(-1, 1, K * S) for _ in range(C)]
+    cfg2.set_seed(880)
+    blobs = [cfg2.encrypt(x) for x in xs]
+    res = [m.blob_residues(b, N, len(q)) for b in blobs]
+    ref = O.wavg(res, w, q, delta)
+    agg = cfg2.computeWeightedAverage(blobs, w)
+    assert np.array_equal(m.blob_residues(agg, N, len(q)), ref)
+    dev = [torch.from_numpy(r.view(np.int64)).cuda() for r in res]
+    assert np.array_equal(D.wavg(cfg2, dev, w).cpu().numpy().view(np.uint64), ref)
+    ar = D.Arena(cfg2, C, K)
+    for c in range(C):
+        ar.put(c, dev[c])
+    assert np.array_equal(ar.wavg(w).cpu().numpy().view(np.uint64), ref)
+    dec = np.asarray(cfg2.decrypt(agg, K * S))
+    exp = sum(float(np.float32(wi)) * x for wi, x in zip(w, xs))
+    assert np.abs(dec - exp).max() < 1e-7
