@@ -1397,7 +1397,13 @@ __global__ __launch_bounds__(256) void ntt_fwd_cols_enc(const int64_t* __restric
 // DeviceTables::enc_vtab entries for each row; this kernel writes only the column's 4 radix-4 group
 // patterns, packed 7 bits each into one uint32 at word c of the ciphertext's pbuf v region (8 KiB per
 // ciphertext instead of v's 4 towers x 256 KiB).
-template <int LOGR, bool TAB, int WV = 4, bool TWL = false, bool TS = false, bool VT = false>
+// X5 (round 6; LOGR = 4, not TS / VT): one more columns stage for rings whose blocks pass starts at
+// global stage 5 (2^16 over 2^11 blocks, nlogR = 5).  A workgroup's threads hold columns c (tid < 128)
+// and c + BLK/2 (tid >= 128) of the 16-row decomposition; stage 4 pairs row r of the two (twiddle
+// psi_rev[16 + r]), so after the register stages each thread trades 8 rows with its partner through
+// LDS and runs 8 of the 16 butterflies: the low thread keeps rows 0-7 of both columns, the high one
+// rows 8-15.  pbuf then holds what a 32-row columns pass leaves, without 32-row register columns.
+template <int LOGR, bool TAB, int WV = 4, bool TWL = false, bool TS = false, bool VT = false, bool X5 = false>
 __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2* __restrict__ fbuf, uint64_t K,
                                                       uint32_t logN, uint32_t logS, uint32_t L,
                                                       double delta, const uint64_t* __restrict__ cdt,
@@ -1412,9 +1418,12 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
   constexpr int NTW = TS ? 4 : 1;  // towers with their own LDS tables in one workgroup
   static_assert(LOGR == 3 || LOGR == 4, "a column is 8 or 16 rows of one sample group");
   static_assert(!VT || (LOGR == 4 && TAB && !TS), "v tables: 16-row columns, one column per thread");
+  static_assert(!X5 || (LOGR == 4 && TAB && !TS && !VT), "the exchanged stage: 16-row columns, one per thread");
+  constexpr int NTWL = X5 ? 2 << LOGR : 1 << LOGR;  // column-stage twiddles psi_rev[1 .. NTWL)
   __shared__ uint32_t thi[64], tlo[64];
   __shared__ uint64_t tabs_all[NTW][kEncTab];  // the tower's DeviceTables::enc_tab slice
-  __shared__ ulonglong2 twl_all[NTW][1 << LOGR];  // TWL: the tower's {w, w'} for column stages (index m + i)
+  __shared__ ulonglong2 twl_all[NTW][NTWL];  // TWL: the tower's {w, w'} for column stages (index m + i)
+  __shared__ uint64_t xch[X5 ? 8 * 256 : 1];   // X5: the 8 rows a thread trades, [row][thread]
   static_assert(!TWL || TAB, "LDS twiddles ride on the table path's per-tower barrier");
   const uint32_t wave = TS ? (threadIdx.x >> 6) : 0u, tid = TS ? (threadIdx.x & 63u) : threadIdx.x;
   uint64_t* tabs = tabs_all[wave];
@@ -1431,8 +1440,11 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
   const uint32_t N = 1u << logN, BLK = N >> LOGR, N16 = N >> 4, V0 = N >> 6;
   const uint64_t gid = TS ? (uint64_t)blockIdx.x * 64 + tid : (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = gid >> (logN - LOGR);
-  if (k >= K) return;
-  const uint32_t c = (uint32_t)(gid & (BLK - 1));
+  if (k >= K) return;  // workgroup-uniform (BLK is a multiple of 256)
+  // X5: workgroup wi of a ciphertext holds column pairs (wi 128 + l, wi 128 + l + BLK/2), l < 128
+  const uint32_t c = X5 ? (((uint32_t)(gid & (BLK - 1)) >> 8) << 7) + (threadIdx.x & 127u) +
+                              ((threadIdx.x >> 7) ? (BLK >> 1) : 0u)
+                        : (uint32_t)(gid & (BLK - 1));
   const uint32_t h = c & (N16 - 1), i0 = c >> (logN - 4);
   const uint64_t nonce = (1ull << 56) | (g0 + k);
   const uint32_t S = 1u << logS, gapLog = logN - 1 - logS;
@@ -1474,6 +1486,61 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
       }
     }
     uint64_t* __restrict__ o = out + (k * 3 + poly) * LN + ((uint64_t)t << logN) + c;
+    if constexpr (X5) {
+      // stage LOGR: row r of column c (low thread) with row r of c + BLK/2 (high thread), twiddle
+      // psi_rev[R + r]; each keeps 8 rows of both columns
+      const bool lo = threadIdx.x < 128;  // wave-uniform
+      __syncthreads();                    // the previous exchange's reads are done
+      // (explicit wave-uniform branches: a select between two register elements becomes a select
+      // of addresses, which puts the array in scratch)
+      if (lo) {
+#pragma unroll
+        for (int r = 0; r < R / 2; ++r) xch[r * 256 + threadIdx.x] = x[R / 2 + r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < R / 2; ++r) xch[r * 256 + threadIdx.x] = x[r];
+      }
+      __syncthreads();
+      uint64_t y[R / 2];
+#pragma unroll
+      for (int r = 0; r < R / 2; ++r) y[r] = xch[r * 256 + (threadIdx.x ^ 128u)];
+      constexpr bool RD = fwd_red_at(LOGR);
+      const uint32_t rb = lo ? 0u : (uint32_t)(R / 2);  // this thread's rows rb .. rb + 7
+      const int64_t dpart = lo ? (int64_t)(BLK >> 1) : -(int64_t)(BLK >> 1);  // the partner column
+#pragma unroll
+      for (int r = 0; r < R / 2; ++r) {
+        uint64_t W, Wp;
+        if constexpr (TWL) {
+          const ulonglong2 T2 = twl[R + rb + r];
+          W = T2.x;
+          Wp = T2.y;
+        } else {
+          W = w[R + rb + r];
+          Wp = wp[R + rb + r];
+        }
+        // low: (x[r], y[r]) = (c, c + BLK/2) at row r; high: (y[r], x[8 + r]) = (c - BLK/2, c) at row 8 + r
+        // (wave-uniform branches with static register indices)
+        if (lo)
+          ct_bfly_s<!NR && RD>(x[r], y[r], W, Wp, q, cst.n8q);
+        else
+          ct_bfly_s<!NR && RD>(y[r], x[R / 2 + r], W, Wp, q, cst.n8q);
+      }
+      const auto fin = [&](uint64_t v) { return (!NR && fwd_bound(LOGR + 1) > 8) ? csub_neg(v, cst.n8q) : v; };
+      if (lo) {
+#pragma unroll
+        for (int r = 0; r < R / 2; ++r) {
+          o[(uint64_t)r * BLK] = fin(x[r]);          // own column
+          o[(uint64_t)r * BLK + dpart] = fin(y[r]);  // the partner's column
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R / 2; ++r) {
+          o[(uint64_t)(R / 2 + r) * BLK] = fin(x[R / 2 + r]);
+          o[(uint64_t)(R / 2 + r) * BLK + dpart] = fin(y[r]);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r)
       o[(uint64_t)r * BLK] = (!NR && fwd_bound(LOGR) > 8) ? csub_neg(x[r], cst.n8q) : x[r];
@@ -1539,7 +1606,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
         tower_sync();  // the previous tower's lookups are done (every thread runs every tower)
         for (uint32_t i = tid; i < (uint32_t)kEncTab; i += (TS ? 64u : 256u)) tabs[i] = enc_tab[(size_t)t * kEncTab + i];
         if constexpr (TWL) {
-          if (tid < (uint32_t)R)
+          if (tid < (uint32_t)NTWL)
             twl[tid] = make_ulonglong2(tw[((uint64_t)t << logN) + tid], twp[((uint64_t)t << logN) + tid]);
         }
         tower_sync();
@@ -1604,7 +1671,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
       if (TS && t != wave) continue;  // wave-uniform
       if constexpr (TWL) {
         tower_sync();  // every thread runs every tower
-        if (tid < (uint32_t)R)
+        if (tid < (uint32_t)NTWL)
           twl[tid] = make_ulonglong2(tw[((uint64_t)t << logN) + tid], twp[((uint64_t)t << logN) + tid]);
         tower_sync();
       }
@@ -1682,10 +1749,15 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   launch_encode_fft(p, dt, x, n, K, fbuf, s);
   Key8 k8;
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
-  const uint32_t nblkLog = ntt_block_log(p.logN);
-  const int nlogR = (int)(p.logN - nblkLog);
   const Switches& sw = switches();
-  const bool fused = (nlogR == 3 || nlogR == 4) && dt.enc_tab && sw.enc_fused;
+  // 2^16 over 2^12 blocks (round 6): a 16-row columns pass, the 2^15 kernels' shape
+  const bool bl12 = p.logN == 16 && dt.tw_fwd_blk12 && sw.enc_bl12;
+  const uint32_t nblkLog = bl12 ? 12u : ntt_block_log(p.logN);
+  const ulonglong2* twb = bl12 ? dt.tw_fwd_blk12 : dt.tw_fwd_blk;
+  const int nlogR = (int)(p.logN - nblkLog);
+  // nlogR = 5 (2^16 over 2^11 blocks, 2^17): the 16-row kernel with the exchanged fifth stage (X5)
+  const bool fused = (nlogR == 3 || nlogR == 4 || (nlogR == 5 && sw.enc_tab && sw.enc_x5 > 0)) && dt.enc_tab &&
+                     sw.enc_fused;
   int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
   int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
   // NORED towers (fwd_set_ct): q < kNoRedQ, run unreduced through both passes — only with the
@@ -1704,7 +1776,7 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   bool vt = false;  // NTT(v)'s columns pass as enc_vtab sums in the blocks pass (round 5)
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
-    const uint64_t nb = (K << (p.logN - nlogR)) / 256;
+    const uint64_t nb = (K << (p.logN - (nlogR == 5 ? 4 : nlogR))) / 256;
     const bool tab = sw.enc_tab;
     // LDS column twiddles at 3 waves/SIMD with the tables (no SGPR / VGPR spills): enc_cols_fused 578 ->
     // 534 us per 714 cts (probes/r03_enc_cols_twl.txt; the scalar-loaded form was removed in round 5)
@@ -1716,7 +1788,11 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     // ciphertexts spreads over 4x the waves; SHELFI_ENC_TS=0 / 1 forces either (A/B switch)
     const bool ts = nlogR == 4 && tab && p.L == 4 && (sw.enc_ts >= 0 ? sw.enc_ts == 1 : K <= kEncTsMaxK);
     vt = pp && tab && !ts && nlogR == 4 && dt.enc_vtab && sw.enc_vt && ntt_wave_local();
-    if (vt)  // v's columns pass left to the blocks pass (enc_vtab sums)
+    if (nlogR == 5 && sw.enc_x5 == 2)  // X5: 16 register rows + the exchanged fifth stage
+      ENC_COLS(4, true, 2, true, false, false, true);
+    else if (nlogR == 5)
+      ENC_COLS(4, true, 3, true, false, false, true);
+    else if (vt)  // v's columns pass left to the blocks pass (enc_vtab sums)
       ENC_COLS(4, true, 3, true, false, true);
     else if (ts)
       hipLaunchKernelGGL((enc_cols_fused<4, true, 3, true, true>), dim3((uint32_t)(nb * 4)), dim3(256), 0, s, fbuf, K,
@@ -1785,10 +1861,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     if (t_split < p.L) launch_pp(t_split, p.L - t_split, true);
   } else if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
+                       pbuf, p.L, p.logN, twb, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
+                       pbuf, p.L, p.logN, twb, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
                      pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
@@ -2859,7 +2935,9 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
   // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts); the
   // last pass fused with the CRT decode where its shape allows
-  const uint32_t blkLog = ntt_block_log(p.logN);
+  const bool bl12 = p.logN == 16 && dt.tw_inv_blk12 && switches().dec_bl12;  // as launch_encrypt's
+  const uint32_t blkLog = bl12 ? 12u : ntt_block_log(p.logN);
+  const ulonglong2* twb = bl12 ? dt.tw_inv_blk12 : dt.tw_inv_blk;
   const int logR = (int)(p.logN - blkLog);
   const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
   const bool fuse = !exact && logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
@@ -2874,25 +2952,25 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
       if (sum_in)
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, true>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else if (ntt_wave_local())
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false, true>), dim3(ncombo * pc), dim3(256), 0, s,
-                           dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
     } else if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 11 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,
