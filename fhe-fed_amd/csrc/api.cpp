@@ -188,8 +188,6 @@ void free_ntt_tables(DeviceTables& dt) {
   dfree_t(dt.ipsi_rev_sh);
   dfree_t(dt.tw_fwd_blk);
   dfree_t(dt.tw_inv_blk);
-  dfree_t(dt.tw_fwd_blk12);
-  dfree_t(dt.tw_inv_blk12);
 }
 
 static void free_tables(shelfi_ctx* ctx) {
@@ -340,10 +338,6 @@ void build_ntt_tables(const Params& p, DeviceTables& dt) {
     const uint32_t BL = ntt_block_log(p.logN);
     dt.tw_fwd_blk = upload(slices(BL, pr, prs).data(), (size_t)L * N);
     dt.tw_inv_blk = upload(slices(BL, ipr, iprs).data(), (size_t)L * N);
-    if (p.logN == 16 && BL == 11) {
-      dt.tw_fwd_blk12 = upload(slices(12, pr, prs).data(), (size_t)L * N);
-      dt.tw_inv_blk12 = upload(slices(12, ipr, iprs).data(), (size_t)L * N);
-    }
   }
 }
 
@@ -662,9 +656,7 @@ void reload_switches() {
   s.enc_vt = env_flag("SHELFI_ENC_VT", '0', true);
   s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
   s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
-  s.enc_bl12 = env_flag("SHELFI_ENC_BL12", '1', false);
-  s.enc_x5 = env_choice("SHELFI_ENC_X5", {0, 1, 2}, 1);
-  s.dec_bl12 = env_flag("SHELFI_DEC_BL12", '1', false);
+  s.enc_x5 = env_flag("SHELFI_ENC_X5", '0', true);
   if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;
   s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
   s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);

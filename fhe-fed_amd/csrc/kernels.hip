@@ -1750,13 +1750,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   Key8 k8;
   for (int i = 0; i < 8; ++i) k8.k[i] = key[i];
   const Switches& sw = switches();
-  // 2^16 over 2^12 blocks (round 6): a 16-row columns pass, the 2^15 kernels' shape
-  const bool bl12 = p.logN == 16 && dt.tw_fwd_blk12 && sw.enc_bl12;
-  const uint32_t nblkLog = bl12 ? 12u : ntt_block_log(p.logN);
-  const ulonglong2* twb = bl12 ? dt.tw_fwd_blk12 : dt.tw_fwd_blk;
+  const uint32_t nblkLog = ntt_block_log(p.logN);
   const int nlogR = (int)(p.logN - nblkLog);
   // nlogR = 5 (2^16 over 2^11 blocks, 2^17): the 16-row kernel with the exchanged fifth stage (X5)
-  const bool fused = (nlogR == 3 || nlogR == 4 || (nlogR == 5 && sw.enc_tab && sw.enc_x5 > 0)) && dt.enc_tab &&
+  const bool fused = (nlogR == 3 || nlogR == 4 || (nlogR == 5 && sw.enc_tab && sw.enc_x5)) && dt.enc_tab &&
                      sw.enc_fused;
   int64_t* me0 = reinterpret_cast<int64_t*>(pbuf + K * 3ull * p.L * p.N);
   int16_t* ve = reinterpret_cast<int16_t*>(me0 + K * (uint64_t)p.N);
@@ -1788,9 +1785,9 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     // ciphertexts spreads over 4x the waves; SHELFI_ENC_TS=0 / 1 forces either (A/B switch)
     const bool ts = nlogR == 4 && tab && p.L == 4 && (sw.enc_ts >= 0 ? sw.enc_ts == 1 : K <= kEncTsMaxK);
     vt = pp && tab && !ts && nlogR == 4 && dt.enc_vtab && sw.enc_vt && ntt_wave_local();
-    if (nlogR == 5 && sw.enc_x5 == 2)  // X5: 16 register rows + the exchanged fifth stage
-      ENC_COLS(4, true, 2, true, false, false, true);
-    else if (nlogR == 5)
+    // X5: 16 register rows + the exchanged fifth stage (10 VGPRs spilled at 3 waves / SIMD; the
+    // spill-free 2-wave build ran 3-4% slower, profiles/r06b)
+    if (nlogR == 5)
       ENC_COLS(4, true, 3, true, false, false, true);
     else if (vt)  // v's columns pass left to the blocks pass (enc_vtab sums)
       ENC_COLS(4, true, 3, true, false, true);
@@ -1861,10 +1858,10 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     if (t_split < p.L) launch_pp(t_split, p.L - t_split, true);
   } else if (nlogR > 0 && nblkLog == 11 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<11, 3, 3, 3, 2>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, twb, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nlogR > 0 && nblkLog == 12 && dt.red_ok)
     hipLaunchKernelGGL((ntt_fwd_blocks_enc_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbb), dim3(256), 0, s,
-                       pbuf, p.L, p.logN, twb, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
+                       pbuf, p.L, p.logN, dt.tw_fwd_blk, dt.tc, dk.pk, dk.pk_sh, ct, 0u, xg);
   else if (nblkLog > 11)
     hipLaunchKernelGGL(ntt_fwd_blocks_enc<8>, dim3((uint32_t)nbb), dim3(256), sizeof(uint64_t) << nblkLog, s,
                      pbuf, p.L, p.logN, (uint32_t)nlogR, dt.psi_rev, dt.psi_rev_sh, dt.tc, dk.pk,
@@ -2935,9 +2932,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);
   // c0 + c1*s formed in the first INTT pass (ntt_inv_blocks reading the ciphertexts); the
   // last pass fused with the CRT decode where its shape allows
-  const bool bl12 = p.logN == 16 && dt.tw_inv_blk12 && switches().dec_bl12;  // as launch_encrypt's
-  const uint32_t blkLog = bl12 ? 12u : ntt_block_log(p.logN);
-  const ulonglong2* twb = bl12 ? dt.tw_inv_blk12 : dt.tw_inv_blk;
+  const uint32_t blkLog = ntt_block_log(p.logN);
   const int logR = (int)(p.logN - blkLog);
   const size_t fuse_lds = (size_t)p.L * 64 * sizeof(uint64_t) << (logR > 0 ? logR : 0);
   const bool fuse = !exact && logR > 0 && fuse_lds <= kCrtFuseLds && p.gap <= 64 &&
@@ -2952,25 +2947,25 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
       const uint32_t pc = pp_per_combo(ncombo, K, 3);
       if (sum_in)
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, true>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else if (ntt_wave_local())
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false, true>), dim3(ncombo * pc), dim3(256), 0, s,
-                           dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
       else
         hipLaunchKernelGGL((ntt_inv_blocks_dec_pp<11, 2, 3, 3, 3, false>), dim3(ncombo * pc), dim3(256), 0, s, dbuf,
-                           p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
+                           p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, (uint32_t)K, pc, ct_L);
     } else if (logR > 0 && blkLog == 11 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 11 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<11, 2, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok && !sum_in)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else if (logR > 0 && blkLog == 12 && dt.red_ok)
       hipLaunchKernelGGL((ntt_inv_blocks_dec_ct<12, 3, 3, 3, 3, true>), dim3((uint32_t)nbBlocks), dim3(256), 0,
-                         s, dbuf, p.L, p.logN, twb, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
+                         s, dbuf, p.L, p.logN, dt.tw_inv_blk, dt.tc, ct, dk.sk, dk.sk_sh, xg, ct_L);
     else
       hipLaunchKernelGGL(ntt_inv_blocks, dim3((uint32_t)nbBlocks), dim3(256), sizeof(uint64_t) << blkLog,
                          s, dbuf, p.L, p.logN, blkLog, dt.ipsi_rev, dt.ipsi_rev_sh, dt.tc,

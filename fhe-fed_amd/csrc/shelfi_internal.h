@@ -71,10 +71,7 @@ struct Switches {
   bool enc_vt = true;          // SHELFI_ENC_VT=0: v's columns pass in enc_cols_fused, not enc_vtab sums
   int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
   bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
-  bool enc_bl12 = false;       // SHELFI_ENC_BL12=1: 2^16 encrypt over 2^12 blocks (16-row columns pass)
-  int enc_x5 = 1;              // SHELFI_ENC_X5=0: nlogR = 5 encrypt through enc_prep_kernel + three column
-                               // passes; 2: the exchanged-stage kernel at 2 waves / SIMD (1: 3 waves)
-  bool dec_bl12 = false;       // SHELFI_DEC_BL12=1: 2^16 decrypt over 2^12 blocks
+  bool enc_x5 = true;          // SHELFI_ENC_X5=0: nlogR = 5 encrypt through enc_prep_kernel + three column passes
   int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
   int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
   int pack_waves = 0;          // SHELFI_PACK_WAVES=2|8 (0: 4 rows per block)
@@ -157,10 +154,6 @@ struct DeviceTables {
   // (BL = ntt_block_log(logN), sstart = logN - BL, nb = 2^sstart)
   ulonglong2* tw_fwd_blk = nullptr;
   ulonglong2* tw_inv_blk = nullptr;
-  // N = 2^16 only (round 6): the same slices for 2^12-element blocks, so encrypt / decrypt can run a
-  // 16-row columns pass (nlogR = 4, the 2^15 kernels' shape) instead of 2^11 blocks and 32 rows
-  ulonglong2* tw_fwd_blk12 = nullptr;
-  ulonglong2* tw_inv_blk12 = nullptr;
   bool red_ok = false;  // every tower has TowerConst::red_ok (q >= 2^40): *_ct kernels usable
   double2* fft_inv = nullptr;       // [B] flat special-FFT twiddles (FFTSpecialInv)
   double2* fft_fwd = nullptr;       // [B] (FFTSpecial)

@@ -34,10 +34,7 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_XCD_ORDER", "0"),       # natural block order
     ("SHELFI_DEV_CHUNK_MIB", "16"),  # the call split into several launch chains
     ("SHELFI_ENC_TS", "0"),          # one column per thread over every tower (K = 7 defaults to one wave per tower)
-    ("SHELFI_ENC_BL12", "1"),        # 2^16: encrypt over 2^12 blocks (16-row columns pass; no-op at 2^15)
     ("SHELFI_ENC_X5", "0"),          # 2^16: enc_prep_kernel + three column passes (no-op at 2^15)
-    ("SHELFI_ENC_X5", "2"),          # 2^16: the exchanged-stage columns kernel at 2 waves / SIMD
-    ("SHELFI_DEC_BL12", "1"),        # 2^16: decrypt over 2^12 blocks (no-op at 2^15)
 ]
 WAVG_SWITCHES = [("SHELFI_WAVG_ROWS", "1"), ("SHELFI_WAVG_ROWS", "2")]
 SEED = 2024

@@ -1,4 +1,5 @@
 # Round 6: cfg4 (2^16 / L6) encrypt / decrypt with 2^11 (default) vs 2^12 blocks, K = 32 and 256, plus
+# (The SHELFI_ENC_BL12 / SHELFI_DEC_BL12 / SHELFI_DEC_XC switches and the SHELFI_ENC_X5=2 build were removed after these A/Bs: profiles/r06b.)
 # kernel stats of the 2^12 form: bash tools/ab_bl12.sh [tag]
 set -e
 cd /root/repo

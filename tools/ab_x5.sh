@@ -1,4 +1,5 @@
 # Round 6: cfg4 (2^16 / L6) encrypt: enc_prep + 3 column passes (X5=0) vs the exchanged-stage fused columns
+# (The SHELFI_ENC_BL12 / SHELFI_DEC_BL12 / SHELFI_DEC_XC switches and the SHELFI_ENC_X5=2 build were removed after these A/Bs: profiles/r06b.)
 # kernel at 3 (X5=1) / 2 (X5=2) waves per SIMD, K = 32 and 256; kernel stats of X5=1: bash tools/ab_x5.sh [tag]
 set -e
 cd /root/repo
