@@ -941,18 +941,22 @@ def main():
         "encrypt_hbm_frac": frac(enc_bytes, enc_ms),
         "decrypt_hbm_frac": frac(dec_bytes, dec_ms_per_ct),
     }
+    # the counter files are per parameter set: 2^15 / L4 (cfg2 / cfg3 / cfg5) in the named files, 2^16 / L6
+    # (cfg4, round 6) in their "_cfg4" siblings (tools/profile_cfg4_r06.sh, K = 32 as the steady loop here)
+    def wl_json(path):
+        return path if args.workload in ("cfg3", "cfg2", "cfg5") else path.replace(".json", "_%s.json" % args.workload)
+
     try:
-        with open(args.encdec_traffic_json) as f:
+        with open(wl_json(args.encdec_traffic_json)) as f:
             et = json.load(f)
-        if args.workload in ("cfg3", "cfg2", "cfg5"):  # 2^15 / L4: the parameters it was measured at
-            for name in ("encrypt", "decrypt", "decrypt_flooded"):
-                if name not in et:
-                    continue
-                res[name + "_traffic"] = {
-                    "hbm_bytes_per_ct": round(et[name]["hbm_bytes_per_ct"]),
-                    "algorithmic_bytes_per_ct": et["algorithmic_bytes_per_ct"],
-                    "over_algorithmic": round(et[name]["traffic_over_algorithmic"], 3),
-                    "source": os.path.relpath(args.encdec_traffic_json, ROOT)}
+        for name in ("encrypt", "decrypt", "decrypt_flooded"):
+            if name not in et:
+                continue
+            res[name + "_traffic"] = {
+                "hbm_bytes_per_ct": round(et[name]["hbm_bytes_per_ct"]),
+                "algorithmic_bytes_per_ct": et["algorithmic_bytes_per_ct"],
+                "over_algorithmic": round(et[name]["traffic_over_algorithmic"], 3),
+                "source": os.path.relpath(wl_json(args.encdec_traffic_json), ROOT)}
     except (OSError, ValueError, KeyError):
         pass
     # VALU roofline of the encrypt / decrypt chains (their bound): PMC
@@ -960,40 +964,38 @@ def main():
     # 4 cycles per SIMD (VOP3 integer ops incl. v_mad_u64_u32, tools/valu_rates.hip) at the
     # 2.4 GHz peak engine clock
     try:
-        with open(args.encdec_valu_json) as f:
+        with open(wl_json(args.encdec_valu_json)) as f:
             ev = json.load(f)
-        if args.workload in ("cfg3", "cfg2", "cfg5"):
-            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-            peak = simds * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST  # G wave-instructions / s
-            for name, ms in (("encrypt", enc_ms), ("decrypt", dec_ms_per_ct),
-                             ("decrypt_flooded", dec_flood_ms_per_ct)):
-                wi = ev[name]["wave_instr_per_ct"]
-                ach = wi / (ms * 1e-3) / 1e9
-                res[name + "_valu"] = {"bound": "valu", "wave_instr_per_ct": wi,
-                                       "achieved": round(ach, 1), "peak": round(peak, 1),
-                                       "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
-                                       "source": os.path.relpath(args.encdec_valu_json, ROOT)}
-                if "before_r02" in ev[name]:  # the round-2 code's count (profiles/encdec_valu_r02.json)
-                    res[name + "_valu"]["wave_instr_per_ct_r02"] = ev[name]["before_r02"]
+        simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        peak = simds * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST  # G wave-instructions / s
+        for name, ms in (("encrypt", enc_ms), ("decrypt", dec_ms_per_ct),
+                         ("decrypt_flooded", dec_flood_ms_per_ct)):
+            wi = ev[name]["wave_instr_per_ct"]
+            ach = wi / (ms * 1e-3) / 1e9
+            res[name + "_valu"] = {"bound": "valu", "wave_instr_per_ct": wi,
+                                   "achieved": round(ach, 1), "peak": round(peak, 1),
+                                   "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
+                                   "source": os.path.relpath(wl_json(args.encdec_valu_json), ROOT)}
+            if "before_r02" in ev[name]:  # the round-2 code's count (profiles/encdec_valu_r02.json)
+                res[name + "_valu"]["wave_instr_per_ct_r02"] = ev[name]["before_r02"]
     except (OSError, ValueError, KeyError):
         pass
     # effective clock of each chain's kernels in the steady loop (GRBM_GUI_ACTIVE / 8 / wall, the
     # chip holds ~2.1 GHz under these VALU-bound passes): the VALU fraction at that clock beside the
     # one at the 2.4 GHz peak
     try:
-        with open(args.encdec_clock_json) as f:
+        with open(wl_json(args.encdec_clock_json)) as f:
             ec = json.load(f)["chains"]
-        if args.workload in ("cfg3", "cfg2", "cfg5"):
-            for name, label in (("encrypt", "encrypt"), ("decrypt", "exact"), ("decrypt_flooded", "flooded")):
-                ks = ec[label]
-                us = sum(v["us"] for v in ks.values())
-                ghz = sum(v["us"] * v["ghz"] for v in ks.values()) / us  # time-weighted
-                clk = {"kernels_ghz": {k: v["ghz"] for k, v in ks.items()}, "time_weighted_ghz": round(ghz, 3),
-                       "source": os.path.relpath(args.encdec_clock_json, ROOT)}
-                if name + "_valu" in res:
-                    v = res[name + "_valu"]
-                    clk["valu_frac_at_this_clock"] = round(v["frac"] * VALU_CLOCK_GHZ / ghz, 3)
-                res[name + "_clock"] = clk
+        for name, label in (("encrypt", "encrypt"), ("decrypt", "exact"), ("decrypt_flooded", "flooded")):
+            ks = ec[label]
+            us = sum(v["us"] for v in ks.values())
+            ghz = sum(v["us"] * v["ghz"] for v in ks.values()) / us  # time-weighted
+            clk = {"kernels_ghz": {k: v["ghz"] for k, v in ks.items()}, "time_weighted_ghz": round(ghz, 3),
+                   "source": os.path.relpath(wl_json(args.encdec_clock_json), ROOT)}
+            if name + "_valu" in res:
+                v = res[name + "_valu"]
+                clk["valu_frac_at_this_clock"] = round(v["frac"] * VALU_CLOCK_GHZ / ghz, 3)
+            res[name + "_clock"] = clk
     except (OSError, ValueError, KeyError, ZeroDivisionError):
         pass
     if check:
