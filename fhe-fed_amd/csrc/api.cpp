@@ -759,6 +759,10 @@ int shelfi_ctx_create(uint32_t ring_dim, uint32_t num_towers, uint32_t scale_bit
     SHELFI_HIP(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
     SHELFI_HIP(hipMalloc(&ctx->dev_flag, 32));
     SHELFI_HIP(hipHostMalloc((void**)&ctx->host_flag, 32, hipHostMallocDefault));
+    // GenFlag words: pinned, mapped and coherent host memory the kernels store to (system scope)
+    SHELFI_HIP(hipHostMalloc((void**)&ctx->map_flag_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(ctx->map_flag_host, 0, 64);
+    SHELFI_HIP(hipHostGetDevicePointer((void**)&ctx->map_flag_dev, ctx->map_flag_host, 0));
     set_params(ctx, N, num_towers, scale_bits, first_mod_bits, batch, q, psi);
   });
   if (rc != SHELFI_OK) {
@@ -802,6 +806,8 @@ void shelfi_ctx_destroy(shelfi_ctx* ctx) {
     dfree_t(ctx->dev_flag);
     if (ctx->host_flag) (void)hipHostFree(ctx->host_flag);
     ctx->host_flag = nullptr;
+    if (ctx->map_flag_host) (void)hipHostFree(ctx->map_flag_host);
+    ctx->map_flag_host = ctx->map_flag_dev = nullptr;
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -1180,11 +1186,25 @@ struct StageRun {
   }
 };
 
+// A call's generation of the GenFlag words (shelfi_internal.h).  Every caller synchronises before the next
+// call starts, so no kernel writes the words while the host clears them at a wrap of the counter.
+static GenFlag next_gen_flag(shelfi_ctx* ctx) {
+  if (++ctx->map_gen == 0) {
+    std::memset(ctx->map_flag_host, 0, 64);
+    ctx->map_gen = 1;
+  }
+  return GenFlag{ctx->map_flag_dev, ctx->map_gen};
+}
+// after the call's synchronisation: did it raise word w?
+static bool gen_flag_raised(const shelfi_ctx* ctx, const GenFlag& f, int w) {
+  return __atomic_load_n(ctx->map_flag_host + w, __ATOMIC_ACQUIRE) == f.gen;
+}
+
 // The encode range flag of an encrypt call (kernels.hip enc_range_flag): non-finite values are refused;
 // a finite |x Delta| above 2^61 means the call is redone on the large-value path.
-static bool encode_needs_approx(uint32_t flag) {
-  if (flag & 2u) throw Error{SHELFI_ERR_RANGE, "encrypt: non-finite input value"};
-  return (flag & 1u) != 0;
+static bool encode_needs_approx(const shelfi_ctx* ctx, const GenFlag& f) {
+  if (gen_flag_raised(ctx, f, 1)) throw Error{SHELFI_ERR_RANGE, "encrypt: non-finite input value"};
+  return gen_flag_raised(ctx, f, 0);
 }
 
 // encode + encrypt n doubles (host) -> K ciphertext payloads written to out_payload (approx: every
@@ -1207,7 +1227,7 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
   Pipe pp(ctx);
   StageRun sr(stager(ctx));
   std::vector<HostPiece> pcs;
-  SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, pp.b));
+  const GenFlag fl = next_gen_flag(ctx);
   const uint64_t nchunks = (K + kc - 1) / kc;
   for (uint64_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
@@ -1223,7 +1243,7 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
                             g0 + k0, pp.b);
     else
       launch_encrypt(p, ctx->dt, ctx->dk, (const double*)xb[b], xn, kn, (uint64_t*)cb[b], scratch, key,
-                     g0 + k0, ctx->dev_flag, pp.b);
+                     g0 + k0, fl, pp.b);
     if (dst.packed)  // canonical residues: the residue check cannot fire
       launch_blob_pack((const uint64_t*)cb[b], kn, p.L, p.logN, ap, ctx->dt.tc, (uint32_t*)pb[b],
                        ctx->dev_flag + 5, pp.b);
@@ -1234,10 +1254,9 @@ static void encrypt_bytes_pipeline(shelfi_ctx* ctx, const double* x, size_t n, u
     SHELFI_HIP(hipEventRecord(pp.out_free[b], pp.c));
     sr.s.poll();
   }
-  SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, pp.b));  // pinned
   sr.finish();
   pp.sync();
-  if (!approx && encode_needs_approx(ctx->host_flag[0]))
+  if (!approx && encode_needs_approx(ctx, fl))
     encrypt_bytes_pipeline(ctx, x, n, K, dst, key, g0, true);
 }
 
@@ -1738,6 +1757,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     advise_huge(out, n * 8);
     DecodeNoise dn = decode_noise_begin(ctx, K, ctx->stream2);
     const uint64_t g0 = dn.g0;
+    const GenFlag fl = next_gen_flag(ctx);
     // one pipelined pass over the call: the decode's tower prefix (decode_towers: only those towers
     // are uploaded) with the fast CRT, or (exact) every tower through crt_exact_kernel
     const auto run = [&](bool exact) {
@@ -1759,7 +1779,6 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, decrypt_scratch_bytes(pd, kc));
       Pipe pp(ctx);
       StageRun sr(stager(ctx));
-      if (!exact) SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, pp.b));
       dn.g0 = g0;
       dn.reset = 1;
       std::vector<HostPiece> pcs;
@@ -1777,7 +1796,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
         if (ci >= 2) SHELFI_HIP(hipStreamWaitEvent(pp.b, pp.out_free[b], 0));
         dn.g0 += (ci ? kc : 0);
         launch_decrypt(pd, dtd, ctx->dk, (const uint64_t*)cb[b], kn, h.scale, on, (double*)ob[b],
-                       scratch, pp.b, &dn, false, 0, ctx->dev_flag + 7, exact);
+                       scratch, pp.b, &dn, false, 0, fl, exact);
         dn.reset = 0;
         SHELFI_HIP(hipEventRecord(pp.computed[b], pp.b));
         SHELFI_HIP(hipStreamWaitEvent(pp.c, pp.computed[b], 0));
@@ -1786,8 +1805,6 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
         sr.s.poll();
       }
       decode_noise_readback(ctx, dn, pp.b);
-      if (!exact)  // pinned, before the one synchronisation
-        SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, pp.b));
       sr.finish();
       pp.sync();
     };
@@ -1795,7 +1812,7 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
       run(true);
     else {
       run(false);
-      if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
+      if (gen_flag_raised(ctx, fl, 2)) run(true);  // a value outside the fast CRT's range: the call again, exactly
     }
     decode_noise_end(ctx, dn);
   });
@@ -2276,7 +2293,7 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
     draw_key(ctx, K, key, &g0);
     const uint64_t kc_max = dev_chunk(K, encrypt_scratch_bytes(p, 1));
     void* scratch = ensure(ctx->scratch, ctx->scratch_bytes, encrypt_scratch_bytes(p, kc_max));
-    SHELFI_HIP(hipMemsetAsync(ctx->dev_flag, 0, 4, s));
+    const GenFlag fl = next_gen_flag(ctx);
     const size_t ct_words = 2ull * p.L * p.N;
     bool approx = false;
     for (int pass = 0; pass < 2; ++pass) {
@@ -2288,14 +2305,13 @@ int shelfi_dev_encrypt(shelfi_ctx* ctx, const double* x_dev, size_t n, uint64_t*
                                 g0 + k0, s);
         else
           launch_encrypt(p, ctx->dt, ctx->dk, x_dev + xs, xn, kc, ct_dev + k0 * ct_words, scratch,
-                         key, g0 + k0, ctx->dev_flag, s);
+                         key, g0 + k0, fl, s);
       }
       if (approx) break;
-      SHELFI_HIP(hipMemcpyAsync(ctx->host_flag, ctx->dev_flag, 4, hipMemcpyDeviceToHost, s));  // pinned
       SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
       bool redo;
       try {
-        redo = encode_needs_approx(ctx->host_flag[0]);
+        redo = encode_needs_approx(ctx, fl);
       } catch (...) {
         std::memset(key, 0, sizeof(key));
         throw;
@@ -2324,6 +2340,7 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
     const size_t ct_words = 2ull * towers * ctx->p.N;
     DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
     const uint64_t g0 = dn.g0;
+    const GenFlag fl = next_gen_flag(ctx);
     // one pass over the call: the decode's tower prefix with the fast CRT, or (exact) every tower
     // through crt_exact_kernel
     const auto run = [&](bool exact) {
@@ -2338,7 +2355,7 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
         const uint64_t o0 = k0 * p.batch, on = std::min<uint64_t>(n - o0, kc * p.batch);
         dn.g0 = g0 + k0;
         launch_decrypt(p, dt, ctx->dk, ct_dev + k0 * ct_words, kc, scale, on, out_dev + o0, scratch, s, &dn,
-                       sum_in, towers, ctx->dev_flag + 7, exact);
+                       sum_in, towers, fl, exact);
         dn.reset = 0;  // the flags are reset by the first chunk's flooding only
       }
       decode_noise_readback(ctx, dn, s);
@@ -2346,11 +2363,9 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
     if (ctx->decode_exact) {
       run(true);
     } else {
-      SHELFI_HIP(hipMemsetAsync(ctx->dev_flag + 7, 0, 4, s));
       run(false);
-      SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 7, ctx->dev_flag + 7, 4, hipMemcpyDeviceToHost, s));  // pinned
       SHELFI_HIP(hipStreamSynchronize(s));
-      if (ctx->host_flag[7]) run(true);  // a value outside the fast CRT's range: the whole call again, exactly
+      if (gen_flag_raised(ctx, fl, 2)) run(true);  // a value outside the fast CRT's range: the call again, exactly
     }
     SHELFI_HIP(hipStreamSynchronize(s));  // scratch is reused by the next call
     decode_noise_end(ctx, dn);

@@ -1262,9 +1262,15 @@ __device__ __forceinline__ void load_cdt32(const uint64_t* __restrict__ cdt, int
   }
 }
 
-// Encode's range flag (dev_flag[0]): bit 0 = a finite |x Delta| above 2^61 (the call is redone on the
-// large-value path, launch_encrypt_approx), bit 1 = a non-finite value (refused).
-__device__ __forceinline__ uint32_t enc_range_flag(double val) { return isfinite(val) ? 1u : 2u; }
+// Encode's range flag (GenFlag words): [0] = a |x Delta| above 2^61 (a finite one: the call is redone on
+// the large-value path, launch_encrypt_approx), [1] = a non-finite value (refused).
+__device__ __forceinline__ void gen_flag_set(GenFlag f, int word) {
+  __hip_atomic_store(f.p + word, f.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void enc_range_flag(GenFlag f, double val) {
+  gen_flag_set(f, 0);
+  if (!isfinite(val)) gen_flag_set(f, 1);
+}
 
 __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict__ fbuf,
                                                        uint64_t K, uint32_t logN, uint32_t logS,
@@ -1273,7 +1279,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
                                                        Key8 key, uint64_t g0,
                                                        int64_t* __restrict__ me0,
                                                        int16_t* __restrict__ ve,
-                                                       uint32_t* __restrict__ flag) {
+                                                       GenFlag flag) {
   const uint32_t N = 1u << logN, S = 1u << logS, N16 = N >> 4, V0 = N >> 6;
   __shared__ uint32_t thi[64], tlo[64];
   load_cdt32(cdt, T, thi, tlo);
@@ -1301,7 +1307,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const double2* __restrict
     if ((jj & ((1u << gapLog) - 1)) == 0) {
       const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
       const double val = __dmul_rn(__ddiv_rn(j < half ? cv.x : cv.y, dS), delta);
-      if (!(fabs(val) <= lim)) atomicOr(flag, enc_range_flag(val));
+      if (!(fabs(val) <= lim)) enc_range_flag(flag, val);
       m = round_half_away(val);
     }
     me0[(k << logN) + j] = m + gauss32(w[i], thi, tlo, [&] { return chacha20_word(key, V0 + 2 * N16 + h, nonce, i); });
@@ -1412,7 +1418,7 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
                                                       const uint64_t* __restrict__ tw,
                                                       const uint64_t* __restrict__ twp,
                                                       uint64_t* __restrict__ out,
-                                                      uint32_t* __restrict__ flag, uint32_t t_split,
+                                                      GenFlag flag, uint32_t t_split,
                                                       const uint64_t* __restrict__ enc_tab) {
   constexpr int R = 1 << LOGR, IS = 16 / R, G = R / 4;
   constexpr int NTW = TS ? 4 : 1;  // towers with their own LDS tables in one workgroup
@@ -1647,7 +1653,10 @@ __global__ __launch_bounds__(256, TS ? 2 : WV) void enc_cols_fused(const double2
         const double2 cv = fbuf[k * S + bitrev_dev(jj >> gapLog, logS)];
         const double vr = __dmul_rn(__dmul_rn(cv.x, invS), delta);
         const double vi = __dmul_rn(__dmul_rn(cv.y, invS), delta);
-        if (!(fabs(vr) <= lim) || !(fabs(vi) <= lim)) atomicOr(flag, enc_range_flag(vr) | enc_range_flag(vi));
+        if (!(fabs(vr) <= lim) || !(fabs(vi) <= lim)) {
+          gen_flag_set(flag, 0);
+          if (!isfinite(vr) || !isfinite(vi)) gen_flag_set(flag, 1);
+        }
         mre = round_half_away(vr);
         mim = round_half_away(vi);
       }
@@ -1740,7 +1749,7 @@ static void launch_encode_fft(const Params& p, const DeviceTables& dt, const dou
 
 void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
                     uint64_t n, uint64_t K, uint64_t* ct, void* scratch, const uint32_t key[8],
-                    uint64_t g0, uint32_t* flag, hipStream_t s) {
+                    uint64_t g0, GenFlag flag, hipStream_t s) {
   if (!K) return;
   const uint32_t logS = __builtin_ctz(p.batch);
   double2* fbuf = reinterpret_cast<double2*>(scratch);
@@ -2231,7 +2240,7 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
                                                          const uint32_t* __restrict__ mw,
                                                          double inv_scale,
                                                          double2* __restrict__ fbuf,
-                                                         uint32_t* __restrict__ wide_flag) {
+                                                         GenFlag wide_flag) {
   const uint32_t N = 1u << logN, S = 1u << logS;
   // S >= 256: a block owns the 256 slots i = hi.2^(logS-4) | mid.16 | lo (hi, lo < 16) of one
   // middle value, so the tower reads (16 consecutive i) and, after a transpose through LDS,
@@ -2265,7 +2274,7 @@ __global__ __launch_bounds__(256) void crt_decode_kernel(const uint64_t* __restr
     else
       res[part] = crt_value<NC>(yf, L, tcs, inv_scale, wide);
   }
-  if (wide) atomicOr(wide_flag, 1u);
+  if (wide) gen_flag_set(wide_flag, 2);
   if (!tiled) {
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
     return;
@@ -2299,7 +2308,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
                                                         const uint64_t* __restrict__ twp,
                                                         const TowerConst* __restrict__ tcs, double inv_scale,
                                                         double2* __restrict__ fbuf,
-                                                        uint32_t* __restrict__ wide_flag) {
+                                                        GenFlag wide_flag) {
   constexpr int R = 1 << LOGR, CW = 64, CWP = 64;
   extern __shared__ uint64_t ys_flat[];  // [L][R][CWP]
   uint64_t(*ys)[R][CWP] = reinterpret_cast<uint64_t(*)[R][CWP]>(ys_flat);
@@ -2365,7 +2374,7 @@ __global__ __launch_bounds__(256) void ntt_inv_cols_crt(const uint64_t* __restri
     const uint32_t i = (col + BLK * r) >> gapLog;
     fbuf[k * S + bitrev_dev(i, logS)] = make_double2(res[0], res[1]);
   }
-  if (wide) atomicOr(wide_flag, 1u);
+  if (wide) gen_flag_set(wide_flag, 2);
 }
 
 // ------------------------------------------------- decode noise flooding ----
@@ -2920,13 +2929,13 @@ size_t decrypt_scratch_bytes(const Params& p, uint64_t K) {
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
                     void* scratch, hipStream_t s, const DecodeNoise* dn, bool sum_in, uint32_t ct_L,
-                    uint32_t* crt_flag, bool exact) {
+                    GenFlag crt_flag, bool exact) {
   if (!K) return;
   if (!ct_L) ct_L = p.L;
   if (ct_L < p.L) throw Error{SHELFI_ERR_ARG, "decrypt: fewer ciphertext towers than decoded towers"};
   exact = exact || dt.crt_nc == 0;  // towers too wide for crt_value's columns: always exact
   if (exact && !dt.crt_mw) throw Error{SHELFI_ERR_STATE, "decrypt: no exact CRT table for these towers"};
-  if (!exact && !crt_flag) throw Error{SHELFI_ERR_STATE, "decrypt: the fast CRT needs a range flag"};
+  if (!exact && !crt_flag.p) throw Error{SHELFI_ERR_STATE, "decrypt: the fast CRT needs a range flag"};
   const uint32_t logS = __builtin_ctz(p.batch);
   uint64_t* dbuf = reinterpret_cast<uint64_t*>(scratch);
   double2* fbuf = reinterpret_cast<double2*>(dbuf + K * (uint64_t)p.L * p.N);

@@ -233,11 +233,14 @@ struct shelfi_ctx {
   uint64_t seed = 0;          // 0 -> OS entropy per call
   uint64_t enc_counter = 0;   // global ciphertext index for the sampler stream
   uint32_t* host_flag = nullptr; // pinned host mirror of dev_flag (async readback before one sync)
-  uint32_t* dev_flag = nullptr;  // device flags: [0] encode range, [1] decode precision,
+  uint32_t* map_flag_host = nullptr;  // GenFlag words in pinned host memory (encode range, decode CRT range)
+  uint32_t* map_flag_dev = nullptr;   // the same words as the device addresses them
+  uint32_t map_gen = 0;               // the last call generation handed out (never 0)
+  uint32_t* dev_flag = nullptr;  // device flags: [0] encode range (before round 6), [1] decode precision,
                                  // [2] max decode logError (noise flooding), [3] bytes-API
                                  // upload residue >= q, [4] arena upload residue >= q, [5] the
                                  // packed wire's pack check, [6] shelfi_dev_check_residues,
-                                 // [7] decode CRT value outside the fast path's range (redo exact)
+                                 // (round 6: the encode and decode-CRT range flags are GenFlag words)
   // arena slots whose last upload was refused (shelfi_dev_arena_put*): an aggregation
   // over an arena range holding one fails instead of summing the refused residues
   // (an entry names the arena by its base, its shelfi_arena_words(C, K) span and C, so a later
@@ -341,9 +344,19 @@ void launch_ntt(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inv
                 const DeviceTables& dt, hipStream_t s);
 void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, bool inverse,
                      const DeviceTables& dt, hipStream_t s);
+// A flag in pinned host memory the kernels write directly (round 6): word i holds the generation of the
+// last call that raised it, so a call compares it with its own generation after its one synchronisation --
+// no reset before a call and no readback copy after it (each was a ~2-4 us copy-engine op plus its launch
+// gap on every device encrypt / decrypt).  Words: [0] an encode value out of the fast range, [1] a
+// non-finite one, [2] a decode coefficient outside the fast CRT's range.  Written with system-scope
+// stores; p == nullptr: no flag.
+struct GenFlag {
+  uint32_t* p = nullptr;
+  uint32_t gen = 0;
+};
 void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
                     const double* x, uint64_t n, uint64_t K, uint64_t* ct, void* scratch,
-                    const uint32_t key[8], uint64_t g0, uint32_t* flag, hipStream_t s);
+                    const uint32_t key[8], uint64_t g0, GenFlag flag, hipStream_t s);
 // encode's large-value path (|x Delta| > 2^61 somewhere in the call; PALISADE's approxFactor): the
 // same ciphertexts' encryption redone with per-ciphertext scale-down exponents (kernels.hip)
 void launch_encrypt_approx(const Params& p, const DeviceTables& dt, const DeviceKeys& dk, const double* x,
@@ -364,8 +377,8 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
                     const uint64_t* ct, uint64_t K, double scale, uint64_t n, double* out,
                     void* scratch, hipStream_t s, const DecodeNoise* dn = nullptr, bool sum_in = false,
                     uint32_t ct_L = 0,  // ct_L: towers of the ciphertexts (0 = p.L; >= p.L)
-                    uint32_t* crt_flag = nullptr, bool exact = false);
-// crt_flag: the fast CRT (crt_value) sets *crt_flag = 1 when a coefficient's centred value is not
+                    GenFlag crt_flag = GenFlag{}, bool exact = false);
+// crt_flag: the fast CRT (crt_value) sets word 2 to crt_flag.gen when a coefficient's centred value is not
 // in (-2^127, 2^127) over these towers -- the caller redoes the call with every tower and exact =
 // true (crt_exact_kernel, any |X| <= (Q - 1) / 2).  A fast-path launch needs crt_flag.
 size_t decrypt_scratch_bytes(const Params& p, uint64_t K);
