@@ -1667,25 +1667,24 @@ int shelfi_weighted_average(shelfi_ctx* ctx, const uint8_t* const* blobs, const 
 
 // Noise-flooding setup for one decrypt of K ciphertexts (enabled by
 // shelfi_set_decode_noise); its randomness comes from the ctx stream like encrypt's.
-static DecodeNoise decode_noise_begin(shelfi_ctx* ctx, uint64_t K, hipStream_t s) {
+static DecodeNoise decode_noise_begin(shelfi_ctx* ctx, uint64_t K, const GenFlag& fl) {
   DecodeNoise dn;
   if (!ctx->decode_noise) return dn;
+  dn.fail = fl;
   dn.enabled = 1;
   dn.m_factor = ctx->decode_m_factor;
   dn.p_bits = ctx->p.scale_bits;
   draw_key(ctx, K, dn.key, &dn.g0);
   dn.flags = ctx->dev_flag;
-  // flags [1], [2] are reset by the first chunk's flooding (launch_decrypt: inside
+  // flag [2] (logError) is reset by the first chunk's flooding (launch_decrypt: inside
   // decode_stats_kernel, or a fill before the small-ring decode_flood_kernel)
-  (void)s;
   return dn;
 }
 
-// Enqueue the flags' readback into pinned host memory on `s`, before the caller's one stream
-// synchronisation (a synchronous pageable hipMemcpy after it cost a second round trip per call).
-static void decode_noise_readback(shelfi_ctx* ctx, const DecodeNoise& dn, hipStream_t s) {
-  if (!dn.enabled) return;
-  SHELFI_HIP(hipMemcpyAsync(ctx->host_flag + 1, ctx->dev_flag + 1, 8, hipMemcpyDeviceToHost, s));
+// After a flooded decrypt was enqueued: its logError (device flag [2]) is read back only when asked for
+// (shelfi_decode_log_error), not after every call; the precision failure is a GenFlag word (round 6).
+static void decode_noise_readback(shelfi_ctx* ctx, const DecodeNoise& dn, hipStream_t) {
+  if (dn.enabled) ctx->log_error_pending = true;
 }
 
 // After the decrypt's stream work has completed: record logError, raise PALISADE's
@@ -1693,9 +1692,7 @@ static void decode_noise_readback(shelfi_ctx* ctx, const DecodeNoise& dn, hipStr
 static void decode_noise_end(shelfi_ctx* ctx, DecodeNoise& dn) {
   if (!dn.enabled) return;
   std::memset(dn.key, 0, sizeof(dn.key));
-  const uint32_t f[2] = {ctx->host_flag[1], ctx->host_flag[2]};  // decode_noise_readback, synchronised
-  ctx->last_log_error = (int)f[1];
-  if (f[0])
+  if (gen_flag_raised(ctx, dn.fail, 3))
     throw Error{SHELFI_ERR_PRECISION,
                 "The decryption failed because the approximation error is too high. Check the "
                 "parameters."};
@@ -1719,8 +1716,15 @@ int shelfi_set_decode_exact(shelfi_ctx* ctx, int exact) {
 int shelfi_decode_log_error(shelfi_ctx* ctx, int* log_error) {
   if (!ctx || !log_error) return SHELFI_ERR_ARG;
   std::lock_guard<std::mutex> lk(ctx_mutex(ctx));
-  *log_error = ctx->last_log_error;
-  return SHELFI_OK;
+  return guarded([&] {
+    if (ctx->log_error_pending) {  // the last flooded decrypt's, read now (every call has synchronised)
+      DeviceGuard g(ctx->device);
+      SHELFI_HIP(hipMemcpy(ctx->host_flag + 2, ctx->dev_flag + 2, 4, hipMemcpyDeviceToHost));
+      ctx->last_log_error = (int)ctx->host_flag[2];
+      ctx->log_error_pending = false;
+    }
+    *log_error = ctx->last_log_error;
+  });
 }
 
 // Towers the decode's fast path reads: the shortest prefix of q_0 .. q_{towers-1} whose product
@@ -1755,9 +1759,9 @@ int shelfi_decrypt(shelfi_ctx* ctx, const uint8_t* blob, size_t len, size_t n, d
     // ckks.cpp:192-196: ciphertext i contributes min(batch, n - i*batch) values
     const uint64_t K = (n + p.batch - 1) / p.batch;
     advise_huge(out, n * 8);
-    DecodeNoise dn = decode_noise_begin(ctx, K, ctx->stream2);
-    const uint64_t g0 = dn.g0;
     const GenFlag fl = next_gen_flag(ctx);
+    DecodeNoise dn = decode_noise_begin(ctx, K, fl);
+    const uint64_t g0 = dn.g0;
     // one pipelined pass over the call: the decode's tower prefix (decode_towers: only those towers
     // are uploaded) with the fast CRT, or (exact) every tower through crt_exact_kernel
     const auto run = [&](bool exact) {
@@ -2338,9 +2342,9 @@ static int dev_decrypt(shelfi_ctx* ctx, const uint64_t* ct_dev, size_t K, uint32
     const uint64_t Kn = (n + ctx->p.batch - 1) / ctx->p.batch;
     if (!Kn) return;
     const size_t ct_words = 2ull * towers * ctx->p.N;
-    DecodeNoise dn = decode_noise_begin(ctx, Kn, s);
-    const uint64_t g0 = dn.g0;
     const GenFlag fl = next_gen_flag(ctx);
+    DecodeNoise dn = decode_noise_begin(ctx, Kn, fl);
+    const uint64_t g0 = dn.g0;
     // one pass over the call: the decode's tower prefix with the fast CRT, or (exact) every tower
     // through crt_exact_kernel
     const auto run = [&](bool exact) {

@@ -2430,7 +2430,7 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
                                                             uint32_t logN, double two_p,
                                                             double p_bits, double m_factor,
                                                             Key8 key, uint64_t g0,
-                                                            uint32_t* __restrict__ flags) {
+                                                            uint32_t* __restrict__ flags, GenFlag fail) {
   __shared__ double red[17];
   const uint32_t S = 1u << logS, half = S >> 1;
   double2* __restrict__ f = fbuf + (uint64_t)blockIdx.x * S;
@@ -2473,7 +2473,7 @@ __global__ __launch_bounds__(1024) void decode_flood_kernel(double2* __restrict_
   double sigma_p = sigma * two_p;  // PALISADE works at scale 2^p
   const double logstd = log2(sigma_p);
   if (!(logstd <= p_bits - 5.0)) {
-    if (threadIdx.x == 0) atomicOr(&flags[1], 1u);  // decode precision failure
+    if (threadIdx.x == 0) gen_flag_set(fail, 3);  // decode precision failure
   }
   const double floor_sd = 0.125 * sqrt((double)(1u << logN));
   if (sigma_p < floor_sd) sigma_p = floor_sd;
@@ -2578,7 +2578,8 @@ struct FloodArgs {
   double two_p, p_bits, m_factor;
   Key8 key;
   uint64_t g0;
-  uint32_t* flags;  // [1] |= precision failure, [2] = max logError
+  uint32_t* flags;  // [2] = max logError
+  GenFlag fail;     // word 3: precision failure
 };
 
 // Ciphertext k's flooding scale from decode_stats_kernel's partial sums: the noise's standard
@@ -2592,7 +2593,7 @@ __device__ __forceinline__ double flood_nsd_sums(const FloodArgs& fa, double s1,
   if (sigma_p < floor_sd) sigma_p = floor_sd;
   const double stddev_p = sqrt(fa.m_factor + 1.0) * sigma_p;
   if (b == 0 && threadIdx.x == 0) {
-    if (fail) atomicOr(&fa.flags[1], 1u);
+    if (fail) gen_flag_set(fa.fail, 3);
     atomicMax((int*)&fa.flags[2], (int)rint(log2(stddev_p * sqrt(2.0 * (double)S))));
   }
   return stddev_p / fa.two_p;
@@ -3034,6 +3035,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     fa.m_factor = dn->m_factor;
     fa.g0 = dn->g0;
     fa.flags = dn->flags;
+    fa.fail = dn->fail;
     fa.logN = p.logN;
     fused_flood = p.batch >= 64;  // decode_flood_kernel below 2^6 slots
     if (fused_flood && whole) {  // fft_fwd_whole<true> sums its own statistics
@@ -3047,7 +3049,7 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     } else {
       if (dn->reset) SHELFI_HIP(hipMemsetAsync(dn->flags + 1, 0, 8, s));
       hipLaunchKernelGGL(decode_flood_kernel, dim3((uint32_t)K), dim3(1024), 0, s, fbuf, logS, p.logN,
-                         fa.two_p, fa.p_bits, fa.m_factor, fa.key, fa.g0, fa.flags);
+                         fa.two_p, fa.p_bits, fa.m_factor, fa.key, fa.g0, fa.flags, fa.fail);
     }
     SHELFI_HIP(hipGetLastError());
   }

@@ -257,6 +257,7 @@ struct shelfi_ctx {
   double decode_m_factor = 1.0;
   int decode_exact = 0;          // shelfi_set_decode_exact: every decrypt over every tower, exact CRT
   int last_log_error = -1;       // of the last flooded decrypt, -1 if none
+  bool log_error_pending = false;  // dev_flag[2] holds a newer one, read on demand (shelfi_decode_log_error)
   std::string pal_ctx_obj;       // PALISADE keys: embedded context object (§8 f1)
   std::string pal_keytag;        // PALISADE keys: key tag
   int wire = 0;                  // encrypt output: 0 blob, 1 PALISADE archive
@@ -348,7 +349,8 @@ void launch_ntt_cols(uint64_t* polys, uint64_t P, uint32_t L, uint32_t logN, boo
 // last call that raised it, so a call compares it with its own generation after its one synchronisation --
 // no reset before a call and no readback copy after it (each was a ~2-4 us copy-engine op plus its launch
 // gap on every device encrypt / decrypt).  Words: [0] an encode value out of the fast range, [1] a
-// non-finite one, [2] a decode coefficient outside the fast CRT's range.  Written with system-scope
+// non-finite one, [2] a decode coefficient outside the fast CRT's range, [3] a flooded decode's precision
+// failure.  Written with system-scope
 // stores; p == nullptr: no flag.
 struct GenFlag {
   uint32_t* p = nullptr;
@@ -370,7 +372,8 @@ struct DecodeNoise {
   uint32_t p_bits = 52;    // PALISADE plaintext modulus of CKKS = scale bits
   uint32_t key[8] = {};    // ChaCha20 key, nonce (3 << 56) | (g0 + ciphertext)
   uint64_t g0 = 0;
-  uint32_t* flags = nullptr;  // device: [1] |= precision failure, [2] = max logError
+  uint32_t* flags = nullptr;  // device: [2] = max logError
+  GenFlag fail;               // word 3: the precision failure (PALISADE's Decode throws)
   int reset = 1;              // the launch's flooding resets flags [1], [2] first (a call's first chunk)
 };
 void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& dk,
