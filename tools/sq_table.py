@@ -11,11 +11,11 @@ def main():
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(sys.argv[1])):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "probe::").split("(")[0]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     for k, d in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
-        if not k.startswith("shelfi"):
+        if not k.startswith(("shelfi", "probe")):
             continue
         n = len(disp[k])
         wc = d.get("SQ_WAVE_CYCLES", 0.0)
