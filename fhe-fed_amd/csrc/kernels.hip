@@ -1120,6 +1120,12 @@ constexpr uint32_t kFftWholeLogS = 14;
 // the whole-vector kernels win, 2.93 vs 2.97 and 0.99 vs 1.03 (profiles/r05zc/small_k.txt)
 constexpr uint64_t kFftWholeMinK = 128;
 constexpr uint64_t kEncNoredMinK = 192;  // launch_encrypt: the NORED tower split from this many ciphertexts
+// launch_decrypt: the persistent first INTT pass (ntt_inv_blocks_dec_pp) from this many (ciphertext, decode
+// tower, 2^11 block) items, the one-shot ntt_inv_blocks_dec_ct below.  Decrypt / flooded us/ct, one-shot vs
+// persistent (profiles/r06f/dpk_*, ppk_*): 2^15 / 3 decode towers K = 4 9.96 / 12.53 vs 10.37 / 13.07, K = 64
+// (3,072 items) 1.52 / 1.75 vs 1.55 / 1.82, K = 96 (4,608) 1.53 / 1.67 vs 1.43 / 1.55; 2^16 K = 32 (3,072)
+// 3.17-3.28 / 3.59-3.70 vs 3.30 / 3.73, K = 64 (6,144) 3.00 / 3.19 vs 2.76-2.84 / 2.92
+constexpr uint64_t kDecPpMinItems = 4096;
 constexpr uint32_t kFftWholeRow = 1088;  // doubles per 1024-element block slice (the largest padding, 1087)
 __device__ __forceinline__ uint32_t fft_wpad(uint32_t e) { return e + (e >> 5); }
 __device__ __forceinline__ uint32_t fft_wt1(uint32_t l, int m) { return 4 * l + (l >> 3) + 264u * (m >> 2) + (m & 3); }
@@ -2951,7 +2957,10 @@ void launch_decrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
     const uint64_t P = K * p.L, nbBlocks = P << logR, nbCols = P * ((p.N >> logR) / 256);
     if (nbBlocks > 0x7FFFFFFFull) throw Error{SHELFI_ERR_ARG, "decrypt batch too large"};
     const uint32_t xg = xcd_combos(p.L << (logR > 0 ? logR : 0));
-    const bool pp = logR > 0 && blkLog == 11 && dt.red_ok && switches().dec_pp;
+    // the persistent pass from kDecPpMinItems (ciphertext, tower, block) items: below, its per-workgroup
+    // prologue is not amortised and the one-shot pass is faster (same dbuf bits)
+    const bool pp = logR > 0 && blkLog == 11 && dt.red_ok && switches().dec_pp &&
+                    K * ((uint64_t)p.L << logR) >= kDecPpMinItems;
     if (pp) {
       const uint32_t ncombo = p.L << logR;
       const uint32_t pc = pp_per_combo(ncombo, K, 3);

@@ -25,7 +25,7 @@ ENC_DEC_SWITCHES = [
     ("SHELFI_FFT_CT", "0"),          # LDS-loop FFT block passes
     ("SHELFI_FFT_WHOLE", "0"),       # no-op at K = 7 (whole-vector FFTs from K = 128: test_large_batch_paths_...)
     ("SHELFI_ENC_PP", "0"),          # one-shot encrypt block pass
-    ("SHELFI_DEC_PP", "0"),          # one-shot decrypt block pass
+    ("SHELFI_DEC_PP", "0"),          # no-op at K = 7 (the persistent decrypt pass from 4,096 items: test_large_batch_...)
     ("SHELFI_ENC_NORED", "0"),       # no-op at K = 7 (the NORED split from K = 192: test_large_batch_paths_...)
     ("SHELFI_ENC_TAB", "0"),         # butterflies instead of the small-polynomial tables
     ("SHELFI_ENC_VT", "0"),          # v's columns pass in enc_cols_fused, not table sums in the blocks pass
@@ -119,12 +119,14 @@ def test_bytes_wavg_chunking_bitexact(ctx, monkeypatch, wire, mode):
 
 
 def test_large_batch_paths_match_small_batch_paths(tmp_path, monkeypatch):
-    """Two choices depend on the batch: the whole-vector encode / decode FFTs (fft_inv_whole,
-    fft_fwd_whole<flag>) run from kFftWholeMinK = 128 ciphertexts at 2^14 slots, and the encrypt's NORED tower
-    split (two blocks-pass launches) from kEncNoredMinK = 192.  200 ciphertexts through the large-batch paths,
-    through the multi-pass FFTs (SHELFI_FFT_WHOLE=0) and through one all-reduced blocks pass
-    (SHELFI_ENC_NORED=0) give the same ciphertexts and the same exact and flooded decodes, bit for bit (the
-    small-batch chains are pinned against the oracle in test_gpu_parity / test_gpu_decode_noise)."""
+    """Three choices depend on the batch: the whole-vector encode / decode FFTs (fft_inv_whole,
+    fft_fwd_whole<flag>) run from kFftWholeMinK = 128 ciphertexts at 2^14 slots, the encrypt's NORED tower
+    split (two blocks-pass launches) from kEncNoredMinK = 192, and decrypt's persistent first INTT pass from
+    kDecPpMinItems = 4,096 (ciphertext, tower, block) items (200 x 3 x 16 = 9,600 here, with uneven tails).
+    200 ciphertexts through the large-batch paths, through the multi-pass FFTs (SHELFI_FFT_WHOLE=0), through
+    one all-reduced blocks pass (SHELFI_ENC_NORED=0) and through the one-shot decrypt pass (SHELFI_DEC_PP=0)
+    give the same ciphertexts and the same exact and flooded decodes, bit for bit (the small-batch chains are
+    pinned against the oracle in test_gpu_parity / test_gpu_decode_noise)."""
     d = str(tmp_path) + os.sep
     ck = m.CKKS("ckks", 16384, 52, d, multDepth=3, seed=5, decodeNoise=False)
     assert ck.genCryptoContextAndKeyGen() == 1
@@ -146,7 +148,7 @@ def test_large_batch_paths_match_small_batch_paths(tmp_path, monkeypatch):
         return ct, dec, fl
 
     ct1, dec1, fl1 = run()
-    for var in ("SHELFI_FFT_WHOLE", "SHELFI_ENC_NORED"):
+    for var in ("SHELFI_FFT_WHOLE", "SHELFI_ENC_NORED", "SHELFI_DEC_PP"):
         set_switch(monkeypatch, var, "0")
         ct0, dec0, fl0 = run()
         assert torch.equal(ct1, ct0), var
