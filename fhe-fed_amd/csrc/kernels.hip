@@ -1784,7 +1784,9 @@ void launch_encrypt(const Params& p, const DeviceTables& dt, const DeviceKeys& d
   // call is latency-bound and one launch over every tower (all reduced) is faster: K = 4 / 16 / 64 / 128
   // encrypt 18.7 / 6.5 / 3.67 / 3.23 vs 21.2 / 6.9 / 3.76 / 3.28 us/ct, K = 256 2.92 vs 2.88
   // (profiles/r05zc/nored_k.txt; tests/test_gpu_switches.py checks both paths bit for bit at K = 200)
-  if (!pp || !sw.enc_nored || K < kEncNoredMinK) t_split = p.L;
+  // At 2^16 (nlogR = 5, X5 columns) the split is slower at every K measured: K = 256 / 512 encrypt 8.91 / 8.50
+  // us/ct in one reduced launch vs 9.00 / 8.74 split, while 2^15 K = 714 gains 2.75 vs 2.88 (profiles/r06f/nr_*)
+  if (!pp || !sw.enc_nored || K < kEncNoredMinK || nlogR == 5) t_split = p.L;
   bool vt = false;  // NTT(v)'s columns pass as enc_vtab sums in the blocks pass (round 5)
   if (fused) {
     // 2+3a. encode + sampling + columns pass of v, m + e0, e1 for every tower
