@@ -120,7 +120,7 @@ def parse():
     ap.add_argument("--f4-cts", type=int, default=256,
                     help="ciphertext pairs for the §8 f4 sample (EvalMult + relinearization, ModReduce; "
                          "rank 0, 2^15/L4 workloads); 0 = skip")
-    ap.add_argument("--f4-counters-json", default=os.path.join(ROOT, "profiles", "r05_f4_counters.json"),
+    ap.add_argument("--f4-counters-json", default=os.path.join(ROOT, "profiles", "r06_f4_counters.json"),
                     help="PMC VALU instructions and HBM bytes per ciphertext of one EvalMult / ModReduce "
                          "(tools/profile_f4.sh)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "wavg_traffic.json"),
