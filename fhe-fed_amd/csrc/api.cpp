@@ -676,6 +676,11 @@ void reload_switches() {
 }
 const Switches& switches() { return *g_switches.load(std::memory_order_acquire); }
 static const bool g_switches_read = (reload_switches(), true);
+// SHELFI_STAGE_TRACE=1 (host_stage.cpp's trace switch): the bytes-API aggregation also prints its call split
+static const bool g_stage_trace = [] {
+  const char* e = std::getenv("SHELFI_STAGE_TRACE");
+  return e && std::atoi(e) != 0;
+}();
 
 }  // namespace shelfi
 
@@ -1621,9 +1626,12 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
       make_output(ctx, fmt, 0, 2, 0, scale, out, &total);
       return;
     }
+    using clk = std::chrono::steady_clock;
+    const auto t_in = clk::now();
     check_weights(weights, C, ctx->p.delta);
     DeviceGuard g(ctx->device);
     const std::vector<CtLayout> in = wavg_inputs(ctx, blobs, lens, C);
+    const auto t_parsed = clk::now();
     const CtLayout& h0 = in.front();
     // EvalMult by a constant (ckks.cpp:288): depth + 1, scale * Delta, same level
     const uint32_t depth = h0.depth + 1;
@@ -1637,8 +1645,16 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     // residues first (the parallel drains first-touch the fresh pages), framing after
     CtLayout dst = make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, nullptr, &total);
     dst.base = out;
+    const auto t_pipe = clk::now();
     if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst, lens);
+    const auto t_done = clk::now();
     make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, out, &total);
+    if (g_stage_trace) {
+      const auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
+      std::fprintf(stderr, "[wavg-call] parse %.3f ms, setup %.3f, pipeline %.3f, framing %.3f, total %.3f\n",
+                   ms(t_in, t_parsed), ms(t_parsed, t_pipe), ms(t_pipe, t_done), ms(t_done, clk::now()),
+                   ms(t_in, clk::now()));
+    }
   });
 }
 
