@@ -28,6 +28,7 @@ def main():
         for r in range(5):
             for s in (sizes if r % 2 == 0 else sizes[::-1]):
                 os.environ["SHELFI_WAVG_CHUNK_MIB"] = str(s)
+                m.reload_switches()  # re-read on request only (never on a launch path)
                 ck.computeWeightedAverage(blobs, w)  # warm for this size
                 t0 = time.perf_counter()
                 out = ck.computeWeightedAverage(blobs, w)

@@ -33,6 +33,7 @@ def main():
         for r in range(4):
             for v in ("1", "0") if r % 2 else ("0", "1"):
                 os.environ["SHELFI_ARENA_STAGER"] = v
+                m.reload_switches()  # re-read on request only (never on a launch path)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 ar.put(0, b)

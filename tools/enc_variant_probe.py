@@ -33,6 +33,7 @@ def main():
     for rep in range(int(os.environ.get("REPS", "3"))):
         for v in (vals if rep % 2 == 0 else vals[::-1]):
             os.environ[var] = v
+            m.reload_switches()  # re-read on request only (never on a launch path)
             ck.set_seed(11)
             out = D.encrypt(ck, x)  # warm (allocations)
             torch.cuda.synchronize()

@@ -1,4 +1,4 @@
-"""A/B of packed-arena wavg variants selected by an environment switch read per launch
+"""A/B of packed-arena wavg variants selected by an environment switch (re-read by the library at each switch)
 (AB_ENV, default SHELFI_PACK_UNROLL; AB_VARIANTS, comma-separated values) on the BASELINE
 shapes, in one process on one box: launches alternate between the variants in rounds, HIP
 events around each round, outputs compared bit for bit.  Prints achieved TB/s (the packed
@@ -39,11 +39,13 @@ def set_variant(v):
         os.environ.pop(k, None)
     _SET.clear()
     if not v:
+        m.reload_switches()
         return
     pairs = [p.split("=", 1) for p in v.split("+")] if "=" in v else [(ENV, v)]
     for k, val in pairs:
         os.environ[k] = val
         _SET.add(k)
+    m.reload_switches()  # switches are re-read on request only (never on a launch path)
 
 
 def main():

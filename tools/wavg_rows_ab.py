@@ -59,6 +59,7 @@ def main():
         for r in range(rounds):
             for v in VARIANTS if r % 2 == 0 else VARIANTS[::-1]:
                 os.environ["SHELFI_WAVG_ROWS"] = v
+                m.reload_switches()  # re-read on request only (never on a launch path)
                 ar.wavg(w, out=out)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
