@@ -24,6 +24,7 @@ SHAPES = [  # name, batch, multDepth, C, K
     ("cfg5 8x156", 16384, 3, 8, 156),
     ("cfg3 16x714", 16384, 3, 16, 714),
     ("cfg4 16x32", 32768, 5, 16, 32),
+    ("cfg4big 16x256", 32768, 5, 16, 256),  # cfg4's ring at cfg3's launch size (ramp / tail vs shape)
     ("N8-cts 128x89", 16384, 3, 128, 89),
 ]
 ENV = os.environ.get("AB_ENV", "SHELFI_PACK_UNROLL")
