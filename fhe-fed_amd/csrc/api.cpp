@@ -657,6 +657,7 @@ void reload_switches() {
   s.enc_ts = env_choice("SHELFI_ENC_TS", {0, 1}, -1);
   s.dec_all_towers = env_flag("SHELFI_DEC_ALL_TOWERS", '1', false);
   s.enc_x5 = env_flag("SHELFI_ENC_X5", '0', true);
+  s.stage_trace = env_choice("SHELFI_STAGE_TRACE", {0, 1}, 0) == 1;
   if (const char* e = getenv("SHELFI_PACK_KERNEL")) s.pack_kernel = !strcmp(e, "v4") ? 4 : !strcmp(e, "r3") ? 3 : 0;
   s.pack_unroll = env_choice("SHELFI_PACK_UNROLL", {1, 2, 4, 8}, 0);
   s.pack_waves = env_choice("SHELFI_PACK_WAVES", {2, 8}, 0);
@@ -676,11 +677,6 @@ void reload_switches() {
 }
 const Switches& switches() { return *g_switches.load(std::memory_order_acquire); }
 static const bool g_switches_read = (reload_switches(), true);
-// SHELFI_STAGE_TRACE=1 (host_stage.cpp's trace switch): the bytes-API aggregation also prints its call split
-static const bool g_stage_trace = [] {
-  const char* e = std::getenv("SHELFI_STAGE_TRACE");
-  return e && std::atoi(e) != 0;
-}();
 
 }  // namespace shelfi
 
@@ -1649,7 +1645,7 @@ int shelfi_weighted_average_into(shelfi_ctx* ctx, const uint8_t* const* blobs, c
     if (h0.K) wavg_bytes_pipeline(ctx, in, weights, C, h0.K, dst, lens);
     const auto t_done = clk::now();
     make_output(ctx, h0.fmt(), h0.K, depth, h0.level, scale, out, &total);
-    if (g_stage_trace) {
+    if (switches().stage_trace) {
       const auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
       std::fprintf(stderr, "[wavg-call] parse %.3f ms, setup %.3f, pipeline %.3f, framing %.3f, total %.3f\n",
                    ms(t_in, t_parsed), ms(t_parsed, t_pipe), ms(t_pipe, t_done), ms(t_done, clk::now()),

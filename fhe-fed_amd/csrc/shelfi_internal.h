@@ -71,6 +71,7 @@ struct Switches {
   bool enc_vt = true;          // SHELFI_ENC_VT=0: v's columns pass in enc_cols_fused, not enc_vtab sums
   int enc_ts = -1;             // SHELFI_ENC_TS=0|1: enc_cols_fused's one-wave-per-tower form (-1: by K)
   bool dec_all_towers = false; // SHELFI_DEC_ALL_TOWERS=1: decode over every tower
+  bool stage_trace = false;    // SHELFI_STAGE_TRACE=1: the bytes-API aggregation prints its call split
   bool enc_x5 = true;          // SHELFI_ENC_X5=0: nlogR = 5 encrypt through enc_prep_kernel + three column passes
   int pack_kernel = 0;         // SHELFI_PACK_KERNEL=r3|v4 (0: by shape)
   int pack_unroll = 0;         // SHELFI_PACK_UNROLL=1|2|4|8 (0: by shape)
